@@ -1,0 +1,161 @@
+"""Headline benchmark: consensus updates/sec (N oracles x D dims, batched) at 1/2/4/8 MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5] [--batch B]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Configs (BASELINE.json):
+  c3 (default): 256 oracles x 4096 dims, streaming updates with failing-oracle masking, DP over
+      independent instances.  One step on every rank = a batch of fresh predictions from 1/4 of the
+      oracles of every local instance (synthetic stream, pre-generated in HBM, cycled) scattered into
+      the state + one full two-pass consensus round per instance (fused HIP kernel) + an RCCL
+      all-reduce of the step's health metrics (reliability sum, OK count).
+  c2: 64 oracles x 1024 dims, 10k instances per GPU, one full consensus round per instance per step.
+Weak scaling: per-GPU instances are fixed; ``value`` is the whole-job consensus rounds per second.
+Synthetic data (Beta(20,20) honest oracles, U(0,1) failing), random state, bf16 storage / fp32 math.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    "c3": dict(model="svoc-consensus N=256 D=4096 streaming (f=32, constrained)", N=256, D=4096, f=32,
+               batch=1024, update_frac=0.25),
+    "c2": dict(model="svoc-consensus N=64 D=1024 batched (f=8, constrained)", N=64, D=1024, f=8,
+               batch=10000, update_frac=0.0),
+}
+METRIC = "consensus updates/sec (N oracles x D dims, batched)"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="instances per GPU (default per config)")
+    ap.add_argument("--wave-hint", type=int, default=0)
+    ap.add_argument("--graph", type=int, default=1, help="capture the step in a HIP graph")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    from svoc.parallel.dp import DataParallelConsensus
+
+    c = CONFIGS[args.config]
+    B = args.batch or c["batch"]
+    cfg = ConsensusConfig(n_oracles=c["N"], dimension=c["D"], n_failing_oracles=c["f"], constrained=True)
+    eng = ConsensusEngine(cfg, batch=B, device=dev, mode="fast")
+    eng.wave_hint = args.wave_hint
+    dp = DataParallelConsensus(eng, rank=rank, world=world)
+    eng.randomize(seed=1000 + rank)
+
+    # synthetic update stream resident in HBM: `pool` steps of updates, cycled
+    U_per_inst = int(round(c["update_frac"] * c["N"]))
+    stream = None
+    if U_per_inst:
+        from svoc.stream import SyntheticUpdateStream
+        stream = SyntheticUpdateStream(B, c["N"], c["D"], U_per_inst, c["f"], pool=2, device=dev, seed=rank)
+
+    def step(i):  # device-only work (capturable)
+        if stream is not None:
+            inst, orc, vals = stream.batch(i)
+            eng.apply_updates(inst, orc, vals)
+            eng.run_round(only_touched=True)
+        else:
+            eng.touched.fill_(1)
+            eng.run_round(only_touched=True)
+        dp.accumulate()
+
+    for i in range(args.warmup):
+        step(i)
+        dp.reduce()
+    torch.cuda.synchronize(dev)
+
+    graph = None
+    if args.graph:
+        # the stream cycles with period `pool`: capture one period and replay it
+        period = stream.pool if stream is not None else 1
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for i in range(period):
+                step(i)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        try:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for i in range(period):
+                    step(i)
+            graph_period = period
+        except Exception as e:  # graph capture is an optimisation; eager stays correct
+            if rank == 0:
+                print(f"[bench] graph capture failed ({e}); running eager", file=sys.stderr)
+            graph = None
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    if graph is not None:
+        reps, rem = divmod(args.steps, graph_period)
+        for _ in range(reps):
+            graph.replay()
+            dp.reduce()            # one RCCL all-reduce of the step metrics per replay
+        for i in range(rem):       # exactly K steps: the tail of a period runs eagerly
+            step(i)
+            dp.reduce()
+        steps_done = args.steps
+    else:
+        for i in range(args.steps):
+            step(i)
+            dp.reduce()
+        steps_done = args.steps
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    el = float(elapsed.item())
+    ms_per_step = 1e3 * el / steps_done
+    rounds = B * world * steps_done
+    value = rounds / el
+    ok = dp.global_ok_fraction()
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": value, "unit": "consensus rounds/s", "n_gpus": world,
+            "steps": steps_done, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"model": c["model"], "global_batch": B * world, "seq_len": c["D"],
+                       "parallelism": f"dp{world}", "n_oracles": c["N"], "dimension": c["D"],
+                       "n_failing": c["f"], "updates_per_instance_per_step": U_per_inst,
+                       "oracle_updates_per_s": (U_per_inst * rounds / el) if U_per_inst else 0.0,
+                       "hip_graph": graph is not None, "ok_fraction": ok},
+        }
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

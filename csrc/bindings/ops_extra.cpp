@@ -1,0 +1,132 @@
+// Extra torch.ops.svoc ops: batched updates (storage half of update_prediction).
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <cstring>
+
+#include "svoc/launch.hpp"
+#include "svoc/ops.hpp"
+#include "svoc/status.hpp"
+
+namespace svoc {
+namespace {
+
+int dtype_code(at::ScalarType t) {
+  if (t == at::kBFloat16) return 0;
+  if (t == at::kFloat) return 1;
+  if (t == at::kLong) return 2;
+  TORCH_CHECK(false, "values dtype must be bf16, fp32 or int64 (wsad)");
+  return -1;
+}
+
+UpdateParams make_update_params(at::Tensor& values, at::Tensor& enabled, at::Tensor& n_active,
+                                at::Tensor& touched, const at::Tensor& inst, const at::Tensor& oracle,
+                                const at::Tensor& upd, bool constrained, at::Tensor& upd_status) {
+  TORCH_CHECK(values.dim() == 3 && values.stride(2) == 1 && values.stride(1) == values.size(2),
+              "values: [B, N, ld] with dense rows");
+  const int64_t B = values.size(0), N = values.size(1), U = inst.numel();
+  TORCH_CHECK(upd.dim() == 2 && upd.size(0) == U && upd.is_contiguous(), "upd: contiguous [U, D]");
+  TORCH_CHECK(upd.scalar_type() == values.scalar_type(), "upd dtype must match values");
+  TORCH_CHECK(upd.size(1) <= values.size(2), "D > ld");
+  TORCH_CHECK(oracle.numel() == U && inst.scalar_type() == at::kLong && oracle.scalar_type() == at::kLong,
+              "inst/oracle: int64 [U]");
+  TORCH_CHECK(inst.is_contiguous() && oracle.is_contiguous(), "inst/oracle contiguous");
+  TORCH_CHECK(enabled.scalar_type() == at::kByte && enabled.numel() == B * N && enabled.is_contiguous(),
+              "enabled: uint8 [B, N]");
+  TORCH_CHECK(n_active.scalar_type() == at::kInt && n_active.numel() == B && n_active.is_contiguous(),
+              "n_active: int32 [B]");
+  TORCH_CHECK(touched.scalar_type() == at::kByte && touched.numel() == B, "touched: uint8 [B]");
+  TORCH_CHECK(upd_status.scalar_type() == at::kInt && upd_status.numel() == U, "upd_status: int32 [U]");
+  UpdateParams p{};
+  p.values = values.data_ptr();
+  p.enabled = enabled.data_ptr<uint8_t>();
+  p.n_active = n_active.data_ptr<int32_t>();
+  p.touched = touched.data_ptr<uint8_t>();
+  p.inst = inst.data_ptr<int64_t>();
+  p.oracle = oracle.data_ptr<int64_t>();
+  p.upd = upd.data_ptr();
+  p.upd_status = upd_status.data_ptr<int32_t>();
+  p.inst_stride = values.stride(0);
+  p.B = (int)B; p.N = (int)N; p.D = (int)upd.size(1); p.ld = (int)values.size(2); p.U = (int)U;
+  p.dtype = dtype_code(values.scalar_type());
+  p.elem_bytes = (int)values.element_size();
+  p.constrained = constrained ? 1 : 0;
+  return p;
+}
+
+bool in_range_cpu(const UpdateParams& p, int64_t u, int d) {
+  if (p.dtype == 0) {
+    uint32_t w = (uint32_t)((const uint16_t*)p.upd)[u * p.D + d] << 16;
+    float f;
+    std::memcpy(&f, &w, 4);
+    return f >= 0.f && f <= 1.f;
+  }
+  if (p.dtype == 1) {
+    const float f = ((const float*)p.upd)[u * p.D + d];
+    return f >= 0.f && f <= 1.f;
+  }
+  const int64_t v = ((const int64_t*)p.upd)[u * p.D + d];
+  return v >= 0 && v <= 1000000;
+}
+
+void apply_updates_cpu(at::Tensor values, at::Tensor enabled, at::Tensor n_active, at::Tensor touched,
+                       at::Tensor winner, const at::Tensor& inst, const at::Tensor& oracle, const at::Tensor& upd,
+                       bool constrained, at::Tensor upd_status) {
+  (void)winner;
+  UpdateParams p = make_update_params(values, enabled, n_active, touched, inst, oracle, upd, constrained, upd_status);
+  const int64_t row_bytes = (int64_t)p.D * p.elem_bytes;
+  for (int64_t u = 0; u < p.U; ++u) {  // sequential = last writer wins
+    const int64_t b = p.inst[u], o = p.oracle[u];
+    int st = ST_OK;
+    if (b < 0 || b >= p.B || o < 0 || o >= p.N) st = ST_NOT_ORACLE;
+    if (st == ST_OK && p.constrained)
+      for (int d = 0; d < p.D; ++d)
+        if (!in_range_cpu(p, u, d)) { st = ST_INTERVAL_INPUT; break; }
+    p.upd_status[u] = st;
+    if (st != ST_OK) continue;
+    std::memcpy((unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes,
+                (const unsigned char*)p.upd + u * row_bytes, row_bytes);
+    if (!p.enabled[b * p.N + o]) {
+      p.enabled[b * p.N + o] = 1;
+      p.n_active[b] += 1;
+    }
+    p.touched[b] = 1;
+  }
+}
+
+void apply_updates_hip(at::Tensor values, at::Tensor enabled, at::Tensor n_active, at::Tensor touched,
+                       at::Tensor winner, const at::Tensor& inst, const at::Tensor& oracle, const at::Tensor& upd,
+                       bool constrained, at::Tensor upd_status) {
+  UpdateParams p = make_update_params(values, enabled, n_active, touched, inst, oracle, upd, constrained, upd_status);
+  TORCH_CHECK(winner.scalar_type() == at::kInt && winner.numel() == (int64_t)p.B * p.N && winner.is_contiguous(),
+              "winner workspace: int32 [B, N] filled with -1");
+  p.winner = winner.data_ptr<int32_t>();
+  auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
+  const int rc = svoc_apply_updates(&p, stream);
+  TORCH_CHECK(rc == 0, "svoc_apply_updates failed: ", rc);
+}
+
+}  // namespace
+
+void register_extra_defs(torch::Library& m) {
+  m.def(
+      "apply_updates(Tensor(a!) values, Tensor(b!) enabled, Tensor(c!) n_active, Tensor(d!) touched, "
+      "Tensor(e!) winner, Tensor inst, Tensor oracle, Tensor upd, bool constrained, Tensor(f!) upd_status) -> ()");
+  register_governance_defs(m);
+  register_generator_defs(m);
+}
+
+void register_extra_cpu(torch::Library& m) {
+  m.impl("apply_updates", &apply_updates_cpu);
+  register_governance_cpu(m);
+  register_generator_cpu(m);
+}
+
+void register_extra_hip(torch::Library& m) {
+  m.impl("apply_updates", &apply_updates_hip);
+  register_governance_hip(m);
+  register_generator_hip(m);
+}
+
+}  // namespace svoc

@@ -1,0 +1,226 @@
+// torch.ops.svoc.* registration.  CPU kernels = the golden C++ engines (reference_cpu.cpp);
+// CUDA (= HIP on ROCm) kernels = the hand-written gfx950 kernels in csrc/kernels/*.hip.
+// All ops write into caller-provided outputs ("out" semantics) so the Python engine owns the state
+// tensors and can capture steady-state steps in HIP graphs.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <thread>
+
+#include "../engine/engine.hpp"
+#include "svoc/launch.hpp"
+#include "svoc/ops.hpp"
+
+namespace svoc {
+namespace {
+
+int cpu_threads() {
+  static int n = [] {
+    unsigned h = std::thread::hardware_concurrency();
+    return (int)(h == 0 ? 1 : (h > 32 ? 32 : h));
+  }();
+  return n;
+}
+
+void check_out(const at::Tensor& t, at::ScalarType dt, std::initializer_list<int64_t> shape, const char* name,
+               const at::Device& dev) {
+  TORCH_CHECK(t.scalar_type() == dt, name, ": wrong dtype ", t.scalar_type());
+  TORCH_CHECK(t.device() == dev, name, ": wrong device");
+  TORCH_CHECK(t.is_contiguous(), name, ": must be contiguous");
+  TORCH_CHECK(t.sizes().vec() == std::vector<int64_t>(shape), name, ": wrong shape ", t.sizes());
+}
+
+const uint8_t* active_ptr(const c10::optional<at::Tensor>& active, int64_t B, const at::Device& dev) {
+  if (!active.has_value()) return nullptr;
+  const auto& a = *active;
+  TORCH_CHECK(a.scalar_type() == at::kByte || a.scalar_type() == at::kBool, "active: uint8/bool");
+  TORCH_CHECK(a.numel() == B && a.is_contiguous() && a.device() == dev, "active: [B] contiguous");
+  return (const uint8_t*)a.data_ptr();
+}
+
+// --------------------------------------------------------------------------------------- fast
+void fast_round_checks(const at::Tensor& values, int64_t D, const at::Tensor& c1, const at::Tensor& cons,
+                       const at::Tensor& skew, const at::Tensor& kurt, const at::Tensor& rel,
+                       const at::Tensor& qr, const at::Tensor& reliable, const at::Tensor& status) {
+  TORCH_CHECK(values.dim() == 3, "values: [B, N, ld]");
+  TORCH_CHECK(values.stride(2) == 1 && values.stride(1) == values.size(2), "values: rows must be dense");
+  const int64_t B = values.size(0), N = values.size(1);
+  TORCH_CHECK(D >= 1 && D <= values.size(2), "D must be <= ld");
+  const auto dev = values.device();
+  check_out(c1, at::kFloat, {B, D}, "c1", dev);
+  check_out(cons, at::kFloat, {B, D}, "consensus", dev);
+  check_out(skew, at::kFloat, {B, D}, "skew", dev);
+  check_out(kurt, at::kFloat, {B, D}, "kurt", dev);
+  check_out(rel, at::kFloat, {B, 2}, "rel", dev);
+  check_out(qr, at::kFloat, {B, N}, "qr", dev);
+  check_out(reliable, at::kByte, {B, N}, "reliable", dev);
+  check_out(status, at::kInt, {B}, "status", dev);
+}
+
+void fast_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t D,
+                    int64_t n_failing, bool constrained, double max_spread, at::Tensor c1, at::Tensor cons,
+                    at::Tensor skew, at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable,
+                    at::Tensor status, int64_t wave_hint) {
+  (void)wave_hint;
+  fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
+  const int64_t B = values.size(0), N = values.size(1), ld = values.size(2), is = values.stride(0);
+  TORCH_CHECK(values.scalar_type() == at::kBFloat16 || values.scalar_type() == at::kFloat,
+              "values: bf16 or fp32");
+  FastBatch fb;
+  fb.values = values.data_ptr();
+  const bool bf = values.scalar_type() == at::kBFloat16;
+  fb.load = [=](const void* base, int64_t i, float* dst) {
+    for (int64_t r = 0; r < N; ++r)
+      for (int64_t d = 0; d < D; ++d) {
+        const int64_t o = i * is + r * ld + d;
+        if (bf) {
+          uint32_t w = (uint32_t)((const uint16_t*)base)[o] << 16;
+          float f;
+          std::memcpy(&f, &w, 4);
+          dst[r * D + d] = f;
+        } else {
+          dst[r * D + d] = ((const float*)base)[o];
+        }
+      }
+  };
+  fb.active = active_ptr(active, B, values.device());
+  fb.B = B; fb.N = N; fb.D = D;
+  fb.n_failing = n_failing;
+  fb.constrained = constrained;
+  fb.max_spread = (float)max_spread;
+  fb.c1 = c1.data_ptr<float>();
+  fb.consensus = cons.data_ptr<float>();
+  fb.rel = rel.data_ptr<float>();
+  fb.skew = skew.data_ptr<float>();
+  fb.kurt = kurt.data_ptr<float>();
+  fb.reliable = reliable.data_ptr<uint8_t>();
+  fb.qr = qr.data_ptr<float>();
+  fb.status = status.data_ptr<int32_t>();
+  fast_round_batch_cpu(fb, cpu_threads());
+}
+
+void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t D,
+                    int64_t n_failing, bool constrained, double max_spread, at::Tensor c1, at::Tensor cons,
+                    at::Tensor skew, at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable,
+                    at::Tensor status, int64_t wave_hint) {
+  fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
+  TORCH_CHECK(values.scalar_type() == at::kBFloat16, "GPU fast path stores values in bf16");
+  const int64_t B = values.size(0), N = values.size(1), ld = values.size(2);
+  TORCH_CHECK(N >= 2 && N <= 256, "GPU fast path supports 2 <= N <= 256 oracles");
+  TORCH_CHECK(ld % 8 == 0, "row stride (ld) must be a multiple of 8 bf16 (16 B)");
+  TORCH_CHECK(((uintptr_t)values.data_ptr() & 15) == 0 && values.stride(0) % 8 == 0, "values must be 16-B aligned");
+  TORCH_CHECK(B < (1ll << 31) && D < (1 << 30), "size limits");
+  FastParams p{};
+  p.values = values.data_ptr();
+  p.active = active_ptr(active, B, values.device());
+  p.inst_stride = values.stride(0);
+  p.B = (int)B; p.N = (int)N; p.D = (int)D; p.ld = (int)ld;
+  p.n_failing = (int)n_failing;
+  p.constrained = constrained ? 1 : 0;
+  p.max_spread = (float)max_spread;
+  p.wave_hint = (int)wave_hint;
+  p.c1 = c1.data_ptr<float>();
+  p.consensus = cons.data_ptr<float>();
+  p.skew = skew.data_ptr<float>();
+  p.kurt = kurt.data_ptr<float>();
+  p.rel = rel.data_ptr<float>();
+  p.qr = qr.data_ptr<float>();
+  p.reliable = reliable.data_ptr<uint8_t>();
+  p.status = status.data_ptr<int32_t>();
+  auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
+  const int rc = svoc_fast_round_bf16(&p, stream);
+  TORCH_CHECK(rc == 0, "svoc_fast_round_bf16 launch failed: ", rc);
+}
+
+// -------------------------------------------------------------------------------------- exact
+void exact_checks(const at::Tensor& values, const at::Tensor& c1, const at::Tensor& cons, const at::Tensor& skew,
+                  const at::Tensor& kurt, const at::Tensor& rel, const at::Tensor& qr, const at::Tensor& reliable,
+                  const at::Tensor& status) {
+  TORCH_CHECK(values.dim() == 3 && values.scalar_type() == at::kLong && values.is_contiguous(),
+              "values: contiguous int64 [B, N, D] wsad");
+  const int64_t B = values.size(0), N = values.size(1), D = values.size(2);
+  const auto dev = values.device();
+  check_out(c1, at::kLong, {B, D}, "c1", dev);
+  check_out(cons, at::kLong, {B, D}, "consensus", dev);
+  check_out(skew, at::kLong, {B, D}, "skew", dev);
+  check_out(kurt, at::kLong, {B, D}, "kurt", dev);
+  check_out(rel, at::kLong, {B, 2}, "rel", dev);
+  check_out(qr, at::kLong, {B, N}, "qr", dev);
+  check_out(reliable, at::kByte, {B, N}, "reliable", dev);
+  check_out(status, at::kInt, {B}, "status", dev);
+}
+
+void exact_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t n_failing,
+                     bool constrained, int64_t max_spread, at::Tensor c1, at::Tensor cons, at::Tensor skew,
+                     at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable, at::Tensor status) {
+  exact_checks(values, c1, cons, skew, kurt, rel, qr, reliable, status);
+  ExactBatch eb{};
+  eb.values = values.data_ptr<int64_t>();
+  eb.B = values.size(0); eb.N = values.size(1); eb.D = values.size(2);
+  eb.active = active_ptr(active, eb.B, values.device());
+  eb.n_failing = n_failing;
+  eb.constrained = constrained;
+  eb.max_spread = max_spread;
+  eb.consensus = cons.data_ptr<int64_t>();
+  eb.rel = rel.data_ptr<int64_t>();
+  eb.skew = skew.data_ptr<int64_t>();
+  eb.kurt = kurt.data_ptr<int64_t>();
+  eb.reliable = reliable.data_ptr<uint8_t>();
+  eb.qr = qr.data_ptr<int64_t>();
+  eb.c1 = c1.data_ptr<int64_t>();
+  eb.status = status.data_ptr<int32_t>();
+  exact_round_batch_cpu(eb, cpu_threads());
+}
+
+void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t n_failing,
+                     bool constrained, int64_t max_spread, at::Tensor c1, at::Tensor cons, at::Tensor skew,
+                     at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable, at::Tensor status) {
+  exact_checks(values, c1, cons, skew, kurt, rel, qr, reliable, status);
+  ExactParams p{};
+  p.values = values.data_ptr<int64_t>();
+  p.B = (int)values.size(0); p.N = (int)values.size(1); p.D = (int)values.size(2);
+  TORCH_CHECK(p.N >= 1 && p.N <= 256, "GPU exact path supports N <= 256");
+  p.active = active_ptr(active, p.B, values.device());
+  p.n_failing = (int)n_failing;
+  p.constrained = constrained ? 1 : 0;
+  p.max_spread = max_spread;
+  p.c1 = c1.data_ptr<int64_t>();
+  p.consensus = cons.data_ptr<int64_t>();
+  p.skew = skew.data_ptr<int64_t>();
+  p.kurt = kurt.data_ptr<int64_t>();
+  p.rel = rel.data_ptr<int64_t>();
+  p.qr = qr.data_ptr<int64_t>();
+  p.reliable = reliable.data_ptr<uint8_t>();
+  p.status = status.data_ptr<int32_t>();
+  auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
+  const int rc = svoc_exact_round(&p, stream);
+  TORCH_CHECK(rc == 0, "svoc_exact_round launch failed: ", rc);
+}
+
+}  // namespace
+}  // namespace svoc
+
+TORCH_LIBRARY(svoc, m) {
+  m.def(
+      "fast_round(Tensor values, Tensor? active, int D, int n_failing, bool constrained, float max_spread, "
+      "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "
+      "Tensor(g!) reliable, Tensor(h!) status, int wave_hint=0) -> ()");
+  m.def(
+      "exact_round(Tensor values, Tensor? active, int n_failing, bool constrained, int max_spread, "
+      "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "
+      "Tensor(g!) reliable, Tensor(h!) status) -> ()");
+  svoc::register_extra_defs(m);
+}
+
+TORCH_LIBRARY_IMPL(svoc, CPU, m) {
+  m.impl("fast_round", &svoc::fast_round_cpu);
+  m.impl("exact_round", &svoc::exact_round_cpu);
+  svoc::register_extra_cpu(m);
+}
+
+TORCH_LIBRARY_IMPL(svoc, CUDA, m) {
+  m.impl("fast_round", &svoc::fast_round_hip);
+  m.impl("exact_round", &svoc::exact_round_hip);
+  svoc::register_extra_hip(m);
+}

@@ -1,0 +1,76 @@
+// Launch descriptors shared by the HIP kernels and the torch bindings (plain C structs, passed by
+// value as kernel arguments).
+#pragma once
+
+#include <stdint.h>
+
+namespace svoc {
+
+struct FastParams {
+  const void* values;       // [B, N, ld] bf16 (instance stride inst_stride elements)
+  const uint8_t* active;    // [B] or null
+  int64_t inst_stride;
+  int B, N, D, ld;
+  int n_failing;
+  int constrained;
+  float max_spread;
+  int wave_hint;            // 0 = auto, 8 = force the 8-wave single-slab variant for N <= 64
+  float* c1;                // [B, D]
+  float* consensus;         // [B, D]
+  float* skew;              // [B, D]
+  float* kurt;              // [B, D]
+  float* rel;               // [B, 2]
+  float* qr;                // [B, N]
+  uint8_t* reliable;        // [B, N]
+  int32_t* status;          // [B]
+};
+
+struct ExactParams {
+  const int64_t* values;    // [B, N, D] wsad
+  const uint8_t* active;    // [B] or null
+  int B, N, D;
+  int n_failing;
+  int constrained;
+  int64_t max_spread;
+  int64_t* c1;              // [B, D]
+  int64_t* consensus;       // [B, D]
+  int64_t* skew;            // [B, D]
+  int64_t* kurt;            // [B, D]
+  int64_t* rel;             // [B, 2]
+  int64_t* qr;              // [B, N]
+  uint8_t* reliable;        // [B, N]
+  int32_t* status;          // [B]
+};
+
+}  // namespace svoc
+
+extern "C" {
+typedef struct ihipStream_t* hipStream_t;
+int svoc_fast_round_bf16(const svoc::FastParams* p, hipStream_t stream);
+int svoc_exact_round(const svoc::ExactParams* p, hipStream_t stream);
+}
+
+namespace svoc {
+
+// Batched oracle updates (update_prediction's storage half, contract.cairo:331-343 + the input
+// interval check of :591-593), last-writer-wins per (instance, oracle) within one batch.
+struct UpdateParams {
+  void* values;             // [B, N, ld] (elem_bytes each)
+  uint8_t* enabled;         // [B, N]
+  int32_t* n_active;        // [B]
+  uint8_t* touched;         // [B]
+  int32_t* winner;          // [B, N] workspace, -1 when idle (restored by the launch)
+  const int64_t* inst;      // [U]
+  const int64_t* oracle;    // [U]
+  const void* upd;          // [U, D] same dtype as values
+  int32_t* upd_status;      // [U]
+  int64_t inst_stride;      // elements
+  int B, N, D, ld, U;
+  int elem_bytes;           // 2 (bf16), 4 (fp32) or 8 (int64 wsad)
+  int dtype;                // 0 bf16, 1 fp32, 2 int64
+  int constrained;
+};
+
+}  // namespace svoc
+
+extern "C" int svoc_apply_updates(const svoc::UpdateParams* p, hipStream_t stream);

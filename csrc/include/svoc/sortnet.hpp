@@ -1,0 +1,163 @@
+// Register-resident sorting networks for per-column order statistics on CDNA4 (wave64).
+//
+// Layout ("lane groups"): a column pair (two adjacent bf16 columns packed in one 32-bit VGPR as
+// u16x2 sort keys) is owned by NSEG lanes; lane `seg` of the group holds rows [64*seg, 64*seg+64)
+// of both columns in 64 VGPRs.  Intra-lane stages are pure VALU (v_pk_min_u16 / v_pk_max_u16 sort
+// two columns per instruction); cross-lane stages exchange whole registers with the partner lane
+// (lane ^ m*P, where P = 64/NSEG is the number of column pairs per wave).
+//
+// The network is the "flip + half-cleaner" form of bitonic sort, so every run stays ascending:
+//   sort64 (21 stages) inside each lane, then for run size s = 2..NSEG segments:
+//   flip across lanes seg ^ (s-1) with index reversal, half-cleaners across lanes for strides
+//   s/4..1 segments, then the 6 intra-lane half-cleaner stages.
+// Replaces the reference's per-column MergeSort (math.cairo:113-126 via alexandria MergeSort):
+// only the order statistics' VALUES matter for the smooth median, so a data-oblivious network is
+// exact.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace svoc {
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+
+#define SVOC_DEV __device__ __forceinline__
+
+SVOC_DEV u16x2 kmin(u16x2 a, u16x2 b) { return __builtin_elementwise_min(a, b); }
+SVOC_DEV u16x2 kmax(u16x2 a, u16x2 b) { return __builtin_elementwise_max(a, b); }
+SVOC_DEV uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+SVOC_DEV u16x2 as_k(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+
+// bf16 bit pattern -> order-preserving unsigned key (and back), two lanes-halves at a time.
+SVOC_DEV u16x2 bf16x2_to_key(uint32_t raw) {
+  u16x2 r = as_k(raw);
+  u16x2 s = __builtin_bit_cast(u16x2, __builtin_bit_cast(s16x2, r) >> (short)15);
+  return r ^ (s | (unsigned short)0x8000);
+}
+SVOC_DEV uint32_t key_to_bf16x2(u16x2 k) {
+  u16x2 nk = ~k;
+  u16x2 s = __builtin_bit_cast(u16x2, __builtin_bit_cast(s16x2, nk) >> (short)15);
+  return as_u32(k ^ (s | (unsigned short)0x8000));
+}
+SVOC_DEV float bf16_lo(uint32_t w) { return __builtin_bit_cast(float, w << 16); }
+SVOC_DEV float bf16_hi(uint32_t w) { return __builtin_bit_cast(float, w & 0xffff0000u); }
+
+SVOC_DEV u16x2 shfl_xor_k(u16x2 v, int m) { return as_k((uint32_t)__shfl_xor((int)as_u32(v), m)); }
+SVOC_DEV u16x2 shfl_k(u16x2 v, int src) { return as_k((uint32_t)__shfl((int)as_u32(v), src)); }
+
+// Full ascending bitonic sort of the 64 registers of one lane (each half independently).
+SVOC_DEV void sort64(u16x2 (&r)[64]) {
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const int l = i ^ j;
+        if (l > i) {
+          const u16x2 a = r[i], b = r[l];
+          if ((i & k) == 0) {
+            r[i] = kmin(a, b);
+            r[l] = kmax(a, b);
+          } else {
+            r[i] = kmax(a, b);
+            r[l] = kmin(a, b);
+          }
+        }
+      }
+    }
+  }
+}
+
+// Ascending half-cleaner cascade (strides 32..1): sorts a bitonic lane-local sequence.
+SVOC_DEV void merge64(u16x2 (&r)[64]) {
+#pragma unroll
+  for (int j = 32; j > 0; j >>= 1) {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      const int l = i ^ j;
+      if (l > i) {
+        const u16x2 a = r[i], b = r[l];
+        r[i] = kmin(a, b);
+        r[l] = kmax(a, b);
+      }
+    }
+  }
+}
+
+// Cross-lane flip: position i meets the partner's position 63-i; lower lane keeps the minima.
+SVOC_DEV void xlane_flip(u16x2 (&r)[64], int xmask, bool upper) {
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const u16x2 a = r[i], b = r[63 - i];
+    const u16x2 pa = shfl_xor_k(b, xmask);  // partner's r[63-i]
+    const u16x2 pb = shfl_xor_k(a, xmask);  // partner's r[i]
+    r[i] = upper ? kmax(a, pa) : kmin(a, pa);
+    r[63 - i] = upper ? kmax(b, pb) : kmin(b, pb);
+  }
+}
+
+// Cross-lane half-cleaner: position i meets the partner's position i.
+SVOC_DEV void xlane_hc(u16x2 (&r)[64], int xmask, bool upper) {
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    const u16x2 a = r[i];
+    const u16x2 p = shfl_xor_k(a, xmask);
+    r[i] = upper ? kmax(a, p) : kmin(a, p);
+  }
+}
+
+// Sort 64*NSEG keys (x2 columns) spread over the NSEG lanes of a group. P = pairs per wave.
+template <int NSEG, int P>
+SVOC_DEV void sort_group(u16x2 (&r)[64], int seg) {
+  sort64(r);
+#pragma unroll
+  for (int s = 2; s <= NSEG; s <<= 1) {
+    xlane_flip(r, (s - 1) * P, (seg & (s >> 1)) != 0);
+#pragma unroll
+    for (int t = s >> 2; t >= 1; t >>= 1) xlane_hc(r, t * P, (seg & t) != 0);
+    merge64(r);
+  }
+}
+
+// Register k (runtime, 0..63) of a lane: a 63-step v_bfi_b32 blend tree.  Written with bit
+// blends, not `?:` -- LLVM folds a select between two array elements into a dynamically indexed
+// load, which demotes the whole register array to scratch.
+SVOC_DEV uint32_t blend(uint32_t a, uint32_t b, uint32_t m) { return (a & ~m) | (b & m); }
+
+SVOC_DEV u16x2 reg_select(const u16x2 (&r)[64], int k) {
+  uint32_t a[32];
+  uint32_t m = 0u - (uint32_t)(k & 1);
+#pragma unroll
+  for (int j = 0; j < 32; ++j) a[j] = blend(as_u32(r[2 * j]), as_u32(r[2 * j + 1]), m);
+  m = 0u - (uint32_t)((k >> 1) & 1);
+#pragma unroll
+  for (int j = 0; j < 16; ++j) a[j] = blend(a[2 * j], a[2 * j + 1], m);
+  m = 0u - (uint32_t)((k >> 2) & 1);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = blend(a[2 * j], a[2 * j + 1], m);
+  m = 0u - (uint32_t)((k >> 3) & 1);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) a[j] = blend(a[2 * j], a[2 * j + 1], m);
+  m = 0u - (uint32_t)((k >> 4) & 1);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) a[j] = blend(a[2 * j], a[2 * j + 1], m);
+  m = 0u - (uint32_t)((k >> 5) & 1);
+  return as_k(blend(a[0], a[1], m));
+}
+
+// Rank `rank` (0-based, runtime) of the group's sorted sequence, broadcast to every group lane.
+template <int NSEG, int P>
+SVOC_DEV u16x2 group_select(const u16x2 (&r)[64], int rank, int lane) {
+  const u16x2 v = reg_select(r, rank & 63);
+  if constexpr (NSEG == 1) {
+    return v;
+  } else {
+    const int owner = (rank >> 6) * P + (lane % P);
+    return shfl_k(v, owner);
+  }
+}
+
+}  // namespace svoc

@@ -1,0 +1,275 @@
+// Bit-exact (wsad, i128 arithmetic) consensus round on the GPU: one wave per instance, lane = oracle
+// row (RPL rows per lane for N > 64), loops over columns.  Every integer operation is the same
+// csrc/include/svoc/wsad.hpp routine the CPU golden engine uses, evaluated in the same stage order
+// (all c1, qr, rel1, rank mask, all consensus, rel2, all means, all variances, all skewness, all
+// kurtosis -- contract/src/contract.cairo:451-500), so the outputs and the first-error status match
+// csrc/engine/reference_cpu.cpp bit for bit.  Per-column intermediates live in LDS; outputs are
+// only written when the whole round succeeds (transaction-revert semantics).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "svoc/launch.hpp"
+#include "svoc/status.hpp"
+#include "svoc/wsad.hpp"
+
+namespace svoc {
+
+__device__ __forceinline__ int64_t shfl64(int64_t v, int src) {
+  const int lo = __shfl((int)(uint32_t)v, src), hi = __shfl((int)(uint32_t)(v >> 32), src);
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ __forceinline__ i128 shfl128(i128 v, int src) {
+  const u128 u = (u128)v;
+  const uint64_t lo = (uint64_t)shfl64((int64_t)(uint64_t)u, src);
+  const uint64_t hi = (uint64_t)shfl64((int64_t)(uint64_t)(u >> 64), src);
+  return (i128)(((u128)hi << 64) | lo);
+}
+
+// wave-wide checked i128 sum in a fixed lane order (0..63) so overflow detection is deterministic.
+__device__ __forceinline__ i128 wave_sum(i128 v, int& st) {
+  i128 acc = 0;
+  for (int l = 0; l < 64; ++l) acc = add(acc, shfl128(v, l), st);
+  return acc;
+}
+
+__device__ __forceinline__ int wave_or(int v) {
+  for (int o = 32; o >= 1; o >>= 1) v |= __shfl_xor(v, o);
+  return v;
+}
+
+template <int RPL>
+struct Rows {
+  int64_t x[RPL];
+  bool on[RPL];  // row exists and takes part
+};
+
+// value of the element of stable rank `k` among the rows with on[] set (k is wave-uniform)
+template <int RPL>
+__device__ i128 rank_value(const Rows<RPL>& r, int lane, int k) {
+  i128 found = 0;
+  int hit = 0;
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    int rank = 0;
+#pragma unroll
+    for (int jj = 0; jj < RPL; ++jj) {
+      for (int l = 0; l < 64; ++l) {
+        const int64_t xk = shfl64(r.x[jj], l);
+        const int onk = __shfl((int)r.on[jj], l);
+        const int idx_k = jj * 64 + l, idx_m = j * 64 + lane;
+        rank += (onk && (xk < r.x[j] || (xk == r.x[j] && idx_k < idx_m))) ? 1 : 0;
+      }
+    }
+    if (r.on[j] && rank == k) { found = r.x[j]; hit = 1; }
+  }
+  int dummy = ST_OK;
+  // exactly one lane holds it
+  i128 v = hit ? found : 0;
+  for (int l = 0; l < 64; ++l) {
+    const int h = __shfl(hit, l);
+    if (h) return shfl128(v, l);
+  }
+  (void)dummy;
+  return 0;
+}
+
+template <int RPL>
+__device__ i128 smooth_median_w(const Rows<RPL>& r, int lane, int count, int& st) {
+  if (count == 0) { fail(st, ST_USIZE_UNDERFLOW); return 0; }
+  if (count == 1) { fail(st, ST_INDEX_OOB); return 0; }
+  const int mid = count / 2;
+  const i128 a = rank_value<RPL>(r, lane, mid - 1), b = rank_value<RPL>(r, lane, mid);
+  return idiv_pos64(add(a, b, st), 2, st);
+}
+
+template <int RPL>
+__global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
+  extern __shared__ __attribute__((aligned(16))) int64_t lds[];
+  const int b = blockIdx.x;
+  if (p.active && !p.active[b]) return;
+  const int lane = threadIdx.x;
+  const int N = p.N, D = p.D;
+  int64_t* c1 = lds;
+  int64_t* cons = lds + D;
+  int64_t* means = lds + 2 * D;
+  int64_t* vars = lds + 3 * D;
+  int64_t* sk = lds + 4 * D;
+  int64_t* ku = lds + 5 * D;
+  const int64_t* X = p.values + (int64_t)b * N * D;
+  int st = ST_OK;  // wave-uniform by construction (every lane runs the same checked reductions)
+
+  Rows<RPL> rows;
+  // ---- pass 1: c1 per column
+  for (int d = 0; d < D && st == ST_OK; ++d) {
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      const int row = j * 64 + lane;
+      rows.on[j] = row < N;
+      rows.x[j] = row < N ? X[(int64_t)row * D + d] : 0;
+    }
+    const i128 c = smooth_median_w<RPL>(rows, lane, N, st);
+    if (lane == 0) c1[d] = (int64_t)c;
+  }
+  __syncthreads();
+  if (st != ST_OK) { if (lane == 0) p.status[b] = st; return; }
+  // quadratic risk per row (lane-local), then the checked mean
+  i128 qr[RPL];
+  int lst = ST_OK;
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int row = j * 64 + lane;
+    i128 acc = 0;
+    if (row < N)
+      for (int d = 0; d < D; ++d) acc = add(acc, qdev(X[(int64_t)row * D + d], c1[d], lst), lst);
+    qr[j] = acc;
+  }
+  // any lane's overflow reverts (first error in row order = the smallest failing code is not
+  // needed: qr can only fail with OVERFLOW)
+  if (wave_or(lst != ST_OK)) st = ST_OVERFLOW;
+  i128 sum_qr = 0;
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) sum_qr = add(sum_qr, wave_sum(qr[j], st), st);
+  const i128 mean_qr = idiv(sum_qr, (i128)N, st);
+  const i128 rel1 = p.constrained ? constrained_reliability(mean_qr, D, st)
+                                  : unconstrained_reliability(wsqrt(mean_qr, st), p.max_spread, st);
+  if (st == ST_OK && !in_unit_interval(rel1)) st = ST_RELIABILITY_INTERVAL;
+  if (st == ST_OK && p.n_failing > N) st = ST_USIZE_UNDERFLOW;
+  if (st != ST_OK) { if (lane == 0) p.status[b] = st; return; }
+  // rank mask: (qr asc, idx desc) (sort.cairo:96-101)
+  const int threshold = N - p.n_failing;
+  bool rel[RPL];
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int me = j * 64 + lane;
+    int rank = 0;
+#pragma unroll
+    for (int jj = 0; jj < RPL; ++jj)
+      for (int l = 0; l < 64; ++l) {
+        const int k = jj * 64 + l;
+        const i128 qk = shfl128(qr[jj], l);
+        if (k < N) rank += (qk < qr[j] || (qk == qr[j] && k > me)) ? 1 : 0;
+      }
+    rel[j] = me < N && rank < threshold;
+  }
+  int R = 0;
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) R += __popcll(__ballot(rel[j]));
+  // ---- pass 2: consensus per column over the reliable rows
+  for (int d = 0; d < D && st == ST_OK; ++d) {
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      const int row = j * 64 + lane;
+      rows.on[j] = rel[j];
+      rows.x[j] = row < N ? X[(int64_t)row * D + d] : 0;
+    }
+    i128 c;
+    if (p.constrained) {
+      c = smooth_median_w<RPL>(rows, lane, R, st);
+    } else {
+      i128 s = 0;
+#pragma unroll
+      for (int j = 0; j < RPL; ++j) s = add(s, wave_sum(rows.on[j] ? (i128)rows.x[j] : 0, st), st);
+      c = idiv(s, (i128)R, st);
+    }
+    if (lane == 0) cons[d] = (int64_t)c;
+  }
+  i128 s2 = 0;
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) s2 = add(s2, wave_sum(rel[j] ? qr[j] : 0, st), st);
+  const i128 mean_qr2 = idiv(s2, (i128)R, st);
+  const i128 rel2 = p.constrained ? constrained_reliability(mean_qr2, D, st)
+                                  : unconstrained_reliability(wsqrt(mean_qr2, st), p.max_spread, st);
+  if (st == ST_OK && !in_unit_interval(rel2)) st = ST_RELIABILITY_INTERVAL;
+  // ---- moments (math.cairo:208-222, 320-398), stage by stage like the CPU engine
+  for (int d = 0; d < D && st == ST_OK; ++d) {
+    i128 s = 0;
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      const int row = j * 64 + lane;
+      s = add(s, wave_sum(rel[j] ? (i128)X[(int64_t)row * D + d] : 0, st), st);
+    }
+    const i128 mu = idiv(s, (i128)R, st);
+    if (lane == 0) means[d] = (int64_t)mu;
+  }
+  __syncthreads();
+  for (int d = 0; d < D && st == ST_OK; ++d) {
+    i128 s = 0;
+    int l2 = ST_OK;
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      const int row = j * 64 + lane;
+      const i128 q = rel[j] ? qdev(X[(int64_t)row * D + d], means[d], l2) : 0;
+      if (wave_or(l2 != ST_OK)) fail(st, ST_OVERFLOW);
+      s = add(s, wave_sum(q, st), st);
+    }
+    const i128 v = idiv(s, (i128)R, st);
+    if (lane == 0) vars[d] = (int64_t)v;
+  }
+  __syncthreads();
+  for (int pass = 0; pass < 2; ++pass) {  // 0: skewness for all d, 1: kurtosis for all d
+    for (int d = 0; d < D && st == ST_OK; ++d) {
+      const i128 sd = wsqrt(vars[d], st);
+      i128 s = 0;
+      int l2 = ST_OK;
+#pragma unroll
+      for (int j = 0; j < RPL; ++j) {
+        const int row = j * 64 + lane;
+        i128 t = 0;
+        if (rel[j] && st == ST_OK) {
+          const i128 z = wdiv(sub(X[(int64_t)row * D + d], means[d], l2), sd, l2);
+          const i128 z2 = wmul(z, z, l2);
+          t = pass == 0 ? wmul(z2, z, l2) : wmul(z2, z2, l2);
+        }
+        // first error in row order, as the CPU loop: smallest failing row's code wins
+        int code = l2;
+        for (int l = 0; l < 64; ++l) {
+          const int c = __shfl(code, l);
+          if (c != ST_OK) { fail(st, c); break; }
+        }
+        s = add(s, wave_sum(t, st), st);
+      }
+      const i128 out = pass == 0 ? skew_from_sum(s, R, st) : kurt_from_sum(s, R, st);
+      if (lane == 0) (pass == 0 ? sk : ku)[d] = (int64_t)out;
+    }
+  }
+  __syncthreads();
+  if (st != ST_OK) { if (lane == 0) p.status[b] = st; return; }
+  // ---- commit
+  for (int d = lane; d < D; d += 64) {
+    const int64_t o = (int64_t)b * D + d;
+    p.consensus[o] = cons[d];
+    p.skew[o] = sk[d];
+    p.kurt[o] = ku[d];
+    if (p.c1) p.c1[o] = c1[d];
+  }
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int row = j * 64 + lane;
+    if (row < N) {
+      p.reliable[(int64_t)b * N + row] = rel[j] ? 1 : 0;
+      p.qr[(int64_t)b * N + row] = (int64_t)qr[j];
+    }
+  }
+  if (lane == 0) {
+    p.rel[2 * (int64_t)b] = (int64_t)rel1;
+    p.rel[2 * (int64_t)b + 1] = (int64_t)rel2;
+    p.status[b] = ST_OK;
+  }
+}
+
+}  // namespace svoc
+
+using namespace svoc;
+
+extern "C" int svoc_exact_round(const ExactParams* p, hipStream_t stream) {
+  if (p->B <= 0) return 0;
+  if (p->N < 1 || p->N > 256 || p->D < 1) return -1;
+  const size_t lds = (size_t)p->D * 6 * sizeof(int64_t);
+  if (lds > 150 * 1024) return -2;
+  auto k = p->N <= 64 ? consensus_exact_kernel<1> : consensus_exact_kernel<4>;
+  hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(k, dim3(p->B), dim3(64), lds, stream, *p);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,54 @@
+"""Consensus configuration: the reference constructor calldata (contract.cairo:235-265) as a dataclass.
+
+Field names follow the contract: ``enable_oracle_replacement``, ``required_majority``,
+``n_failing_oracles``, ``constrained``, ``unconstrained_max_spread``, ``dimension``.  Real-unit
+floats are used by the fast engine; the exact engine converts with the wsad codec (1e6 scale).
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+from typing import Any, Dict
+
+WSAD = 1_000_000
+
+
+@dataclasses.dataclass
+class ConsensusConfig:
+    n_oracles: int = 7
+    dimension: int = 6
+    n_failing_oracles: int = 2
+    constrained: bool = True
+    unconstrained_max_spread: float = 1.0     # real units (wsad / 1e6)
+    n_admins: int = 3
+    required_majority: int = 2
+    enable_oracle_replacement: bool = True
+
+    def validate(self) -> None:
+        if self.n_oracles < 1 or self.dimension < 1:
+            raise ValueError("n_oracles and dimension must be >= 1")
+        if not (0 <= self.n_admins <= 64):
+            raise ValueError("n_admins must be in [0, 64] (bit-packed vote rows)")
+        if not self.constrained and self.unconstrained_max_spread <= 0:
+            # the contract would divide by zero on the first round (contract.cairo:367)
+            raise ValueError("unconstrained_max_spread must be > 0")
+
+    @property
+    def max_spread_wsad(self) -> int:
+        return int(self.unconstrained_max_spread * WSAD)
+
+    def to_dict(self) -> Dict[str, Any]:
+        return dataclasses.asdict(self)
+
+    @classmethod
+    def from_dict(cls, d: Dict[str, Any]) -> "ConsensusConfig":
+        return cls(**{k: v for k, v in d.items() if k in {f.name for f in dataclasses.fields(cls)}})
+
+    def to_json(self) -> str:
+        return json.dumps(self.to_dict())
+
+    # deployed demo configuration (contract/README.md:43-61; client/common.py:8-9,31)
+    @classmethod
+    def deployed_demo(cls) -> "ConsensusConfig":
+        return cls(n_oracles=7, dimension=6, n_failing_oracles=2, constrained=True, n_admins=3,
+                   required_majority=2, enable_oracle_replacement=True)

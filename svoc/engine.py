@@ -1,0 +1,221 @@
+"""Batched consensus engine: B independent reference contracts as device-resident SoA tensors.
+
+One *instance* = one ``OracleConsensusNDS`` contract (contract/src/contract.cairo:38-832).  The state
+mirrors its ``Storage`` struct (contract.cairo:80-102) as tensors with a leading batch dimension:
+
+    values[B, N, ld]      oracles_values (bf16 / fp32 in fast mode, int64 wsad in exact mode)
+    enabled[B, N]         OracleInfo.enabled          reliable[B, N]   OracleInfo.reliable
+    n_active[B]           n_active_oracles            consensus_active[B]
+    consensus[B, D]       consensus_value             rel[B, 2]        first / second pass reliability
+    skew[B, D], kurt[B, D]
+
+Two numeric modes share one semantics:
+
+* ``exact``: int64 wsad storage, the bit-exact HIP kernel (csrc/kernels/consensus_exact.hip) or the
+  C++ CPU engine; updates are transactions (a reverted round rolls the update back, exactly like a
+  reverted Starknet tx) and are replayed in order per instance.
+* ``fast``: bf16 storage / fp32 math through the fused HIP kernel (csrc/kernels/consensus_fast.hip).
+  Updates inside one step are coalesced (last writer wins) -- exact for the reference because a
+  round is a pure function of the current values (survey §2.8-13); a reverted round keeps the stored
+  values but leaves every consensus output untouched.
+
+Steady-state steps issue no host synchronisation, so they can be captured in a HIP graph.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import ops as svops
+from .config import WSAD, ConsensusConfig
+from .status import Status
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+class ConsensusEngine:
+    def __init__(self, cfg: ConsensusConfig, batch: int, device="cuda", mode: str = "fast",
+                 storage: str = "bf16"):
+        cfg.validate()
+        if mode not in ("fast", "exact"):
+            raise ValueError("mode must be 'fast' or 'exact'")
+        self.cfg = cfg
+        self.B = int(batch)
+        self.N = cfg.n_oracles
+        self.D = cfg.dimension
+        self.mode = mode
+        self.device = torch.device(device)
+        self._ops = svops.ops()
+        B, N, D = self.B, self.N, self.D
+        dev = self.device
+        if mode == "fast":
+            self.vdtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[storage]
+            if self.device.type == "cuda" and self.vdtype != torch.bfloat16:
+                raise ValueError("the GPU fast path stores oracle values in bf16")
+            self.ld = _round_up(D, 8)              # 16-B rows for global_load_lds
+            odt = torch.float32
+        else:
+            self.vdtype = torch.int64
+            self.ld = D
+            odt = torch.int64
+        self.values = torch.zeros(B, N, self.ld, dtype=self.vdtype, device=dev)
+        self.enabled = torch.zeros(B, N, dtype=torch.uint8, device=dev)
+        self.n_active = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.reliable = torch.ones(B, N, dtype=torch.uint8, device=dev)   # constructor: reliable=true
+        self.consensus_active = torch.zeros(B, dtype=torch.bool, device=dev)
+        self.c1 = torch.zeros(B, D, dtype=odt, device=dev)
+        self.consensus = torch.zeros(B, D, dtype=odt, device=dev)
+        self.skew = torch.zeros(B, D, dtype=odt, device=dev)
+        self.kurt = torch.zeros(B, D, dtype=odt, device=dev)
+        self.rel = torch.zeros(B, 2, dtype=odt, device=dev)
+        self.qr = torch.zeros(B, N, dtype=odt, device=dev)
+        self.status = torch.full((B,), int(Status.NOT_ACTIVE), dtype=torch.int32, device=dev)
+        self.touched = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self._winner = torch.full((B, N), -1, dtype=torch.int32, device=dev)
+        self._active = torch.zeros(B, dtype=torch.uint8, device=dev)
+        self.wave_hint = 0
+        self.rounds = 0
+
+    # ------------------------------------------------------------------ sizing
+    @staticmethod
+    def bytes_per_instance(n: int, d: int, mode: str = "fast") -> int:
+        """HBM bytes of state per instance (survey §7.6 sizing)."""
+        s = 2 if mode == "fast" else 8
+        o = 4 if mode == "fast" else 8
+        ld = _round_up(d, 8) if mode == "fast" else d
+        return n * ld * s + 4 * d * o + n * (1 + 1 + o + 4) + 2 * o + 4 + 4 + 2
+
+    # ------------------------------------------------------------------ updates
+    def _as_storage(self, vals: torch.Tensor) -> torch.Tensor:
+        if self.mode == "exact":
+            if vals.dtype.is_floating_point:
+                raise TypeError("exact mode takes int64 wsad values (use svoc.codec.float_to_wsad)")
+            return vals.to(self.device, torch.int64).contiguous()
+        return vals.to(self.device, self.vdtype).contiguous()
+
+    def apply_updates(self, inst: torch.Tensor, oracle: torch.Tensor, vals: torch.Tensor) -> torch.Tensor:
+        """Store a batch of predictions (no consensus). Returns the per-update status [U] (device)."""
+        inst = torch.as_tensor(inst, dtype=torch.int64, device=self.device).contiguous()
+        oracle = torch.as_tensor(oracle, dtype=torch.int64, device=self.device).contiguous()
+        vals = self._as_storage(torch.as_tensor(vals))
+        if vals.dim() != 2 or vals.shape[1] != self.D:
+            raise ValueError(f"predictions must be [U, {self.D}]")
+        st = torch.empty(inst.numel(), dtype=torch.int32, device=self.device)
+        self._ops.apply_updates(self.values, self.enabled, self.n_active, self.touched, self._winner,
+                                inst, oracle, vals, self.cfg.constrained, st)
+        return st
+
+    # ------------------------------------------------------------------ rounds
+    def run_round(self, only_touched: bool = True) -> None:
+        """Consensus round for every instance that is fully active (and touched, by default)."""
+        full = self.n_active == self.N
+        act = full & (self.touched.bool() if only_touched else torch.ones_like(full))
+        self._active.copy_(act)
+        mx = self.cfg.unconstrained_max_spread
+        if self.mode == "fast":
+            self._ops.fast_round(self.values, self._active, self.D, self.cfg.n_failing_oracles,
+                                 self.cfg.constrained, float(mx), self.c1, self.consensus, self.skew,
+                                 self.kurt, self.rel, self.qr, self.reliable, self.status, self.wave_hint)
+            ok = (self.status == Status.OK) | (self.status == Status.ZERO_VARIANCE)
+        else:
+            self._ops.exact_round(self.values, self._active, self.cfg.n_failing_oracles, self.cfg.constrained,
+                                  self.cfg.max_spread_wsad, self.c1, self.consensus, self.skew, self.kurt,
+                                  self.rel, self.qr, self.reliable, self.status)
+            ok = self.status == Status.OK
+        self.consensus_active |= act & ok
+        self.touched.zero_()
+        self.rounds += 1
+
+    def step(self, inst, oracle, vals) -> torch.Tensor:
+        """update_prediction for a batch of (instance, oracle, prediction) + the consensus rounds.
+
+        fast: one coalesced round per touched instance.  exact: per-instance sequential
+        transactions (a reverted round restores that update's previous row)."""
+        if self.mode == "fast":
+            st = self.apply_updates(inst, oracle, vals)
+            self.run_round()
+            return st
+        return self._exact_transactions(inst, oracle, vals)
+
+    def _exact_transactions(self, inst, oracle, vals) -> torch.Tensor:
+        inst_h = np.asarray(torch.as_tensor(inst).cpu(), dtype=np.int64).reshape(-1)
+        orc_h = np.asarray(torch.as_tensor(oracle).cpu(), dtype=np.int64).reshape(-1)
+        vals = self._as_storage(torch.as_tensor(vals))
+        U = inst_h.size
+        out = torch.full((U,), int(Status.NOT_ORACLE), dtype=torch.int32, device=self.device)
+        ok_idx = (inst_h >= 0) & (inst_h < self.B) & (orc_h >= 0) & (orc_h < self.N)
+        # wave k = the k-th update of every instance (order preserved per instance)
+        occ = np.full(U, -1, dtype=np.int64)
+        seen: Dict[int, int] = {}
+        for u in np.nonzero(ok_idx)[0].tolist():
+            b = int(inst_h[u])
+            occ[u] = seen.get(b, 0)
+            seen[b] = occ[u] + 1
+        for k in range(int(occ.max()) + 1 if U else 0):
+            sel_h = np.nonzero(occ == k)[0]
+            sel = torch.as_tensor(sel_h, device=self.device)
+            bi = torch.as_tensor(inst_h[sel_h], device=self.device)
+            oi = torch.as_tensor(orc_h[sel_h], device=self.device)
+            old_rows = self.values[bi, oi].clone()
+            old_en = self.enabled[bi, oi].clone()
+            old_na = self.n_active[bi].clone()
+            self.touched.zero_()
+            st_u = self.apply_updates(bi, oi, vals[sel])
+            self.run_round(only_touched=True)        # outputs are only written when a round succeeds
+            st_b = self.status[bi]
+            full = self.n_active[bi] == self.N
+            tx = torch.where(st_u != 0, st_u,
+                             torch.where(full, st_b, torch.full_like(st_b, int(Status.NOT_ACTIVE))))
+            revert = (st_u == 0) & full & (st_b != int(Status.OK))
+            # roll back reverted transactions (contract semantics: the whole tx disappears)
+            self.values[bi, oi] = torch.where(revert[:, None], old_rows, self.values[bi, oi])
+            self.enabled[bi, oi] = torch.where(revert, old_en, self.enabled[bi, oi])
+            self.n_active[bi] = torch.where(revert, old_na, self.n_active[bi])
+            out[sel] = tx
+        return out
+
+    # ------------------------------------------------------------------ synthetic data
+    def randomize(self, seed: int = 0, a: float = 20.0, failing_low: float = 0.0) -> None:
+        """Fill every oracle of every instance (Beta(a,a) honest, U(0,1) failing), all enabled."""
+        from .models.oracle_gen import beta_failing_oracles
+        g = torch.Generator(device=self.device).manual_seed(seed)
+        x = beta_failing_oracles(self.B, self.N, self.D, self.cfg.n_failing_oracles, a, g, self.device)
+        if self.mode == "exact":
+            self.values[:, :, : self.D] = (x.double() * WSAD).to(torch.int64)
+        else:
+            self.values[:, :, : self.D] = x.to(self.vdtype)
+        self.enabled.fill_(1)
+        self.n_active.fill_(self.N)
+        self.touched.fill_(1)
+
+    # ------------------------------------------------------------------ getters (contract ABI names)
+    def get_consensus_value(self, i: Optional[int] = None) -> torch.Tensor:
+        return self.consensus if i is None else self.consensus[i]
+
+    def get_first_pass_consensus_reliability(self, i: Optional[int] = None):
+        return self.rel[:, 0] if i is None else self.rel[i, 0]
+
+    def get_second_pass_consensus_reliability(self, i: Optional[int] = None):
+        return self.rel[:, 1] if i is None else self.rel[i, 1]
+
+    def get_skewness(self, i: Optional[int] = None):
+        return self.skew if i is None else self.skew[i]
+
+    def get_kurtosis(self, i: Optional[int] = None):
+        return self.kurt if i is None else self.kurt[i]
+
+    def get_reliability(self) -> torch.Tensor:
+        """North-star alias: [B, 2] (first pass, second pass)."""
+        return self.rel
+
+    get_consensus = get_consensus_value
+
+    def get_predictions_dimension(self) -> int:
+        return self.D
+
+    def get_oracle_value_list(self, i: int):
+        return (self.values[i, :, : self.D], self.enabled[i].bool(), self.reliable[i].bool())

@@ -1,0 +1,66 @@
+"""Streaming update sources and queues.
+
+* :class:`SyntheticUpdateStream`: a device-resident pool of synthetic prediction batches (the
+  stochastic oracles of client/oracle_scheduler.py:73-92 at scale): every step, ``U`` distinct oracles
+  of every instance publish a new prediction; failing oracles (a fixed random subset per instance,
+  survey §5.3 fault injection) publish U(0,1)^D noise, honest ones Beta(a, a) draws.  The pool is
+  generated once and cycled, so the timed loop measures the engine, not the RNG.
+* :class:`UpdateQueue`: host-side accumulation of (instance, oracle, prediction) triples from any
+  producer (CLI, sentiment path, tests) flushed to the engine as one batched step.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+
+from .models.oracle_gen import failing_mask
+
+
+class SyntheticUpdateStream:
+    def __init__(self, B: int, N: int, D: int, U: int, f: int, pool: int = 2, device="cuda", seed: int = 0,
+                 a: float = 20.0, dtype=torch.bfloat16):
+        self.B, self.N, self.D, self.U, self.pool = B, N, D, U, pool
+        dev = torch.device(device)
+        g = torch.Generator(device=dev).manual_seed(seed)
+        self.failing = failing_mask(B, N, f, g, dev)            # [B, N] fixed per instance
+        self.batches: List[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = []
+        inst = torch.arange(B, device=dev).repeat_interleave(U)
+        for _ in range(pool):
+            orc = torch.rand(B, N, generator=g, device=dev).argsort(1)[:, :U].reshape(-1)
+            fail = self.failing[inst, orc]
+            vals = torch.empty(B * U, D, dtype=dtype, device=dev)
+            chunk = max(1, (1 << 26) // max(1, D))            # bound the fp32 temporaries
+            for s in range(0, B * U, chunk):
+                e = min(B * U, s + chunk)
+                ga = torch._standard_gamma(torch.full((e - s, D), a, device=dev), generator=g)
+                gb = torch._standard_gamma(torch.full((e - s, D), a, device=dev), generator=g)
+                hon = ga / (ga + gb)
+                uni = torch.rand(e - s, D, generator=g, device=dev)
+                vals[s:e] = torch.where(fail[s:e, None], uni, hon).to(dtype)
+            self.batches.append((inst.contiguous(), orc.contiguous(), vals))
+
+    def batch(self, i: int):
+        return self.batches[i % self.pool]
+
+
+class UpdateQueue:
+    def __init__(self):
+        self.inst: List[int] = []
+        self.orc: List[int] = []
+        self.vals: List[torch.Tensor] = []
+
+    def push(self, instance: int, oracle: int, prediction) -> None:
+        self.inst.append(int(instance))
+        self.orc.append(int(oracle))
+        self.vals.append(torch.as_tensor(prediction))
+
+    def __len__(self) -> int:
+        return len(self.inst)
+
+    def flush(self, engine) -> Optional[torch.Tensor]:
+        if not self.inst:
+            return None
+        st = engine.step(torch.tensor(self.inst), torch.tensor(self.orc), torch.stack(self.vals))
+        self.inst, self.orc, self.vals = [], [], []
+        return st

@@ -1,0 +1,96 @@
+"""Native CPU engines (csrc/engine/reference_cpu.cpp) vs the golden Python model and the torch ref."""
+import random
+
+import pytest
+import torch
+
+from fixtures import GOLDEN, N_FAILING
+from helpers import beta_oracles, run_exact, run_fast
+from svoc import ops as svops
+from svoc import reference as ref
+from svoc.ops import torch_ref
+from svoc.status import Status
+
+pytestmark = pytest.mark.skipif(not svops.available(), reason="svoc/_C.so not built")
+
+
+@pytest.mark.parametrize("name", list(GOLDEN))
+def test_exact_cpu_goldens(name):
+    values, constrained, ms, g = GOLDEN[name]
+    o = run_exact(torch.tensor([values], dtype=torch.int64), N_FAILING, constrained, ms)
+    assert o["status"].tolist() == [0]
+    assert o["c1"][0].tolist() == g["c1"]
+    assert o["qr"][0].tolist() == g["qr"]
+    assert o["reliable"][0].bool().tolist() == g["reliable"]
+    assert o["consensus"][0].tolist() == g["consensus"]
+    assert o["rel"][0].tolist() == [g["rel1"], g["rel2"]]
+    assert o["skew"][0].tolist() == g["skewness"]
+    assert o["kurt"][0].tolist() == g["kurtosis"]
+
+
+def _random_instance(rng, N, D, constrained, spread):
+    if constrained:
+        c = [rng.randint(0, 1_000_000) for _ in range(D)]
+        return [[min(1_000_000, max(0, c[d] + rng.randint(-spread, spread))) for d in range(D)] for _ in range(N)]
+    c = [rng.randint(-50_000_000, 50_000_000) for _ in range(D)]
+    return [[c[d] + rng.randint(-spread, spread) for d in range(D)] for _ in range(N)]
+
+
+@pytest.mark.parametrize("constrained", [True, False])
+def test_exact_cpu_matches_python_random(constrained):
+    """Bit-exact agreement incl. status codes on random instances (many of them revert)."""
+    rng = random.Random(1234 + constrained)
+    cases = []
+    for _ in range(60):
+        N = rng.choice([2, 3, 4, 5, 7, 9, 16])
+        D = rng.choice([1, 2, 3, 6])
+        f = rng.choice([0, 1, 2, 3])
+        spread = rng.choice([0, 3, 50, 5000, 400_000])
+        cases.append((N, D, f, _random_instance(rng, N, D, constrained, spread)))
+    ms = 3_000_000
+    for N, D, f, vals in cases:
+        st_ref, r = ref.round_status(vals, f, constrained, ms)
+        o = run_exact(torch.tensor([vals], dtype=torch.int64), f, constrained, ms)
+        assert o["status"].item() == int(st_ref), (N, D, f, vals)
+        if st_ref == Status.OK:
+            assert o["consensus"][0].tolist() == r.consensus
+            assert o["rel"][0].tolist() == [r.rel1, r.rel2]
+            assert o["skew"][0].tolist() == r.skewness
+            assert o["kurt"][0].tolist() == r.kurtosis
+            assert o["reliable"][0].bool().tolist() == r.reliable
+
+
+def test_exact_cpu_revert_leaves_outputs():
+    vals = [[500_000, 100_000]] * 7      # zero variance -> DIV_BY_ZERO
+    o = run_exact(torch.tensor([vals], dtype=torch.int64), 2, True)
+    assert o["status"].item() == Status.DIV_BY_ZERO
+    assert o["consensus"].abs().sum().item() == 0
+
+
+@pytest.mark.parametrize("N,D,f,constrained", [(7, 6, 2, True), (64, 40, 8, True), (33, 17, 5, False),
+                                                (256, 24, 32, True), (20, 3, 15, True)])
+def test_fast_cpu_vs_torch_ref(N, D, f, constrained):
+    x, _ = beta_oracles(6, N, D, f, seed=N + D)
+    ms = 1.0
+    o = run_fast(x, D, f, constrained, ms)
+    r = torch_ref.fast_round(x[:, :, :D], f, constrained, ms)
+    ok = o["status"] == 0
+    assert ok.any()
+    assert torch.equal(o["reliable"][ok].bool(), r["reliable"][ok])
+    torch.testing.assert_close(o["c1"][ok], r["c1"][ok], rtol=0, atol=1e-6)
+    torch.testing.assert_close(o["consensus"][ok], r["consensus"][ok], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(o["qr"][ok], r["qr"][ok], rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(o["rel"][ok], r["rel"][ok], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(o["skew"][ok], r["skew"][ok], rtol=1e-3, atol=1e-3)
+    torch.testing.assert_close(o["kurt"][ok], r["kurt"][ok], rtol=1e-3, atol=1e-3)
+
+
+def test_fast_cpu_tracks_exact_on_fixtures():
+    """Fast mode on the reference fixtures stays within wsad rounding of the exact engine (A.3)."""
+    for name, (values, constrained, ms, g) in GOLDEN.items():
+        x = torch.tensor([values], dtype=torch.float64) / 1e6
+        o = run_fast(x.float(), x.shape[2], N_FAILING, constrained, ms / 1e6 if ms else 1.0)
+        assert o["status"].item() == 0
+        assert o["reliable"][0].bool().tolist() == g["reliable"]
+        assert torch.allclose(o["consensus"][0].double(), torch.tensor(g["consensus"], dtype=torch.float64) / 1e6, atol=2e-6)
+        assert torch.allclose(o["rel"][0].double(), torch.tensor([g["rel1"], g["rel2"]], dtype=torch.float64) / 1e6, atol=2e-5)

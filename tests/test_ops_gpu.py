@@ -1,0 +1,113 @@
+"""HIP kernels on a real MI355X vs the plain-PyTorch fp32 reference / the bit-exact CPU engine."""
+import random
+
+import pytest
+import torch
+
+from fixtures import GOLDEN, N_FAILING
+from helpers import beta_oracles, run_exact, run_fast
+from svoc import ops as svops
+from svoc.ops import torch_ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _cmp_fast(o, r, ok):
+    assert torch.equal(o["reliable"][ok].bool().cpu(), r["reliable"][ok].cpu())
+    torch.testing.assert_close(o["c1"][ok], r["c1"][ok], rtol=0, atol=1e-6)
+    torch.testing.assert_close(o["consensus"][ok], r["consensus"][ok], rtol=0, atol=2e-6)
+    torch.testing.assert_close(o["qr"][ok], r["qr"][ok], rtol=2e-4, atol=1e-5)
+    torch.testing.assert_close(o["rel"][ok], r["rel"][ok], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(o["skew"][ok], r["skew"][ok], rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(o["kurt"][ok], r["kurt"][ok], rtol=2e-3, atol=5e-3)
+
+
+@pytest.mark.parametrize("N,D,f,constrained,hint", [
+    (7, 6, 2, True, 0), (64, 1024, 8, True, 8), (64, 1024, 8, True, 0), (64, 1000, 8, False, 0),
+    (50, 300, 5, True, 0), (128, 512, 16, True, 0), (100, 260, 10, False, 0),
+    (256, 4096, 32, True, 0), (256, 600, 32, False, 0), (200, 136, 20, True, 0), (20, 8, 15, True, 0)])
+def test_fast_hip_vs_torch(N, D, f, constrained, hint):
+    B = 12
+    x, _ = beta_oracles(B, N, D, f, seed=7 * N + D)
+    xg = x.to(DEV)
+    o = run_fast(xg, D, f, constrained, 1.0, wave_hint=hint)
+    torch.cuda.synchronize()
+    r = torch_ref.fast_round(xg[:, :, :D], f, constrained, 1.0)
+    ok = (o["status"] == 0)
+    assert ok.any(), o["status"]
+    _cmp_fast(o, r, ok)
+    # the CPU engine agrees on status
+    oc = run_fast(x, D, f, constrained, 1.0)
+    assert torch.equal(oc["status"], o["status"].cpu())
+
+
+def test_fast_hip_active_mask_and_revert():
+    B, N, D = 6, 64, 128
+    x, _ = beta_oracles(B, N, D, 8, seed=3)
+    x[1] = 0.0                          # zero-variance everywhere -> ZERO_VARIANCE flag (non fatal)
+    x[2, :40, :D] = 0.0                 # c1 = 0, 24/64 rows at distance 1: rel1 = 1 - 2*sqrt(.375) < 0
+    x[2, 40:, :D] = 1.0
+    xg = x.to(DEV)
+    active = torch.tensor([1, 1, 1, 0, 1, 1], dtype=torch.uint8, device=DEV)
+    o = run_fast(xg, D, 8, True, 1.0, active=active)
+    st = o["status"].cpu().tolist()
+    assert st[3] == -1                  # inactive: untouched
+    assert st[0] == 0 and st[4] == 0
+    assert st[1] == 32                  # ZERO_VARIANCE
+    assert st[2] == 6                   # RELIABILITY_INTERVAL
+    oc = run_fast(x, D, 8, True, 1.0, active=active.cpu())
+    assert oc["status"].tolist() == st
+
+
+@pytest.mark.parametrize("name", list(GOLDEN))
+def test_exact_hip_goldens(name):
+    values, constrained, ms, g = GOLDEN[name]
+    o = run_exact(torch.tensor([values] * 3, dtype=torch.int64, device=DEV), N_FAILING, constrained, ms)
+    assert o["status"].tolist() == [0, 0, 0]
+    assert o["consensus"][2].tolist() == g["consensus"]
+    assert o["rel"][1].tolist() == [g["rel1"], g["rel2"]]
+    assert o["skew"][0].tolist() == g["skewness"]
+    assert o["kurt"][0].tolist() == g["kurtosis"]
+    assert o["qr"][0].tolist() == g["qr"]
+
+
+@pytest.mark.parametrize("constrained", [True, False])
+def test_exact_hip_matches_cpu_random(constrained):
+    rng = random.Random(99)
+    for N, D, f in [(7, 6, 2), (9, 3, 1), (70, 5, 9), (130, 4, 20), (5, 2, 1), (4, 2, 0), (3, 1, 1)]:
+        B = 16
+        if constrained:
+            base = torch.randint(0, 1_000_001, (B, 1, D))
+            v = (base + torch.randint(-rng.choice([3, 500, 90_000]), 90_001, (B, N, D))).clamp(0, 1_000_000)
+        else:
+            v = torch.randint(-10**8, 10**8, (B, 1, D)) + torch.randint(-4_000_000, 4_000_000, (B, N, D))
+        v[0] = v[0, :1]                 # zero variance instance -> revert
+        oc = run_exact(v, f, constrained, 5_000_000)
+        og = run_exact(v.to(DEV), f, constrained, 5_000_000)
+        for k in oc:
+            assert torch.equal(oc[k], og[k].cpu()), (k, N, D, f)
+
+
+def test_apply_updates_hip_vs_cpu():
+    B, N, D, ld = 5, 16, 24, 24
+    U = 200
+    g = torch.Generator().manual_seed(0)
+    inst = torch.randint(0, B, (U,), generator=g)
+    orc = torch.randint(0, N, (U,), generator=g)
+    orc[7] = N + 3                      # not an oracle
+    upd = torch.rand(U, D, generator=g).to(torch.bfloat16)
+    upd[11, 3] = 1.5                    # interval error
+    res = []
+    for dev in ("cpu", DEV):
+        vals = torch.zeros(B, N, ld, dtype=torch.bfloat16, device=dev)
+        en = torch.zeros(B, N, dtype=torch.uint8, device=dev)
+        na = torch.zeros(B, dtype=torch.int32, device=dev)
+        tch = torch.zeros(B, dtype=torch.uint8, device=dev)
+        win = torch.full((B, N), -1, dtype=torch.int32, device=dev)
+        st = torch.empty(U, dtype=torch.int32, device=dev)
+        svops.ops().apply_updates(vals, en, na, tch, win, inst.to(dev), orc.to(dev), upd.to(dev), True, st)
+        res.append([t.cpu() for t in (vals, en, na, tch, st, win)])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    assert res[1][5].eq(-1).all()
