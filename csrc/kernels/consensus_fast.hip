@@ -135,9 +135,10 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
   for (int i = 0; i < KEEP; ++i) acc[i] = 0.f;
 
   // ------------------------------------------------------------ pass 1
+#pragma nounroll
   for (int s = 0; s < nslab; ++s) {
     const int col0 = s * G::W;
-    if (s > 0) __syncthreads();
+    if (s > 0) __syncthreads();  // previous slab fully consumed before it is overwritten
     load_slab<NSEG, WAVES>(inst, N, ld, col0, smem, tid, relmask, false);
     const int colA = col0 + 2 * cp;
     const bool vA = colA < D, vB = colA + 1 < D;
@@ -156,6 +157,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
       if (vA) p.c1[(int64_t)b * D + colA] = cA;
       if (vB) p.c1[(int64_t)b * D + colA + 1] = cB;
     }
+    __builtin_amdgcn_sched_barrier(0);  // keep the qr loads below the sort (register pressure)
     // per-row partials of qr; rows >= N hold NaN sentinels and are never read back
     float part[64];
 #pragma unroll
@@ -206,8 +208,17 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
     float myq = 0.f;
     if (tid < N) {
       myq = qr_lds[tid];
+      // rank = #{j : (qr_j, -j) < (qr_me, -me)}; 4 rows per ds_read_b128, independent loads
       int rank = 0;
-      for (int j = 0; j < N; ++j) {
+      const int n4 = N & ~3;
+      for (int j = 0; j < n4; j += 4) {
+        const float4 q4 = *(const float4*)(qr_lds + j);
+        rank += (q4.x < myq || (q4.x == myq && j > tid)) ? 1 : 0;
+        rank += (q4.y < myq || (q4.y == myq && j + 1 > tid)) ? 1 : 0;
+        rank += (q4.z < myq || (q4.z == myq && j + 2 > tid)) ? 1 : 0;
+        rank += (q4.w < myq || (q4.w == myq && j + 3 > tid)) ? 1 : 0;
+      }
+      for (int j = n4; j < N; ++j) {
         const float qj = qr_lds[j];
         rank += (qj < myq || (qj == myq && j > tid)) ? 1 : 0;  // (qr asc, idx desc)
       }
@@ -274,6 +285,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
 
   // ------------------------------------------------------------ pass 2 (contract.cairo:476-500)
   // slabs walked backwards: the slab resident from pass 1 is reused without a reload
+#pragma nounroll
   for (int s = nslab - 1; s >= 0; --s) {
     const int col0 = s * G::W;
     if (s != nslab - 1) {
@@ -295,6 +307,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
       const uint32_t hi = key_to_bf16x2(group_select<NSEG, P>(r, m2, lane));
       shA = 0.5f * (bf16_lo(lo) + bf16_lo(hi));
       shB = 0.5f * (bf16_hi(lo) + bf16_hi(hi));
+      __builtin_amdgcn_sched_barrier(0);
       // moments straight from the sorted registers: positions < cnt are the reliable values
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
@@ -388,8 +401,11 @@ extern "C" int svoc_fast_round_bf16(const FastParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
   if (p->N < 2 || p->N > 256 || p->ld % 8 != 0 || p->D > p->ld) return -1;
   if (p->N <= 64) {
-    if (p->D <= 512 && p->wave_hint != 8) return launch_fast<1, 4>(*p, stream);
-    return launch_fast<1, 8>(*p, stream);
+    // wave_hint: 2 / 4 / 8 waves per workgroup = 256 / 512 / 1024-column slabs (32/64/128 KiB LDS)
+    if (p->wave_hint == 2) return launch_fast<1, 2>(*p, stream);
+    if (p->wave_hint == 4) return launch_fast<1, 4>(*p, stream);
+    if (p->wave_hint == 8) return launch_fast<1, 8>(*p, stream);
+    return launch_fast<1, 4>(*p, stream);  // measured best for 64 x 1024 (2 workgroups / CU)
   }
   if (p->N <= 128) return launch_fast<2, 4>(*p, stream);
   return launch_fast<4, 4>(*p, stream);

@@ -24,7 +24,12 @@ __device__ __forceinline__ bool in_range(const UpdateParams& p, int64_t u, int d
   return v >= 0 && v <= 1000000;
 }
 
-// one wave per update: validate (wave-parallel over D), then claim the (instance, oracle) slot
+__device__ __forceinline__ bool bf16_unit(uint32_t raw16) {  // 0 <= x <= 1 (and -0.0)
+  return raw16 <= 0x3f80u || raw16 == 0x8000u;
+}
+
+// one wave per update: validate (wave-parallel over D, 16-B loads when rows allow), then claim the
+// (instance, oracle) slot with an atomicMax on the update's sequence number
 __global__ __launch_bounds__(256) void upd_validate_kernel(UpdateParams p) {
   const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -34,7 +39,17 @@ __global__ __launch_bounds__(256) void upd_validate_kernel(UpdateParams p) {
   if (b < 0 || b >= p.B || o < 0 || o >= p.N) st = ST_NOT_ORACLE;
   if (st == ST_OK && p.constrained) {
     bool ok = true;
-    for (int d = lane; d < p.D; d += 64) ok = ok && in_range(p, u, d);
+    const uint16_t* row = (const uint16_t*)p.upd + u * p.D;
+    if (p.dtype == 0 && (p.D & 7) == 0 && (((uintptr_t)row) & 15) == 0) {
+      for (int c = lane; c < p.D / 8; c += 64) {
+        const uint4 v = ((const uint4*)row)[c];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ok = ok && bf16_unit(w[k] & 0xffffu) && bf16_unit(w[k] >> 16);
+      }
+    } else {
+      for (int d = lane; d < p.D; d += 64) ok = ok && in_range(p, u, d);
+    }
     if (!__all(ok)) st = ST_INTERVAL_INPUT;
   }
   if (lane == 0) {

@@ -16,7 +16,8 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 fi
 
-for spec in ${BENCHES:-"c2:10:2 c3:10:2"}; do
+BENCHES="${BENCHES:-c2:10:2 c3:10:2}"
+for spec in $BENCHES; do
   IFS=: read cfg steps warm <<< "$spec"
   stage "bench $cfg"
   timeout -k 10 400 python bench.py --config $cfg --steps $steps --warmup $warm > gpurun_out/bench_$cfg.log 2>&1
