@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import dataclasses
 import json
-from typing import Any, Dict
+from typing import Any, Dict, Optional
 
 WSAD = 1_000_000
 
@@ -23,19 +23,22 @@ class ConsensusConfig:
     n_admins: int = 3
     required_majority: int = 2
     enable_oracle_replacement: bool = True
+    # exact wsad value of the spread when it must round-trip bit for bit (set by the ABI facade)
+    unconstrained_max_spread_wsad: Optional[int] = None
 
     def validate(self) -> None:
         if self.n_oracles < 1 or self.dimension < 1:
             raise ValueError("n_oracles and dimension must be >= 1")
         if not (0 <= self.n_admins <= 64):
             raise ValueError("n_admins must be in [0, 64] (bit-packed vote rows)")
-        if not self.constrained and self.unconstrained_max_spread <= 0:
-            # the contract would divide by zero on the first round (contract.cairo:367)
-            raise ValueError("unconstrained_max_spread must be > 0")
+        # unconstrained_max_spread == 0 is accepted: like the contract, every round then reverts
+        # with a division by zero (contract.cairo:367)
 
     @property
     def max_spread_wsad(self) -> int:
-        return int(self.unconstrained_max_spread * WSAD)
+        if self.unconstrained_max_spread_wsad is not None:
+            return int(self.unconstrained_max_spread_wsad)
+        return int(round(self.unconstrained_max_spread * WSAD))
 
     def to_dict(self) -> Dict[str, Any]:
         return dataclasses.asdict(self)
