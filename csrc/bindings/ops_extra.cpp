@@ -115,6 +115,7 @@ void register_extra_defs(torch::Library& m) {
       "Tensor(e!) winner, Tensor inst, Tensor oracle, Tensor upd, bool constrained, Tensor(f!) upd_status) -> ()");
   register_governance_defs(m);
   register_generator_defs(m);
+  register_io_defs(m);
 }
 
 void register_extra_cpu(torch::Library& m) {

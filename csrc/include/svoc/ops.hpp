@@ -16,4 +16,6 @@ void register_governance_hip(torch::Library& m);
 void register_generator_defs(torch::Library& m);
 void register_generator_cpu(torch::Library& m);
 void register_generator_hip(torch::Library& m);
+void register_io_defs(torch::Library& m);
+void register_io_cpu(torch::Library& m);
 }  // namespace svoc

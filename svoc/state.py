@@ -1,0 +1,91 @@
+"""``.svoc`` checkpoints of a whole :class:`ConsensusService` (engine state + governance).
+
+The byte format is implemented natively (csrc/engine/svoc_io.cpp: CRC-checked typed sections,
+atomic rename on write).  Sections follow the field order of the contract ``Storage`` struct
+(contract/src/contract.cairo:80-102); wsad integers are widened to i128 and addresses written as
+32-byte big-endian felts, so an exact-mode checkpoint carries exactly the contract's values.
+Restoring a checkpoint and continuing gives bit-identical results to never having stopped
+(tests/test_state.py).
+"""
+from __future__ import annotations
+
+import json
+from typing import Dict
+
+import torch
+
+from . import ops as svops
+from .config import ConsensusConfig
+
+FORMAT = "svoc-state/1"
+
+
+def save(svc, path: str) -> None:
+    e, g = svc.engine, svc.gov
+    D = e.D
+    exact = e.mode == "exact"
+    num = "i128" if exact else ""
+    meta = dict(format=FORMAT, mode=e.mode, batch=e.B, config=svc.cfg.to_dict(),
+                value_dtype=str(e.vdtype).replace("torch.", ""), rounds=e.rounds)
+    secs = [
+        ("admins", g.admins, "felt"),
+        ("unconstrained_max_spread", torch.tensor([svc.cfg.max_spread_wsad], dtype=torch.int64), "i128"),
+        ("oracle_address", g.oracle_addr, "felt"),
+        ("enabled", e.enabled, ""),
+        ("reliable", e.reliable, ""),
+        ("oracles_values", e.values[:, :, :D].contiguous(), num),
+        ("n_active_oracles", e.n_active, ""),
+        ("consensus_active", e.consensus_active.to(torch.uint8), ""),
+        ("vote_matrix_columns", g.votes, ""),
+        ("proposition_tag", g.prop_tag, ""),
+        ("proposition_oracle_index", g.prop_idx, ""),
+        ("proposition_address", g.prop_addr, "felt"),
+        ("consensus_value", e.consensus, num),
+        ("consensus_reliability_second_pass", e.rel[:, 1].contiguous(), num),
+        ("consensus_reliability_first_pass", e.rel[:, 0].contiguous(), num),
+        ("skewness", e.skew, num),
+        ("kurtosis", e.kurt, num),
+        # engine diagnostics (not contract storage)
+        ("essence_first_pass", e.c1, num),
+        ("quadratic_risk", e.qr, num),
+        ("status", e.status, ""),
+    ]
+    svops.ops().save_state(path, json.dumps(meta), [s[0] for s in secs],
+                           [s[1].detach().cpu().contiguous() for s in secs], [s[2] for s in secs])
+
+
+def load(path: str, device="cpu"):
+    """Rebuild a :class:`svoc.api.ConsensusService` from a checkpoint."""
+    from .api import ConsensusService
+    from .codec import limbs_to_address
+    meta_s, names, tensors = svops.ops().load_state(path)
+    meta = json.loads(meta_s)
+    if meta.get("format") != FORMAT:
+        raise ValueError("not an svoc-state/1 checkpoint")
+    t: Dict[str, torch.Tensor] = dict(zip(names, tensors))
+    cfg = ConsensusConfig.from_dict(meta["config"])
+    B = int(meta["batch"])
+    admins = [[limbs_to_address(x) for x in r] for r in t["admins"].tolist()]
+    oracles = [[limbs_to_address(x) for x in r] for r in t["oracle_address"].tolist()]
+    svc = ConsensusService(cfg, B, admins, oracles, device=device, mode=meta["mode"])
+    e, g = svc.engine, svc.gov
+    dev = e.device
+    e.values[:, :, : e.D].copy_(t["oracles_values"].to(dev, e.vdtype))
+    e.enabled.copy_(t["enabled"].to(dev))
+    e.reliable.copy_(t["reliable"].to(dev))
+    e.n_active.copy_(t["n_active_oracles"].to(dev))
+    e.consensus_active.copy_(t["consensus_active"].to(dev).bool())
+    g.votes.copy_(t["vote_matrix_columns"].to(dev))
+    g.prop_tag.copy_(t["proposition_tag"].to(dev))
+    g.prop_idx.copy_(t["proposition_oracle_index"].to(dev))
+    g.prop_addr.copy_(t["proposition_address"].to(dev))
+    e.consensus.copy_(t["consensus_value"].to(dev, e.consensus.dtype))
+    e.rel[:, 1].copy_(t["consensus_reliability_second_pass"].to(dev, e.rel.dtype))
+    e.rel[:, 0].copy_(t["consensus_reliability_first_pass"].to(dev, e.rel.dtype))
+    e.skew.copy_(t["skewness"].to(dev, e.skew.dtype))
+    e.kurt.copy_(t["kurtosis"].to(dev, e.kurt.dtype))
+    e.c1.copy_(t["essence_first_pass"].to(dev, e.c1.dtype))
+    e.qr.copy_(t["quadratic_risk"].to(dev, e.qr.dtype))
+    e.status.copy_(t["status"].to(dev))
+    e.rounds = int(meta.get("rounds", 0))
+    return svc

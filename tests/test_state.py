@@ -1,0 +1,71 @@
+"""Checkpoint / resume: .svoc round trip and restart equivalence (survey §5.4)."""
+import os
+import random
+
+import pytest
+import torch
+
+from fixtures import ADMINS, ORACLES, NEW_ORACLE
+from svoc import ops as svops
+from svoc import state
+from svoc.api import ConsensusService
+from svoc.config import ConsensusConfig
+
+pytestmark = pytest.mark.skipif(not svops.available(), reason="svoc/_C.so not built")
+
+
+def _drive(svc, rng, steps):
+    for _ in range(steps):
+        b = rng.randrange(svc.B)
+        if rng.random() < 0.85:
+            svc.update_predictions([(b, rng.choice(ORACLES), [rng.randint(0, 1_000_000) for _ in range(3)])])
+        else:
+            svc.governance([("propose", b, ADMINS[0], (rng.randrange(7), NEW_ORACLE + rng.randrange(3))),
+                            ("vote", b, ADMINS[1], 0, True)])
+
+
+def _snapshot(svc):
+    e, g = svc.engine, svc.gov
+    return [x.clone() for x in (e.values, e.enabled, e.reliable, e.n_active, e.consensus_active, e.consensus,
+                                e.rel, e.skew, e.kurt, g.oracle_addr, g.votes, g.prop_tag, g.prop_idx)]
+
+
+def test_restart_equivalence(tmp_path):
+    cfg = ConsensusConfig(n_oracles=7, dimension=3, n_failing_oracles=2, constrained=True, n_admins=3)
+    a = ConsensusService(cfg, 3, ADMINS, ORACLES, device="cpu", mode="exact")
+    rng = random.Random(7)
+    _drive(a, rng, 60)
+    p = os.path.join(tmp_path, "s.svoc")
+    state.save(a, p)
+    b = state.load(p)
+    for x, y in zip(_snapshot(a), _snapshot(b)):
+        assert torch.equal(x, y)
+    r1, r2 = random.Random(9), random.Random(9)
+    _drive(a, r1, 80)
+    _drive(b, r2, 80)
+    for x, y in zip(_snapshot(a), _snapshot(b)):
+        assert torch.equal(x, y)
+
+
+def test_corruption_detected(tmp_path):
+    cfg = ConsensusConfig(n_oracles=7, dimension=3, n_failing_oracles=2, n_admins=3)
+    a = ConsensusService(cfg, 2, ADMINS, ORACLES, device="cpu", mode="exact")
+    p = os.path.join(tmp_path, "s.svoc")
+    state.save(a, p)
+    raw = bytearray(open(p, "rb").read())
+    raw[-3] ^= 0xFF
+    open(p, "wb").write(bytes(raw))
+    with pytest.raises(Exception, match="CRC"):
+        state.load(p)
+
+
+def test_fast_mode_roundtrip(tmp_path):
+    cfg = ConsensusConfig(n_oracles=16, dimension=20, n_failing_oracles=2, n_admins=2)
+    a = ConsensusService(cfg, 4, ADMINS[:2], [100 + i for i in range(16)], device="cpu", mode="fast")
+    a.engine.randomize(0)
+    a.engine.run_round()
+    p = os.path.join(tmp_path, "f.svoc")
+    state.save(a, p)
+    b = state.load(p)
+    assert torch.equal(a.engine.values, b.engine.values)
+    assert torch.equal(a.engine.consensus, b.engine.consensus)
