@@ -61,7 +61,7 @@ void fast_round_checks(const at::Tensor& values, int64_t D, const at::Tensor& c1
 void fast_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t D,
                     int64_t n_failing, bool constrained, double max_spread, at::Tensor c1, at::Tensor cons,
                     at::Tensor skew, at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable,
-                    at::Tensor status, int64_t wave_hint) {
+                    at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim) {
   (void)wave_hint;
   fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
   const int64_t B = values.size(0), N = values.size(1), ld = values.size(2), is = values.stride(0);
@@ -97,13 +97,15 @@ void fast_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& a
   fb.reliable = reliable.data_ptr<uint8_t>();
   fb.qr = qr.data_ptr<float>();
   fb.status = status.data_ptr<int32_t>();
+  fb.mode = (int)mode;
+  fb.rel_dim = rel_dim;
   fast_round_batch_cpu(fb, cpu_threads());
 }
 
 void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t D,
                     int64_t n_failing, bool constrained, double max_spread, at::Tensor c1, at::Tensor cons,
                     at::Tensor skew, at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable,
-                    at::Tensor status, int64_t wave_hint) {
+                    at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim) {
   fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
   TORCH_CHECK(values.scalar_type() == at::kBFloat16, "GPU fast path stores values in bf16");
   const int64_t B = values.size(0), N = values.size(1), ld = values.size(2);
@@ -120,6 +122,9 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
   p.constrained = constrained ? 1 : 0;
   p.max_spread = (float)max_spread;
   p.wave_hint = (int)wave_hint;
+  TORCH_CHECK(mode >= 0 && mode <= 2, "mode must be 0, 1 or 2");
+  p.mode = (int)mode;
+  p.rel_dim = (int)rel_dim;
   p.c1 = c1.data_ptr<float>();
   p.consensus = cons.data_ptr<float>();
   p.skew = skew.data_ptr<float>();
@@ -205,7 +210,7 @@ TORCH_LIBRARY(svoc, m) {
   m.def(
       "fast_round(Tensor values, Tensor? active, int D, int n_failing, bool constrained, float max_spread, "
       "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "
-      "Tensor(g!) reliable, Tensor(h!) status, int wave_hint=0) -> ()");
+      "Tensor(g!) reliable, Tensor(h!) status, int wave_hint=0, int mode=0, int rel_dim=0) -> ()");
   m.def(
       "exact_round(Tensor values, Tensor? active, int n_failing, bool constrained, int max_spread, "
       "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "

@@ -70,10 +70,14 @@ struct FastBatch {
   uint8_t* reliable;
   float* qr;
   int32_t* status;
+  int mode = 0;
+  int64_t rel_dim = 0;
 };
 
+// mode 0: full round; 1: pass 1 only (c1 + qr partials); 2: pass 2 from o.qr (already reduced).
+// rel_dim: divisor of the constrained reliability (0 = D).
 int fast_round_one(const float* X, int64_t N, int64_t D, int64_t n_failing, bool constrained,
-                   float max_spread, FastOut& o);
+                   float max_spread, FastOut& o, int mode = 0, int64_t rel_dim = 0);
 void fast_round_batch_cpu(const FastBatch& b, int threads);
 
 }  // namespace svoc

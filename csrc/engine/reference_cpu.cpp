@@ -164,12 +164,13 @@ void exact_round_batch_cpu(const ExactBatch& b, int threads) {
 // ------------------------------------------------------------------------------------------------
 
 int fast_round_one(const float* X, int64_t N, int64_t D, int64_t n_failing, bool constrained,
-                   float max_spread, FastOut& o) {
+                   float max_spread, FastOut& o, int mode, int64_t rel_dim) {
   if (n_failing > N) return ST_USIZE_UNDERFLOW;
   if (N < 2) return ST_INDEX_OOB;
   std::vector<float> col(N);
   const int64_t m = N / 2;
-  for (int64_t d = 0; d < D; ++d) {
+  const double rd = (double)(rel_dim > 0 ? rel_dim : D);
+  for (int64_t d = 0; d < D && mode != 2; ++d) {
     for (int64_t i = 0; i < N; ++i) col[i] = X[i * D + d];
     std::nth_element(col.begin(), col.begin() + m, col.end());
     float hi = col[m];
@@ -178,16 +179,19 @@ int fast_round_one(const float* X, int64_t N, int64_t D, int64_t n_failing, bool
   }
   double sum_qr = 0.0;
   for (int64_t i = 0; i < N; ++i) {
-    float acc = 0.f;
-    for (int64_t d = 0; d < D; ++d) {
-      float y = X[i * D + d] - o.c1[d];
-      acc = std::fma(y, y, acc);
+    if (mode != 2) {
+      float acc = 0.f;
+      for (int64_t d = 0; d < D; ++d) {
+        float y = X[i * D + d] - o.c1[d];
+        acc = std::fma(y, y, acc);
+      }
+      o.qr[i] = acc;
     }
-    o.qr[i] = acc;
-    sum_qr += acc;
+    sum_qr += o.qr[i];
   }
+  if (mode == 1) return ST_OK;
   auto rel_of = [&](double mean_qr) -> float {
-    return constrained ? (float)(1.0 - 2.0 * std::sqrt(mean_qr / (double)D))
+    return constrained ? (float)(1.0 - 2.0 * std::sqrt(mean_qr / rd))
                        : (float)(1.0 - std::min((double)max_spread, std::sqrt(mean_qr)) / (double)max_spread);
   };
   float rel1 = rel_of(sum_qr / (double)N);
@@ -250,10 +254,15 @@ void fast_round_batch_cpu(const FastBatch& b, int threads) {
     std::vector<float> x(N * D), c1(D), cons(D), sk(D), ku(D), qr(N);
     std::vector<uint8_t> rel(N);
     b.load(b.values, i, x.data());
+    if (b.mode == 2) std::memcpy(qr.data(), b.qr + i * N, N * sizeof(float));
     FastOut o{c1.data(), qr.data(), rel.data(), cons.data(), sk.data(), ku.data(), 0.f, 0.f};
-    int st = fast_round_one(x.data(), N, D, b.n_failing, b.constrained, b.max_spread, o);
+    int st = fast_round_one(x.data(), N, D, b.n_failing, b.constrained, b.max_spread, o, b.mode, b.rel_dim);
     b.status[i] = st;
-    if (b.c1 && b.n_failing <= N && N >= 2) std::memcpy(b.c1 + i * D, c1.data(), D * sizeof(float));
+    if (b.c1 && b.n_failing <= N && N >= 2 && b.mode != 2) std::memcpy(b.c1 + i * D, c1.data(), D * sizeof(float));
+    if (b.mode == 1) {
+      if (st == ST_OK) std::memcpy(b.qr + i * N, qr.data(), N * sizeof(float));
+      return;
+    }
     if (st != ST_OK) return;
     std::memcpy(b.consensus + i * D, cons.data(), D * sizeof(float));
     std::memcpy(b.skew + i * D, sk.data(), D * sizeof(float));

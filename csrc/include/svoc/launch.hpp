@@ -14,7 +14,9 @@ struct FastParams {
   int n_failing;
   int constrained;
   float max_spread;
-  int wave_hint;            // 0 = auto, 8 = force the 8-wave single-slab variant for N <= 64
+  int wave_hint;            // 0 = auto, 2/4/8 = waves per workgroup for N <= 64
+  int mode;                 // 0 full round, 1 pass 1 only (qr partials + c1), 2 pass 2 from qr (D-sharding)
+  int rel_dim;              // divisor of the constrained reliability (0 = D; global D when D-sharded)
   float* c1;                // [B, D]
   float* consensus;         // [B, D]
   float* skew;              // [B, D]

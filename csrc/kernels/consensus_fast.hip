@@ -135,8 +135,9 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
   for (int i = 0; i < KEEP; ++i) acc[i] = 0.f;
 
   // ------------------------------------------------------------ pass 1
+  const int pass1_slabs = p.mode == 2 ? 0 : nslab;  // mode 2: qr comes all-reduced from the caller
 #pragma nounroll
-  for (int s = 0; s < nslab; ++s) {
+  for (int s = 0; s < pass1_slabs; ++s) {
     const int col0 = s * G::W;
     if (s > 0) __syncthreads();  // previous slab fully consumed before it is overwritten
     load_slab<NSEG, WAVES>(inst, N, ld, col0, smem, tid, relmask, false);
@@ -195,11 +196,20 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
   __syncthreads();
   for (int t = tid; t < G::NPAD; t += G::NT) {
     float q = 0.f;
+    if (p.mode == 2) {
+      q = t < N ? p.qr[(int64_t)b * N + t] : 0.f;
+    } else {
 #pragma unroll
-    for (int w = 0; w < WAVES; ++w) q += qr_part[w * G::NPAD + t];
+      for (int w = 0; w < WAVES; ++w) q += qr_part[w * G::NPAD + t];
+    }
     qr_lds[t] = q;
   }
   __syncthreads();
+  if (p.mode == 1) {  // D-sharding, pass 1: publish this shard's qr partials (c1 already written)
+    for (int t = tid; t < N; t += G::NT) p.qr[(int64_t)b * N + t] = qr_lds[t];
+    if (tid == 0) p.status[b] = ST_OK;
+    return;
+  }
 
   // ------------------------------------------------------------ rank mask (contract.cairo:345-363)
   const int R = N - p.n_failing;
@@ -247,12 +257,13 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
     }
     int st = ST_OK;
     float rel1, rel2 = 0.f;
-    if (CONS) rel1 = 1.f - 2.f * sqrtf(sa / (float)N / (float)D);           // contract.cairo:436-439
+    const float rd = (float)(p.rel_dim > 0 ? p.rel_dim : D);
+    if (CONS) rel1 = 1.f - 2.f * sqrtf(sa / (float)N / rd);                  // contract.cairo:436-439
     else rel1 = 1.f - fminf(p.max_spread, sqrtf(sa / (float)N)) / p.max_spread;  // :365-368
     if (!(rel1 >= 0.f && rel1 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
     else if (R < 2) st = R <= 0 ? ST_USIZE_UNDERFLOW : ST_INDEX_OOB;
     else {
-      if (CONS) rel2 = 1.f - 2.f * sqrtf(sr / (float)R / (float)D);
+      if (CONS) rel2 = 1.f - 2.f * sqrtf(sr / (float)R / rd);
       else rel2 = 1.f - fminf(p.max_spread, sqrtf(sr / (float)R)) / p.max_spread;
       if (!(rel2 >= 0.f && rel2 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
       else if (R < 4) st = ST_TOO_FEW_RELIABLE;
@@ -288,7 +299,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
 #pragma nounroll
   for (int s = nslab - 1; s >= 0; --s) {
     const int col0 = s * G::W;
-    if (s != nslab - 1) {
+    if (s != nslab - 1 || p.mode == 2) {
       __syncthreads();
       load_slab<NSEG, WAVES>(inst, N, ld, col0, smem, tid, relmask, true);
     } else if (CONS) {

@@ -1,0 +1,97 @@
+"""Multi-process paths on CPU with the gloo backend (world_size 2): DP and D-sharding."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from svoc import ops as svops
+
+pytestmark = pytest.mark.skipif(not svops.available(), reason="svoc/_C.so not built")
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.set_num_threads(2)
+
+
+def _dp_worker(rank, world, port, outdir):
+    _init(rank, world, port)
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    from svoc.parallel.dp import DataParallelConsensus
+    cfg = ConsensusConfig(n_oracles=16, dimension=24, n_failing_oracles=2)
+    e = ConsensusEngine(cfg, 3, device="cpu", mode="fast")
+    dp = DataParallelConsensus(e, rank, world)
+    e.randomize(seed=100 + rank)
+    e.run_round()
+    dp.accumulate()
+    g = dp.reduce().clone()
+    summ = dp.all_gather_summaries(k=4)
+    torch.save(dict(g=g, summ=summ, ids=dp.global_ids(), local=e.consensus[:, :4].clone(),
+                    rel=e.rel.clone()), os.path.join(outdir, f"dp{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_data_parallel_gloo():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_dp_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"dp{i}.pt"), weights_only=True) for i in range(world)]
+    assert torch.equal(r[0]["g"], r[1]["g"])
+    assert r[0]["g"][2].item() == 6            # 2 ranks x 3 instances processed
+    full = r[0]["summ"]["consensus"]
+    assert torch.allclose(full[:3].float(), r[0]["local"].float())
+    assert torch.allclose(full[3:].float(), r[1]["local"].float())
+    assert r[1]["ids"].tolist() == [3, 4, 5]
+
+
+def _ds_worker(rank, world, port, outdir, x, cfgd):
+    _init(rank, world, port)
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    from svoc.parallel.dshard import run_round_sharded, shard_bounds
+    cfg = ConsensusConfig(**cfgd)
+    lo, hi = shard_bounds(cfg.dimension, rank, world)
+    lcfg = ConsensusConfig(**{**cfgd, "dimension": hi - lo})
+    e = ConsensusEngine(lcfg, x.shape[0], device="cpu", mode="fast")
+    e.values[:, :, : hi - lo] = x[:, :, lo:hi]
+    e.enabled.fill_(1); e.n_active.fill_(cfg.n_oracles); e.touched.fill_(1)
+    run_round_sharded(e, cfg.dimension, world=world)
+    torch.save(dict(cons=e.consensus.clone(), rel=e.rel.clone(), reliable=e.reliable.clone(),
+                    skew=e.skew.clone(), st=e.status.clone(), lo=lo, hi=hi),
+               os.path.join(outdir, f"ds{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("constrained", [True, False])
+def test_dsharding_matches_single_process(constrained):
+    from helpers import beta_oracles, run_fast
+    B, N, D, f = 4, 32, 40, 4
+    x, _ = beta_oracles(B, N, D, f, seed=11)
+    x = x[:, :, :D].contiguous()
+    ref = run_fast(x, D, f, constrained, 1.0)
+    cfgd = dict(n_oracles=N, dimension=D, n_failing_oracles=f, constrained=constrained, unconstrained_max_spread=1.0)
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ds_worker, args=(world, _free_port(), d, x, cfgd), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"ds{i}.pt"), weights_only=True) for i in range(world)]
+    for s in r:
+        assert torch.equal(s["st"], ref["status"])
+        assert torch.equal(s["reliable"], ref["reliable"])
+        torch.testing.assert_close(s["rel"], ref["rel"], rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(s["cons"], ref["consensus"][:, s["lo"]:s["hi"]], rtol=0, atol=1e-6)
+        torch.testing.assert_close(s["skew"], ref["skew"][:, s["lo"]:s["hi"]], rtol=1e-4, atol=1e-4)

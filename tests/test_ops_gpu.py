@@ -111,3 +111,40 @@ def test_apply_updates_hip_vs_cpu():
     for a, b in zip(*res):
         assert torch.equal(a, b)
     assert res[1][5].eq(-1).all()
+
+
+@pytest.mark.parametrize("N,D,f,constrained", [(64, 1000, 8, True), (256, 700, 32, True), (100, 260, 10, False)])
+def test_fast_hip_split_modes_match_full(N, D, f, constrained):
+    """mode 1 (pass 1: qr partials) + mode 2 (pass 2 from qr) == the fused round (D-sharding path),
+    and two column shards with a summed qr reproduce the full instance."""
+    B = 6
+    x, _ = beta_oracles(B, N, D, f, seed=N)
+    xg = x.to(DEV)
+    full = run_fast(xg, D, f, constrained, 1.0)
+    from helpers import alloc_fast_out
+    o = alloc_fast_out(B, N, D, DEV)
+    args = (xg, None, D, f, constrained, 1.0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"], o["qr"],
+            o["reliable"], o["status"], 0)
+    svops.ops().fast_round(*args, 1, D)
+    svops.ops().fast_round(*args, 2, D)
+    for k in ("consensus", "rel", "reliable", "status", "skew", "kurt"):
+        torch.testing.assert_close(o[k], full[k], rtol=0, atol=0)
+    # two shards of the columns
+    h = (D // 2 + 7) // 8 * 8
+    parts = []
+    for lo, hi in ((0, h), (h, D)):
+        xs = torch.zeros(B, N, (hi - lo + 7) // 8 * 8, dtype=torch.bfloat16, device=DEV)
+        xs[:, :, : hi - lo] = xg[:, :, lo:hi]
+        os_ = alloc_fast_out(B, N, hi - lo, DEV)
+        parts.append((xs, os_, hi - lo, lo, hi))
+        svops.ops().fast_round(xs, None, hi - lo, f, constrained, 1.0, os_["c1"], os_["consensus"], os_["skew"],
+                               os_["kurt"], os_["rel"], os_["qr"], os_["reliable"], os_["status"], 0, 1, D)
+    qsum = parts[0][1]["qr"] + parts[1][1]["qr"]
+    for xs, os_, dd, lo, hi in parts:
+        os_["qr"].copy_(qsum)
+        svops.ops().fast_round(xs, None, dd, f, constrained, 1.0, os_["c1"], os_["consensus"], os_["skew"],
+                               os_["kurt"], os_["rel"], os_["qr"], os_["reliable"], os_["status"], 0, 2, D)
+        ok = full["status"] == 0
+        assert torch.equal(os_["reliable"][ok], full["reliable"][ok])
+        torch.testing.assert_close(os_["consensus"][ok], full["consensus"][ok][:, lo:hi], rtol=0, atol=1e-6)
+        torch.testing.assert_close(os_["rel"][ok], full["rel"][ok], rtol=1e-5, atol=1e-5)
