@@ -1,0 +1,123 @@
+"""RoBERTa/BERT-base style encoder + go_emotions multi-label head (the oracle's sentiment model).
+
+The reference client runs HF ``pipeline("text-classification", "SamLowe/roberta-base-go_emotions",
+top_k=None)`` (client/oracle_scheduler.py:23-25): a RoBERTa-base encoder, a 28-way classification
+head, sigmoid scores for all 28 go_emotions labels; the client keeps 6 labels
+(client/common.py:19-31) and normalises them to sum 1 (oracle_scheduler.py:20-21, 36-40).
+
+There is no network on the GPU boxes, so the weights are random-initialised with a fixed seed and
+the architecture is BERT-base sized (12 layers, hidden 768, 12 heads, FFN 3072, vocab 50265,
+512 positions).  The implementation is plain PyTorch-ROCm: bf16 weights, fused QKV projection
+(one hipBLASLt GEMM), ``scaled_dot_product_attention`` (flash attention kernels on ROCm), pre-sized
+buffers so the forward can be captured in a HIP graph.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+GO_EMOTIONS = [
+    "admiration", "amusement", "anger", "annoyance", "approval", "caring", "confusion", "curiosity",
+    "desire", "disappointment", "disapproval", "disgust", "embarrassment", "excitement", "fear",
+    "gratitude", "grief", "joy", "love", "nervousness", "optimism", "pride", "realization", "relief",
+    "remorse", "sadness", "surprise", "neutral",
+]
+# client/common.py:19-26 (order matters: it is the consensus vector's component order)
+ORACLE_LABELS = ["optimism", "anger", "annoyance", "excitement", "nervousness", "remorse"]
+ORACLE_LABEL_IDX = [GO_EMOTIONS.index(x) for x in ORACLE_LABELS]
+
+
+@dataclasses.dataclass
+class EncoderConfig:
+    vocab_size: int = 50265
+    hidden: int = 768
+    layers: int = 12
+    heads: int = 12
+    ffn: int = 3072
+    max_positions: int = 514
+    n_labels: int = 28
+    layer_norm_eps: float = 1e-5
+    pad_id: int = 1
+
+    @classmethod
+    def tiny(cls) -> "EncoderConfig":
+        return cls(vocab_size=1000, hidden=64, layers=2, heads=4, ffn=128, max_positions=130)
+
+
+class Layer(nn.Module):
+    def __init__(self, c: EncoderConfig):
+        super().__init__()
+        self.heads = c.heads
+        self.qkv = nn.Linear(c.hidden, 3 * c.hidden)
+        self.out = nn.Linear(c.hidden, c.hidden)
+        self.ln1 = nn.LayerNorm(c.hidden, eps=c.layer_norm_eps)
+        self.fc1 = nn.Linear(c.hidden, c.ffn)
+        self.fc2 = nn.Linear(c.ffn, c.hidden)
+        self.ln2 = nn.LayerNorm(c.hidden, eps=c.layer_norm_eps)
+
+    def forward(self, x: torch.Tensor, mask: Optional[torch.Tensor]) -> torch.Tensor:
+        B, S, H = x.shape
+        q, k, v = self.qkv(x).view(B, S, 3, self.heads, H // self.heads).permute(2, 0, 3, 1, 4)
+        a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask)
+        x = self.ln1(x + self.out(a.transpose(1, 2).reshape(B, S, H)))   # post-LN (BERT/RoBERTa)
+        return self.ln2(x + self.fc2(F.gelu(self.fc1(x))))
+
+
+class SentimentEncoder(nn.Module):
+    def __init__(self, c: EncoderConfig = EncoderConfig()):
+        super().__init__()
+        self.cfg = c
+        self.tok = nn.Embedding(c.vocab_size, c.hidden, padding_idx=c.pad_id)
+        self.pos = nn.Embedding(c.max_positions, c.hidden)
+        self.typ = nn.Embedding(1, c.hidden)
+        self.ln = nn.LayerNorm(c.hidden, eps=c.layer_norm_eps)
+        self.layers = nn.ModuleList([Layer(c) for _ in range(c.layers)])
+        self.dense = nn.Linear(c.hidden, c.hidden)      # RobertaClassificationHead: dense-tanh-out
+        self.head = nn.Linear(c.hidden, c.n_labels)
+        self.apply(self._init)
+
+    @staticmethod
+    def _init(m):
+        if isinstance(m, (nn.Linear, nn.Embedding)):
+            nn.init.normal_(m.weight, std=0.02)
+        if isinstance(m, nn.Linear) and m.bias is not None:
+            nn.init.zeros_(m.bias)
+
+    def forward(self, ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """ids [B, S] -> 28 sigmoid scores [B, 28] (float32)."""
+        B, S = ids.shape
+        pos = torch.arange(2, S + 2, device=ids.device)           # RoBERTa positions start at pad+1
+        x = self.ln(self.tok(ids) + self.pos(pos)[None] + self.typ.weight[0])
+        mask = None
+        if attention_mask is not None:
+            mask = torch.zeros(B, 1, 1, S, dtype=x.dtype, device=x.device)
+            mask.masked_fill_(attention_mask[:, None, None, :] == 0, float("-inf"))
+        for layer in self.layers:
+            x = layer(x, mask)
+        h = torch.tanh(self.dense(x[:, 0]))
+        return torch.sigmoid(self.head(h).float())
+
+
+def scores_to_oracle_vectors(scores: torch.Tensor) -> torch.Tensor:
+    """prediction_to_vector + normalize (oracle_scheduler.py:20-34): [..., 28] -> [..., 6], sum 1."""
+    v = scores[..., ORACLE_LABEL_IDX]
+    return v / v.sum(-1, keepdim=True)
+
+
+def build(device="cuda", dtype=torch.bfloat16, seed: int = 0, cfg: EncoderConfig = EncoderConfig()) -> SentimentEncoder:
+    state = torch.random.get_rng_state()   # deterministic weights without disturbing the caller's RNG
+    torch.manual_seed(seed)
+    m = SentimentEncoder(cfg)
+    torch.random.set_rng_state(state)
+    return m.to(device=device, dtype=dtype).eval()
+
+
+def flops_per_sequence(c: EncoderConfig, S: int) -> float:
+    """Forward FLOPs for one sequence (GEMMs + attention), for throughput reporting."""
+    per_layer = 2 * S * c.hidden * (3 * c.hidden + c.hidden + 2 * c.ffn) + 4 * S * S * c.hidden
+    return c.layers * per_layer + 2 * c.hidden * (c.hidden + c.n_labels)
