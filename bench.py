@@ -32,6 +32,10 @@ CONFIGS = {
                batch=1024, update_frac=0.25),
     "c2": dict(model="svoc-consensus N=64 D=1024 batched (f=8, constrained)", N=64, D=1024, f=8,
                batch=10000, update_frac=0.0),
+    "c4": dict(model="sentiment oracles: BERT-base (12x768, bf16) on 30-comment windows -> 7 oracles x 6 dims",
+               N=7, D=6, f=2, batch=64, update_frac=1.0, seq_len=128),
+    "c5": dict(model="deployed config 7 oracles x 6 dims, governance + reliability stream (1% instances vote/step)",
+               N=7, D=6, f=2, batch=1 << 20, update_frac=1 / 7, gov_frac=0.01),
 }
 METRIC = "consensus updates/sec (N oracles x D dims, batched)"
 
@@ -69,19 +73,54 @@ def main():
 
     # synthetic update stream resident in HBM: `pool` steps of updates, cycled
     U_per_inst = int(round(c["update_frac"] * c["N"]))
-    stream = None
-    if U_per_inst:
+    stream = pipe = gov = None
+    extra = {}
+    if args.config == "c4":
+        from svoc.models import corpus
+        from svoc.models.encoder import flops_per_sequence
+        from svoc.models.sentiment_oracle import SentimentOraclePipeline
+        pipe = SentimentOraclePipeline(eng, seed=0)
+        g = torch.Generator(device=dev).manual_seed(rank)
+        toks = [corpus.synthetic_token_batch(B * 30, c["seq_len"], 50265, g, dev) for _ in range(2)]
+        extra["comments_per_step"] = B * 30
+        extra["encoder_gflop_per_step"] = B * 30 * flops_per_sequence(pipe.encoder.cfg, c["seq_len"]) / 1e9
+    elif U_per_inst:
         from svoc.stream import SyntheticUpdateStream
         stream = SyntheticUpdateStream(B, c["N"], c["D"], U_per_inst, c["f"], pool=2, device=dev, seed=rank)
+    if args.config == "c5":
+        from svoc.codec import address_to_limbs
+        from svoc.governance import Governance
+        gov = Governance(B, 3, c["N"], dev, True, 2)
+        gov.admins.copy_(torch.tensor([address_to_limbs(1000 + a) for a in range(3)], device=dev).expand(B, 3, 4))
+        ora = torch.tensor([address_to_limbs(5000 + o) for o in range(c["N"])], device=dev)
+        gov.oracle_addr.copy_(ora.expand(B, c["N"], 4))
+        K = max(1, int(B * c["gov_frac"]))
+        gg = torch.Generator(device=dev).manual_seed(7 + rank)
+        gov_batches = []
+        for i in range(2):      # alternate: proposals by admin 0, then a supporting vote by admin 1
+            inst = torch.randperm(B, generator=gg, device=dev)[:K]
+            caller = torch.tensor(address_to_limbs(1000 + i), device=dev).expand(K, 4).contiguous()
+            kind = torch.full((K,), i, dtype=torch.int32, device=dev)
+            a0 = torch.full((K,), 1 if i == 0 else 0, dtype=torch.int32, device=dev)
+            a1 = torch.randint(0, c["N"], (K,), generator=gg, device=dev) if i == 0 else torch.ones(K, dtype=torch.int64, device=dev)
+            addr = torch.randint(10**6, 10**9, (K, 4), generator=gg, device=dev)
+            gov_batches.append((inst, caller, kind, a0, a1, addr))
+        extra["governance_actions_per_step"] = K
+        extra["state_bytes_per_instance"] = eng.bytes_per_instance(c["N"], c["D"], "fast") + 3 * 4 * 8 + 3 * 8 + 3 * (1 + 4 + 32) + c["N"] * 32
+        extra["instances_per_288GB"] = int(288e9 // extra["state_bytes_per_instance"])
 
     def step(i):  # device-only work (capturable)
-        if stream is not None:
+        if pipe is not None:
+            pipe.fetch(*toks[i % 2])
+        elif stream is not None:
             inst, orc, vals = stream.batch(i)
             eng.apply_updates(inst, orc, vals)
             eng.run_round(only_touched=True)
         else:
             eng.touched.fill_(1)
             eng.run_round(only_touched=True)
+        if gov is not None:
+            gov.submit_tensors(*gov_batches[i % 2])
         dp.accumulate()
 
     for i in range(args.warmup):
@@ -92,7 +131,7 @@ def main():
     graph = None
     if args.graph:
         # the stream cycles with period `pool`: capture one period and replay it
-        period = stream.pool if stream is not None else 1
+        period = stream.pool if stream is not None else (2 if (pipe is not None or gov is not None) else 1)
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
@@ -150,7 +189,7 @@ def main():
                        "parallelism": f"dp{world}", "n_oracles": c["N"], "dimension": c["D"],
                        "n_failing": c["f"], "updates_per_instance_per_step": U_per_inst,
                        "oracle_updates_per_s": (U_per_inst * rounds / el) if U_per_inst else 0.0,
-                       "hip_graph": graph is not None, "ok_fraction": ok},
+                       "hip_graph": graph is not None, "ok_fraction": ok, **extra},
         }
         print(json.dumps(out))
     if world > 1:

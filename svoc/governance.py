@@ -129,6 +129,16 @@ class Governance:
             self.replacements += int(applied.sum())
         return status, applied
 
+    def submit_tensors(self, inst, caller, kind, arg0, arg1, addr):
+        """Low-level device path: one action per instance (instances must be unique), no host work."""
+        K = inst.numel()
+        st = torch.empty(K, dtype=torch.int32, device=self.device)
+        ap = torch.zeros(K, dtype=torch.uint8, device=self.device)
+        self._ops.governance(self.admins, self.oracle_addr, self.votes, self.prop_tag, self.prop_idx,
+                             self.prop_addr, inst, caller, kind, arg0, arg1, addr, self.enable, self.majority, st, ap)
+        self._oracle_cache = None
+        return st, ap
+
     # ------------------------------------------------------------------ getters
     def propositions(self, b: int) -> List[Optional[Tuple[int, int]]]:
         tag = self.prop_tag[b].cpu().tolist()
