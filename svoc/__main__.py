@@ -1,0 +1,42 @@
+"""``python -m svoc``: the reference client's CLI (client/main.py:14-74) on the local engine."""
+import argparse
+import sys
+
+from .cli import DIMENSION, Client
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="svoc oracle consensus client")
+    ap.add_argument("--disable_startup_fetch", action="store_true", default=False)
+    ap.add_argument("--dimension", type=int, default=DIMENSION)
+    ap.add_argument("--live_mode", action="store_true", default=False)
+    ap.add_argument("--scraper", action="store_true", default=False, help="append synthetic comments on fetch")
+    ap.add_argument("--rate", type=int, default=30 * 60, help="(kept for compatibility; no network)")
+    ap.add_argument("--device", default="cpu")
+    ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
+    ap.add_argument("--db", default=None, help="SQLite corpus (reference schema)")
+    ap.add_argument("--encoder", default="tiny", choices=["tiny", "base"])
+    ap.add_argument("-c", "--command", action="append", default=[], help="run a command and exit")
+    a = ap.parse_args(argv)
+    cl = Client(device=a.device, mode=a.mode, db_path=a.db, encoder=a.encoder, dimension=a.dimension)
+    cl.flags["scraper"] = a.scraper
+    cl.flags["live_mode"] = a.live_mode
+    if a.command:
+        for c in a.command:
+            print(cl.query(c))
+        return 0
+    if not a.disable_startup_fetch:
+        print(cl.query("resume"))
+        print(cl.query("fetch"))
+    while True:
+        try:
+            line = input("svoc> ")
+        except EOFError:
+            return 0
+        if line.strip() == "exit":
+            return 0
+        print(cl.query(line))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

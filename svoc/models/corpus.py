@@ -29,12 +29,28 @@ _WORDS = ("the a this that it is was not very really quite so just still rust py
           "believe argue agree disagree because but and or if when then however although").split()
 
 
+_MOODS = {
+    "optimism": "hopeful promising bright future improve better optimistic confident upside growth".split(),
+    "anger": "furious outraged angry rage unacceptable disgrace hostile livid scandal".split(),
+    "annoyance": "annoying irritating tedious again useless bloated slow broken meh".split(),
+    "excitement": "excited amazing wow incredible launch thrilled awesome finally breakthrough".split(),
+    "nervousness": "worried nervous anxious risky afraid uncertain scary concerned fragile".split(),
+    "remorse": "sorry regret apologize mistake my fault should have ashamed unfortunately".split(),
+}
+
+
 def synthetic_comments(n: int, seed: int = 0) -> List[str]:
+    """HN-like comments with a latent mood: each comment mixes neutral tech words with the words of
+    one dominant emotion (so even a random-init encoder sees systematically different inputs)."""
     rng = random.Random(seed)
+    moods = list(_MOODS)
     out = []
     for _ in range(n):
         k = rng.randint(8, 60)
-        out.append(" ".join(rng.choice(_WORDS) for _ in range(k)).capitalize() + ".")
+        mood = _MOODS[rng.choice(moods)]
+        share = rng.uniform(0.1, 0.7)
+        words = [rng.choice(mood) if rng.random() < share else rng.choice(_WORDS) for _ in range(k)]
+        out.append(" ".join(words).capitalize() + ".")
     return out
 
 

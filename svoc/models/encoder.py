@@ -43,6 +43,10 @@ class EncoderConfig:
     n_labels: int = 28
     layer_norm_eps: float = 1e-5
     pad_id: int = 1
+    # "cls" = RoBERTa's <s> head; "mean" = masked mean pooling.  With random weights the layers
+    # barely mix tokens, so the <s> state is ~input independent: mean pooling keeps the synthetic
+    # oracle scores content dependent (the default here, since no trained checkpoint is available).
+    pool: str = "mean"
 
     @classmethod
     def tiny(cls) -> "EncoderConfig":
@@ -80,6 +84,11 @@ class SentimentEncoder(nn.Module):
         self.dense = nn.Linear(c.hidden, c.hidden)      # RobertaClassificationHead: dense-tanh-out
         self.head = nn.Linear(c.hidden, c.n_labels)
         self.apply(self._init)
+        # random-init head scaled so the synthetic scores spread like a trained multi-label head's
+        # (larger logits than the default init): keeps honest bootstrap oracles distinguishable at wsad
+        # resolution, otherwise every column has ~zero variance and the contract reverts (§2.8-5)
+        nn.init.normal_(self.head.weight, std=6.0 / math.sqrt(c.hidden))
+        nn.init.normal_(self.dense.weight, std=3.0 / math.sqrt(c.hidden))
 
     @staticmethod
     def _init(m):
@@ -99,7 +108,12 @@ class SentimentEncoder(nn.Module):
             mask.masked_fill_(attention_mask[:, None, None, :] == 0, float("-inf"))
         for layer in self.layers:
             x = layer(x, mask)
-        h = torch.tanh(self.dense(x[:, 0]))
+        if self.cfg.pool == "cls" or attention_mask is None:
+            pooled = x[:, 0] if self.cfg.pool == "cls" else x.mean(1)
+        else:
+            m = attention_mask.to(x.dtype)[:, :, None]
+            pooled = (x * m).sum(1) / m.sum(1).clamp(min=1)
+        h = torch.tanh(self.dense(pooled))
         return torch.sigmoid(self.head(h).float())
 
 

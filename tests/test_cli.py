@@ -1,0 +1,29 @@
+"""Command router (client/web_interface.py:133-303 equivalents) on the local exact engine."""
+import pytest
+
+from svoc import ops as svops
+from svoc.cli import Client
+
+pytestmark = pytest.mark.skipif(not svops.available(), reason="svoc/_C.so not built")
+
+
+def test_fetch_commit_resume_governance(tmp_path):
+    cl = Client(device="cpu", mode="exact", db_path=str(tmp_path / "db.sqlite"), seed=1)
+    assert "optimism" in cl.query("fetch")
+    out = cl.query("commit")
+    assert out.count("NOT_ACTIVE") == 6 and "OK" in out.splitlines()[-1]
+    assert cl.query("is_consensus_active") == "True"
+    r = float(cl.query("reliability"))
+    assert 0.0 <= r <= 1.0
+    assert len(cl.query("oracle_list").splitlines()) == 7
+    assert cl.query("dimension") == "6"
+    assert cl.query("update_proposition 0 6 0x1234") == "proposition updated"
+    assert cl.query("vote_for_a_proposition 0 0 yes") == "vote recorded"
+    assert "replaced" in cl.query("vote_for_a_proposition 1 0 yes")
+    assert cl.query("oracle_list").splitlines()[6] == "0x1234"
+    assert cl.query("update_proposition 0 9 0x99").startswith("REVERT")
+    assert cl.query("save " + str(tmp_path / "c.svoc")).startswith("saved")
+    assert cl.query("load " + str(tmp_path / "c.svoc")).startswith("loaded")
+    assert cl.query("oracle_list").splitlines()[6] == "0x1234"
+    assert "unknown" in cl.query("frobnicate")
+    assert "Commands" in cl.query("help")
