@@ -41,8 +41,24 @@ SVOC_DEV uint32_t key_to_bf16x2(u16x2 k) {
   u16x2 s = __builtin_bit_cast(u16x2, __builtin_bit_cast(s16x2, nk) >> (short)15);
   return as_u32(k ^ (s | (unsigned short)0x8000));
 }
+// Constrained inputs are validated to [0, 1] (math.cairo:298-310), i.e. sign bit clear (or -0.0):
+// on that domain x ^ 0x8000 is an order-preserving bijection both ways (-0.0 -> key 0, below +0.0,
+// and back to -0.0) -- one v_xor_b32 instead of the general sign-magnitude mapping.
+SVOC_DEV u16x2 pos_to_key(uint32_t raw) { return as_k(raw ^ 0x80008000u); }
+SVOC_DEV uint32_t key_to_pos(u16x2 k) { return as_u32(k) ^ 0x80008000u; }
+
 SVOC_DEV float bf16_lo(uint32_t w) { return __builtin_bit_cast(float, w << 16); }
 SVOC_DEV float bf16_hi(uint32_t w) { return __builtin_bit_cast(float, w & 0xffff0000u); }
+
+// All-ones / zero lane masks built arithmetically (no v_cmp): a compare writes a VCC/SGPR pair, and
+// 64 unrolled rows of them exhaust the SGPR file (spills) and get hoisted out of loops.
+// (v_bfe_i32 keeps LLVM from canonicalising the arithmetic back into icmp + select.)
+SVOC_DEV uint32_t lt_mask(int i, int n) { return (uint32_t)__builtin_amdgcn_sbfe(i - n, 31, 1); }  // i < n
+SVOC_DEV uint32_t bit_mask(uint64_t m, int i) {  // bit i set
+  const uint32_t w = i < 32 ? (uint32_t)m : (uint32_t)(m >> 32);
+  return (uint32_t)__builtin_amdgcn_sbfe((int)w, i & 31, 1);
+}
+SVOC_DEV float fand(float x, uint32_t m) { return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, x) & m); }
 
 SVOC_DEV u16x2 shfl_xor_k(u16x2 v, int m) { return as_k((uint32_t)__shfl_xor((int)as_u32(v), m)); }
 SVOC_DEV u16x2 shfl_k(u16x2 v, int src) { return as_k((uint32_t)__shfl((int)as_u32(v), src)); }
@@ -157,6 +173,23 @@ SVOC_DEV u16x2 group_select(const u16x2 (&r)[64], int rank, int lane) {
   } else {
     const int owner = (rank >> 6) * P + (lane % P);
     return shfl_k(v, owner);
+  }
+}
+
+// The two middle order statistics of the group's sorted 64*NSEG keys when the sentinel padding has
+// been split so that they sit at fixed positions: (NPAD/2 - 1 - odd, NPAD/2 - odd).  No runtime
+// register indexing: one uniform select (NSEG = 1) or one select + one cross-lane read per value.
+template <int NSEG, int P>
+SVOC_DEV void middle_pair(const u16x2 (&r)[64], bool odd, int seg, int lane, u16x2& lo, u16x2& hi) {
+  if constexpr (NSEG == 1) {
+    lo = odd ? r[30] : r[31];
+    hi = odd ? r[31] : r[32];
+  } else {
+    constexpr int h = NSEG / 2;
+    const int pw = lane % P;
+    lo = shfl_k(odd ? r[62] : r[63], (h - 1) * P + pw);
+    const u16x2 c = seg == h - 1 ? r[63] : r[0];
+    hi = shfl_k(c, (odd ? h - 1 : h) * P + pw);
   }
 }
 

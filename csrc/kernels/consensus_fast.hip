@@ -307,6 +307,10 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
     }
     const int colA = col0 + 2 * cp;
     const bool vA = colA < D, vB = colA + 1 < D;
+    const uint32_t mA = vA ? 0xffffffffu : 0u, mB = vB ? 0xffffffffu : 0u;
+    uint64_t mm = mymask;  // opaque per-iteration copies: stop LICM from hoisting 64 row masks
+    int cntl = cnt;
+    asm volatile("" : "+v"(mm), "+v"(cntl));
     float shA, shB;
     float s1A = 0.f, s2A = 0.f, s3A = 0.f, s4A = 0.f, s1B = 0.f, s2B = 0.f, s3B = 0.f, s4B = 0.f;
     if (CONS) {
@@ -322,9 +326,11 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
       // moments straight from the sorted registers: positions < cnt are the reliable values
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
+        // sched_barrier every 8 rows: otherwise hipcc converts all 64 keys up front (+100 VGPRs)
+        if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
         const uint32_t w = key_to_bf16x2(r[i]);
-        const bool mk = i < cnt;
-        const float yA = mk ? bf16_lo(w) - shA : 0.f, yB = mk ? bf16_hi(w) - shB : 0.f;
+        const uint32_t mk = lt_mask(i, cntl);  // sorted positions >= cnt hold NaN sentinels
+        const float yA = fand(bf16_lo(w) - shA, mk), yB = fand(bf16_hi(w) - shB, mk);
         const float qA = yA * yA, qB = yB * yB;
         s1A += yA; s2A += qA; s3A = __builtin_fmaf(qA, yA, s3A); s4A = __builtin_fmaf(qA, qA, s4A);
         s1B += yB; s2B += qB; s3B = __builtin_fmaf(qB, yB, s3B); s4B = __builtin_fmaf(qB, qB, s4B);
@@ -336,7 +342,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         const uint32_t w = *(const uint32_t*)(smem + a0 + i * G::ROWB);
-        const bool mk = (mymask >> i) & 1;
+        const bool mk = (mm >> i) & 1;
         const float yA = mk ? bf16_lo(w) - shA : 0.f, yB = mk ? bf16_hi(w) - shB : 0.f;
         const float qA = yA * yA, qB = yB * yB;
         s1A += yA; s2A += qA; s3A = __builtin_fmaf(qA, yA, s3A); s4A = __builtin_fmaf(qA, qA, s4A);
@@ -408,8 +414,13 @@ using namespace svoc;
 // Picks the lane-group geometry from N (rows) and D (columns):
 //   N <= 64  -> 1 lane per column pair; 8 waves when the whole instance fits one 128-KiB slab.
 //   N <= 128 -> 2 lanes; N <= 256 -> 4 lanes (4 waves, 64-KiB slabs, 2 workgroups per CU).
+extern "C" int svoc_fast_round_bf16_reg(const FastParams* p, hipStream_t stream);
+
 extern "C" int svoc_fast_round_bf16(const FastParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
+  // default (0) and negative hints: register-streaming kernel (consensus_fast_reg.hip; -1 = split
+  // into two launches).  Positive hints select this LDS-tiled kernel (1 = its default geometry).
+  if (p->wave_hint <= 0) return svoc_fast_round_bf16_reg(p, stream);
   if (p->N < 2 || p->N > 256 || p->ld % 8 != 0 || p->D > p->ld) return -1;
   if (p->N <= 64) {
     // wave_hint: 2 / 4 / 8 waves per workgroup = 256 / 512 / 1024-column slabs (32/64/128 KiB LDS)

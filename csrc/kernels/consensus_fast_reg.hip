@@ -1,0 +1,404 @@
+// Fused two-pass robust consensus, fast mode, "register-streaming" variant: no LDS tile.
+//
+// Same semantics and outputs as consensus_fast.hip (contract/src/contract.cairo:442-503 /
+// :370-434; see that file).  Difference: every lane loads its column-pair segment (64 rows x 2
+// bf16 = one dword per row) straight from HBM/L2 into VGPRs, so the workgroup holds no [N x W] LDS
+// tile and there is no slab barrier: occupancy is set by VGPRs only (the LDS tile capped the tiled
+// kernel at 2 workgroups per CU), and waves drift freely so one wave's loads overlap another's
+// sorting network.  The qr pass re-reads the same dwords (L2/MALL-hot, just touched); pass 2 reads
+// the instance again, with unreliable rows turned into max-key sentinels by a register OR.
+// LDS holds only the per-wave qr partials, the reduced qr, the reliable bitmask and the status.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "svoc/launch.hpp"
+#include "svoc/sortnet.hpp"
+#include "svoc/status.hpp"
+
+namespace svoc {
+
+// Buffer resource over one instance: row offsets ride in SGPRs (soffset), the lane's column-pair
+// offset in one VGPR (voffset); rows past N fall outside num_records and read as 0 (no clamping).
+SVOC_DEV __amdgpu_buffer_rsrc_t instance_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t pa = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pa);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+SVOC_DEV uint32_t bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+}
+
+// MODE 0: fused round; 1: pass 1 only (c1 + qr -> global); 2: rank + pass 2 from the global qr.
+// The default launch runs MODE 1 then MODE 2: each half gets its own register allocation (~110
+// VGPRs instead of ~230 for the fused body), i.e. twice the resident waves per SIMD.
+template <bool CONS>
+SVOC_DEV u16x2 to_key(uint32_t raw) {
+  if constexpr (CONS) return pos_to_key(raw);
+  else return bf16x2_to_key(raw);
+}
+template <bool CONS>
+SVOC_DEV uint32_t from_key(u16x2 k) {
+  if constexpr (CONS) return key_to_pos(k);
+  else return key_to_bf16x2(k);
+}
+
+template <int NSEG, int WAVES, bool CONS, int MODE>
+__global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastParams p) {
+  constexpr int P = 64 / NSEG;          // column pairs per wave
+  constexpr int NPAD = 64 * NSEG;       // padded oracle rows
+  constexpr int W = WAVES * P * 2;      // columns per workgroup step
+  constexpr int NT = WAVES * 64;
+  constexpr int KEEP = 64 / P;
+  __shared__ float qr_part[WAVES * NPAD];
+  __shared__ float qr_lds[NPAD];
+  __shared__ uint64_t relmask[4];
+  __shared__ uint64_t lowmask[4];  // non-reliable rows turned into -inf sentinels (pass 2)
+  __shared__ float misc_f[2];
+  __shared__ int misc_i[2];
+
+  const int b = blockIdx.x;
+  if (p.active && !p.active[b]) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int seg = lane / P, pair_w = lane % P;
+  const int cp = wave * P + pair_w;
+  const int N = p.N, D = p.D;
+  const int rowb = p.ld * 2;  // row stride in bytes
+  const uint16_t* inst = (const uint16_t*)p.values + (int64_t)b * p.inst_stride;
+  const __amdgpu_buffer_rsrc_t rs = instance_rsrc(inst, (uint32_t)(N * rowb));
+  const int nslab = (D + W - 1) / W;
+  // sentinel split (pass 1): rows >= N are padding; the first lo1 of them become -inf (key 0), the
+  // rest +inf (key 0xFFFF), so the smooth-median ranks N/2-1, N/2 (math.cairo:118-119) always land
+  // on the fixed positions NPAD/2-1-odd, NPAD/2-odd of the sorted sequence
+  const int lo1 = (NPAD - N) >> 1;
+  const int nv = N - seg * 64;          // rows < nv are real
+  const int nl = N + lo1 - seg * 64;    // rows in [nv, nl) are -inf, rows >= nl are +inf
+  const bool odd1 = N & 1;
+  const int seg_off = seg * 64 * rowb;  // this lane's first row (bytes)
+
+  float acc[KEEP];
+#pragma unroll
+  for (int i = 0; i < KEEP; ++i) acc[i] = 0.f;
+
+  // ------------------------------------------------------------ pass 1
+  const int pass1_slabs = MODE == 2 ? 0 : nslab;
+#pragma nounroll
+  for (int s = 0; s < pass1_slabs; ++s) {
+    const int colA = s * W + 2 * cp;
+    const bool vA = colA < D, vB = colA + 1 < D;
+    const int vo = seg_off + (vA ? colA * 2 : 0);
+    // opaque per-iteration copy: otherwise LICM hoists the 64 row masks out of the slab loop and
+    // keeps them live in 64 VGPRs (+ their SGPR twins), doubling the register footprint
+    int nvl = nv, nll = nl;
+    asm volatile("" : "+v"(nvl), "+v"(nll));
+    float cA, cB;
+    {
+      u16x2 r[64];
+      if (N == NPAD) {  // uniform: no padding rows
+#pragma unroll
+        for (int i = 0; i < 64; ++i) r[i] = to_key<CONS>(bload(rs, vo, i * rowb));
+      } else {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          const uint32_t hi_m = ~lt_mask(i, nll);
+          r[i] = as_k((as_u32(to_key<CONS>(bload(rs, vo, i * rowb))) & (lt_mask(i, nvl) | hi_m)) | hi_m);
+        }
+      }
+      sort_group<NSEG, P>(r, seg);
+      u16x2 klo, khi;
+      middle_pair<NSEG, P>(r, odd1, seg, lane, klo, khi);
+      const uint32_t lo = from_key<CONS>(klo), hi = from_key<CONS>(khi);
+      cA = 0.5f * (bf16_lo(lo) + bf16_lo(hi));
+      cB = 0.5f * (bf16_hi(lo) + bf16_hi(hi));
+    }
+    if (seg == 0) {
+      if (vA) p.c1[(int64_t)b * D + colA] = cA;
+      if (vB) p.c1[(int64_t)b * D + colA + 1] = cB;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    float part[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      const uint32_t w = bload(rs, vo, i * rowb);  // L2/MALL-hot re-read
+      const float yA = vA ? bf16_lo(w) - cA : 0.f;
+      const float yB = vB ? bf16_hi(w) - cB : 0.f;
+      part[i] = __builtin_fmaf(yA, yA, yB * yB);
+    }
+#pragma unroll
+    for (int h = 32, msk = P / 2; msk >= 1; h >>= 1, msk >>= 1) {
+      const bool up = (lane & msk) != 0;
+#pragma unroll
+      for (int i = 0; i < h; ++i) {
+        const float lo_v = part[i], hi_v = part[i + h];
+        const float send = up ? lo_v : hi_v;
+        const float keep = up ? hi_v : lo_v;
+        part[i] = keep + __shfl_xor(send, msk);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < KEEP; ++i) acc[i] += part[i];
+  }
+
+  // ------------------------------------------------------------ qr reduction
+  {
+    int base = 0;
+#pragma unroll
+    for (int h = 32, msk = P / 2; msk >= 1; h >>= 1, msk >>= 1) base += (lane & msk) ? h : 0;
+#pragma unroll
+    for (int i = 0; i < KEEP; ++i) qr_part[wave * NPAD + seg * 64 + base + i] = acc[i];
+  }
+  __syncthreads();
+  for (int t = tid; t < NPAD; t += NT) {
+    float q = 0.f;
+    if (MODE == 2) {
+      q = t < N ? p.qr[(int64_t)b * N + t] : 0.f;
+    } else {
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) q += qr_part[w * NPAD + t];
+    }
+    qr_lds[t] = q;
+  }
+  __syncthreads();
+  if (MODE == 1) {
+    for (int t = tid; t < N; t += NT) p.qr[(int64_t)b * N + t] = qr_lds[t];
+    if (tid == 0) p.status[b] = ST_OK;
+    return;
+  }
+
+  // ------------------------------------------------------------ rank mask (contract.cairo:345-363)
+  const int R = N - p.n_failing;
+  for (int base = 0; base < NPAD; base += NT) {  // NT >= 64: one ballot word per wave-chunk
+    const int t = base + tid;
+    bool rel = false;
+    float myq = 0.f;
+    if (t < N) {
+      myq = qr_lds[t];
+      int rank = 0;
+      const int n4 = N & ~3;
+      for (int j = 0; j < n4; j += 4) {
+        const float4 q4 = *(const float4*)(qr_lds + j);
+        rank += (q4.x < myq || (q4.x == myq && j > t)) ? 1 : 0;
+        rank += (q4.y < myq || (q4.y == myq && j + 1 > t)) ? 1 : 0;
+        rank += (q4.z < myq || (q4.z == myq && j + 2 > t)) ? 1 : 0;
+        rank += (q4.w < myq || (q4.w == myq && j + 3 > t)) ? 1 : 0;
+      }
+      for (int j = n4; j < N; ++j) {
+        const float qj = qr_lds[j];
+        rank += (qj < myq || (qj == myq && j > t)) ? 1 : 0;
+      }
+      rel = rank < R;
+    }
+    const uint64_t bal = __ballot(rel);
+    if (lane == 0 && (t >> 6) < 4) relmask[t >> 6] = bal;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float s_all = 0.f, s_rel = 0.f;
+    for (int t = tid; t < N; t += 64) {
+      const float q = qr_lds[t];
+      s_all += q;
+      s_rel += ((relmask[t >> 6] >> (t & 63)) & 1) ? q : 0.f;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      s_all += __shfl_xor(s_all, o);
+      s_rel += __shfl_xor(s_rel, o);
+    }
+    if (tid == 0) {
+      // pass-2 sentinel split: the first (NPAD - R) / 2 non-reliable rows become -inf
+      int need = (NPAD - (N - p.n_failing)) >> 1;
+      for (int w = 0; w < 4; ++w) {
+        uint64_t nr = w < NSEG ? ~relmask[w] : 0ull, lm = 0ull;
+        while (need > 0 && nr) {
+          const uint64_t bit = nr & (0ull - nr);
+          lm |= bit;
+          nr ^= bit;
+          --need;
+        }
+        lowmask[w] = lm;
+      }
+      int st = ST_OK;
+      const float rd = (float)(p.rel_dim > 0 ? p.rel_dim : D);
+      float rel1, rel2 = 0.f;
+      if (CONS) rel1 = 1.f - 2.f * sqrtf(s_all / (float)N / rd);
+      else rel1 = 1.f - fminf(p.max_spread, sqrtf(s_all / (float)N)) / p.max_spread;
+      if (!(rel1 >= 0.f && rel1 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
+      else if (R < 2) st = R <= 0 ? ST_USIZE_UNDERFLOW : ST_INDEX_OOB;
+      else {
+        if (CONS) rel2 = 1.f - 2.f * sqrtf(s_rel / (float)R / rd);
+        else rel2 = 1.f - fminf(p.max_spread, sqrtf(s_rel / (float)R)) / p.max_spread;
+        if (!(rel2 >= 0.f && rel2 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
+        else if (R < 4) st = ST_TOO_FEW_RELIABLE;
+      }
+      misc_f[0] = rel1;
+      misc_f[1] = rel2;
+      misc_i[0] = st;
+      misc_i[1] = 0;
+    }
+  }
+  __syncthreads();
+  if (misc_i[0] != ST_OK) {
+    if (tid == 0) p.status[b] = misc_i[0];
+    return;
+  }
+  for (int t = tid; t < N; t += NT) {
+    p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
+    p.qr[(int64_t)b * N + t] = qr_lds[t];
+  }
+  const float n = (float)R;
+  const int lo2 = (NPAD - R) >> 1;
+  const int ra = lo2 - seg * 64;        // sorted positions [ra, ra + R) hold the reliable values
+  const uint64_t mymask = relmask[seg];
+  const uint64_t mylow = lowmask[seg];
+  const bool odd2 = R & 1;
+  int first_rel = 0;
+  if (!CONS) {
+    for (int w = 0; w < 4; ++w)
+      if (relmask[w]) { first_rel = 64 * w + __builtin_ctzll(relmask[w]); break; }
+  }
+
+  // ------------------------------------------------------------ pass 2 (contract.cairo:476-500)
+#pragma nounroll
+  for (int s = 0; s < nslab; ++s) {
+    const int colA = s * W + 2 * cp;
+    const bool vA = colA < D, vB = colA + 1 < D;
+    const int vo = seg_off + (vA ? colA * 2 : 0);
+    const uint32_t mA = vA ? 0xffffffffu : 0u, mB = vB ? 0xffffffffu : 0u;
+    uint64_t mm = mymask, ml = mylow;
+    int ral = ra;
+    asm volatile("" : "+v"(mm), "+v"(ml), "+v"(ral));
+    float shA, shB;
+    float s1A = 0.f, s2A = 0.f, s3A = 0.f, s4A = 0.f, s1B = 0.f, s2B = 0.f, s3B = 0.f, s4B = 0.f;
+    if (CONS) {
+      u16x2 r[64];
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const uint32_t rm = bit_mask(mm, i), lm = bit_mask(ml, i);
+        r[i] = as_k((as_u32(pos_to_key(bload(rs, vo, i * rowb))) & rm) | ~(rm | lm));
+      }
+      sort_group<NSEG, P>(r, seg);
+      u16x2 klo, khi;
+      middle_pair<NSEG, P>(r, odd2, seg, lane, klo, khi);
+      const uint32_t lo = key_to_pos(klo), hi = key_to_pos(khi);
+      shA = 0.5f * (bf16_lo(lo) + bf16_lo(hi));
+      shB = 0.5f * (bf16_hi(lo) + bf16_hi(hi));
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        uint32_t w = as_u32(r[i]);
+        int ti = i - ral;
+        // keep the accumulation in row order: no SLP pairing / early key conversion of all 64 rows
+        asm volatile("" : "+v"(w), "+v"(ti), "+v"(s1A), "+v"(s1B), "+v"(s2A), "+v"(s2B), "+v"(s3A), "+v"(s3B),
+                     "+v"(s4A), "+v"(s4B));
+        w ^= 0x80008000u;                      // key_to_pos
+        const uint32_t mk = ~lt_mask(ti, 0) & lt_mask(ti, R);  // sentinels outside [ra, ra+R)
+        const float yA = fand(bf16_lo(w) - shA, mk), yB = fand(bf16_hi(w) - shB, mk);
+        const float qA = yA * yA, qB = yB * yB;
+        s1A += yA; s2A += qA; s3A = __builtin_fmaf(qA, yA, s3A); s4A = __builtin_fmaf(qA, qA, s4A);
+        s1B += yB; s2B += qB; s3B = __builtin_fmaf(qB, yB, s3B); s4B = __builtin_fmaf(qB, qB, s4B);
+      }
+    } else {
+      const uint32_t w0 = bload(rs, vA ? colA * 2 : 0, first_rel * rowb);
+      shA = bf16_lo(w0);
+      shB = bf16_hi(w0);
+      uint32_t wv[64];
+#pragma unroll
+      for (int i = 0; i < 64; ++i) wv[i] = bload(rs, vo, i * rowb);
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        uint32_t w = wv[i];
+        asm volatile("" : "+v"(w), "+v"(s1A), "+v"(s1B), "+v"(s2A), "+v"(s2B), "+v"(s3A), "+v"(s3B),
+                     "+v"(s4A), "+v"(s4B));
+        const uint32_t mk = bit_mask(mm, i);
+        const float yA = fand(bf16_lo(w) - shA, mk & mA), yB = fand(bf16_hi(w) - shB, mk & mB);
+        const float qA = yA * yA, qB = yB * yB;
+        s1A += yA; s2A += qA; s3A = __builtin_fmaf(qA, yA, s3A); s4A = __builtin_fmaf(qA, qA, s4A);
+        s1B += yB; s2B += qB; s3B = __builtin_fmaf(qB, yB, s3B); s4B = __builtin_fmaf(qB, qB, s4B);
+      }
+    }
+#pragma unroll
+    for (int t = 1; t < NSEG; t <<= 1) {
+      s1A += __shfl_xor(s1A, t * P); s2A += __shfl_xor(s2A, t * P);
+      s3A += __shfl_xor(s3A, t * P); s4A += __shfl_xor(s4A, t * P);
+      s1B += __shfl_xor(s1B, t * P); s2B += __shfl_xor(s2B, t * P);
+      s3B += __shfl_xor(s3B, t * P); s4B += __shfl_xor(s4B, t * P);
+    }
+    if (seg == 0) {
+      const float k3 = n / ((n - 1.f) * (n - 2.f));
+      const float k4a = n * (n + 1.f) / (n - 1.f), k4b = 3.f * (n - 1.f) * (n - 1.f), k4c = (n - 2.f) * (n - 3.f);
+      bool zv = false;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const bool v = h ? vB : vA;
+        if (!v) continue;
+        const float s1 = h ? s1B : s1A, s2 = h ? s2B : s2A, s3 = h ? s3B : s3A, s4 = h ? s4B : s4A;
+        const float sh = h ? shB : shA;
+        const float dl = s1 / n, e2 = s2 / n, e3 = s3 / n, e4 = s4 / n;
+        const float mu2 = e2 - dl * dl;
+        const float mu3 = e3 - 3.f * dl * e2 + 2.f * dl * dl * dl;
+        const float mu4 = e4 - 4.f * dl * e3 + 6.f * dl * dl * e2 - 3.f * dl * dl * dl * dl;
+        float sk = 0.f, ku = 0.f;
+        if (mu2 > 0.f) {
+          const float sd = sqrtf(mu2);
+          const float z3 = n * mu3 / (mu2 * sd), z4 = n * mu4 / (mu2 * mu2);
+          sk = z3 * k3;
+          ku = (z4 * k4a - k4b) / k4c;
+        } else {
+          zv = true;
+        }
+        const int64_t o = (int64_t)b * D + colA + h;
+        p.consensus[o] = CONS ? sh : sh + dl;
+        p.skew[o] = sk;
+        p.kurt[o] = ku;
+      }
+      if (zv) misc_i[1] = 1;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    p.rel[2 * (int64_t)b] = misc_f[0];
+    p.rel[2 * (int64_t)b + 1] = misc_f[1];
+    p.status[b] = misc_i[1] ? ST_ZERO_VARIANCE : ST_OK;
+  }
+}
+
+template <int NSEG, int WAVES, int MODE>
+static void launch_reg_mode(const FastParams& p, hipStream_t stream) {
+  auto k = p.constrained ? consensus_fast_reg_kernel<NSEG, WAVES, true, MODE>
+                         : consensus_fast_reg_kernel<NSEG, WAVES, false, MODE>;
+  hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+}
+
+template <int NSEG, int WAVES>
+static int launch_reg(const FastParams& p, hipStream_t stream) {
+  if (p.mode == 1) {
+    launch_reg_mode<NSEG, WAVES, 1>(p, stream);
+  } else if (p.mode == 2) {
+    launch_reg_mode<NSEG, WAVES, 2>(p, stream);
+  } else if (p.wave_hint != -1) {
+    launch_reg_mode<NSEG, WAVES, 0>(p, stream);  // fused single launch (default)
+  } else {
+    launch_reg_mode<NSEG, WAVES, 1>(p, stream);  // split: pass 1 ...
+    launch_reg_mode<NSEG, WAVES, 2>(p, stream);  // ... then rank + pass 2
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace svoc
+
+using namespace svoc;
+
+extern "C" int svoc_fast_round_bf16_reg(const FastParams* p, hipStream_t stream) {
+  if (p->B <= 0) return 0;
+  if (p->N < 2 || p->N > 256 || p->ld % 8 != 0 || p->D > p->ld) return -1;
+  // wave_hint -3 / -4: 8 / 2 waves per workgroup (fused); default 4 (16 waves per CU at <= 128 VGPRs)
+  if (p->N <= 64) {
+    if (p->wave_hint == -3) return launch_reg<1, 8>(*p, stream);
+    if (p->wave_hint == -4) return launch_reg<1, 2>(*p, stream);
+    return launch_reg<1, 4>(*p, stream);
+  }
+  if (p->N <= 128) return launch_reg<2, 4>(*p, stream);
+  return launch_reg<4, 4>(*p, stream);
+}

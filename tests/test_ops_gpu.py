@@ -23,10 +23,16 @@ def _cmp_fast(o, r, ok):
     torch.testing.assert_close(o["kurt"][ok], r["kurt"][ok], rtol=2e-3, atol=5e-3)
 
 
-@pytest.mark.parametrize("N,D,f,constrained,hint", [
-    (7, 6, 2, True, 0), (64, 1024, 8, True, 8), (64, 1024, 8, True, 0), (64, 1000, 8, False, 0),
-    (50, 300, 5, True, 0), (128, 512, 16, True, 0), (100, 260, 10, False, 0),
-    (256, 4096, 32, True, 0), (256, 600, 32, False, 0), (200, 136, 20, True, 0), (20, 8, 15, True, 0)])
+_SHAPES = [(7, 6, 2, True), (64, 1024, 8, True), (64, 1000, 8, False), (50, 300, 5, True),
+           (128, 512, 16, True), (100, 260, 10, False), (256, 4096, 32, True), (256, 600, 32, False),
+           (200, 136, 20, True), (20, 8, 15, True)]
+
+
+# hint 0: register-streaming fused kernel (default); -1: its split two-launch form; -3 / -4: 8 / 2
+# waves per workgroup; 1 / 2 / 8: the LDS-tiled kernel (consensus_fast.hip)
+@pytest.mark.parametrize("N,D,f,constrained,hint",
+                         [s + (h,) for s in _SHAPES for h in (0, -1, 1)]
+                         + [(64, 1024, 8, True, h) for h in (-3, -4, 2, 8)] + [(33, 70, 4, False, h) for h in (-3, -4)])
 def test_fast_hip_vs_torch(N, D, f, constrained, hint):
     B = 12
     x, _ = beta_oracles(B, N, D, f, seed=7 * N + D)
