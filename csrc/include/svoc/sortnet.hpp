@@ -87,6 +87,40 @@ SVOC_DEV void sort64(u16x2 (&r)[64]) {
   }
 }
 
+// Batcher's odd-even merge sort of the 64 registers of one lane: 543 compare-exchanges instead of
+// bitonic's 672, and when only a few outputs are consumed (the two middle order statistics) dead
+// code elimination prunes it to ~414 (bitonic: 543).  The comparator list is a compile-time table;
+// the fully unrolled loop indexes registers with constants only.
+struct CmpNet64 {
+  unsigned char a[543], b[543];
+  int n;
+};
+constexpr CmpNet64 make_oem64() {
+  CmpNet64 t{};
+  int c = 0;
+  for (int p = 1; p < 64; p <<= 1)
+    for (int k = p; k >= 1; k >>= 1)
+      for (int j = k % p; j + k < 64; j += 2 * k)
+        for (int i = 0; i < k && i + j + k < 64; ++i)
+          if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+            t.a[c] = (unsigned char)(i + j);
+            t.b[c] = (unsigned char)(i + j + k);
+            ++c;
+          }
+  t.n = c;
+  return t;
+}
+SVOC_DEV void sort64_oem(u16x2 (&r)[64]) {
+  constexpr CmpNet64 T = make_oem64();
+  static_assert(T.n == 543, "odd-even merge sort of 64");
+#pragma unroll
+  for (int c = 0; c < 543; ++c) {
+    const u16x2 x = r[T.a[c]], y = r[T.b[c]];
+    r[T.a[c]] = kmin(x, y);
+    r[T.b[c]] = kmax(x, y);
+  }
+}
+
 // Ascending half-cleaner cascade (strides 32..1): sorts a bitonic lane-local sequence.
 SVOC_DEV void merge64(u16x2 (&r)[64]) {
 #pragma unroll
@@ -128,7 +162,7 @@ SVOC_DEV void xlane_hc(u16x2 (&r)[64], int xmask, bool upper) {
 // Sort 64*NSEG keys (x2 columns) spread over the NSEG lanes of a group. P = pairs per wave.
 template <int NSEG, int P>
 SVOC_DEV void sort_group(u16x2 (&r)[64], int seg) {
-  sort64(r);
+  sort64_oem(r);
 #pragma unroll
   for (int s = 2; s <= NSEG; s <<= 1) {
     xlane_flip(r, (s - 1) * P, (seg & (s >> 1)) != 0);
@@ -177,19 +211,18 @@ SVOC_DEV u16x2 group_select(const u16x2 (&r)[64], int rank, int lane) {
 }
 
 // The two middle order statistics of the group's sorted 64*NSEG keys when the sentinel padding has
-// been split so that they sit at fixed positions: (NPAD/2 - 1 - odd, NPAD/2 - odd).  No runtime
-// register indexing: one uniform select (NSEG = 1) or one select + one cross-lane read per value.
+// been split so that they sit at the fixed positions NPAD/2 - 1 and NPAD/2: no runtime register
+// indexing, at most one cross-lane read per value.
 template <int NSEG, int P>
-SVOC_DEV void middle_pair(const u16x2 (&r)[64], bool odd, int seg, int lane, u16x2& lo, u16x2& hi) {
+SVOC_DEV void middle_pair(const u16x2 (&r)[64], int seg, int lane, u16x2& lo, u16x2& hi) {
   if constexpr (NSEG == 1) {
-    lo = odd ? r[30] : r[31];
-    hi = odd ? r[31] : r[32];
+    lo = r[31];
+    hi = r[32];
   } else {
     constexpr int h = NSEG / 2;
     const int pw = lane % P;
-    lo = shfl_k(odd ? r[62] : r[63], (h - 1) * P + pw);
-    const u16x2 c = seg == h - 1 ? r[63] : r[0];
-    hi = shfl_k(c, (odd ? h - 1 : h) * P + pw);
+    lo = shfl_k(r[63], (h - 1) * P + pw);
+    hi = shfl_k(r[0], h * P + pw);
   }
 }
 

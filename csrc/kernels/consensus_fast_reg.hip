@@ -69,13 +69,14 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
   const uint16_t* inst = (const uint16_t*)p.values + (int64_t)b * p.inst_stride;
   const __amdgpu_buffer_rsrc_t rs = instance_rsrc(inst, (uint32_t)(N * rowb));
   const int nslab = (D + W - 1) / W;
-  // sentinel split (pass 1): rows >= N are padding; the first lo1 of them become -inf (key 0), the
-  // rest +inf (key 0xFFFF), so the smooth-median ranks N/2-1, N/2 (math.cairo:118-119) always land
-  // on the fixed positions NPAD/2-1-odd, NPAD/2-odd of the sorted sequence
-  const int lo1 = (NPAD - N) >> 1;
+  // sentinel split (pass 1): rows >= N are padding; the first lo1 = ceil((NPAD-N)/2) of them become
+  // -inf (key 0), the rest +inf (key 0xFFFF), so the smooth-median ranks N/2-1, N/2 (math.cairo:
+  // 118-119, floor division for odd N too) always land on positions NPAD/2-1, NPAD/2 of the sorted
+  // sequence: only those two network outputs are consumed, and dead-code elimination prunes the
+  // sorting network down to a median selection network
+  const int lo1 = (NPAD - N + 1) >> 1;
   const int nv = N - seg * 64;          // rows < nv are real
   const int nl = N + lo1 - seg * 64;    // rows in [nv, nl) are -inf, rows >= nl are +inf
-  const bool odd1 = N & 1;
   const int seg_off = seg * 64 * rowb;  // this lane's first row (bytes)
 
   float acc[KEEP];
@@ -108,7 +109,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
       }
       sort_group<NSEG, P>(r, seg);
       u16x2 klo, khi;
-      middle_pair<NSEG, P>(r, odd1, seg, lane, klo, khi);
+      middle_pair<NSEG, P>(r, seg, lane, klo, khi);
       const uint32_t lo = from_key<CONS>(klo), hi = from_key<CONS>(khi);
       cA = 0.5f * (bf16_lo(lo) + bf16_lo(hi));
       cB = 0.5f * (bf16_hi(lo) + bf16_hi(hi));
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
     }
     if (tid == 0) {
       // pass-2 sentinel split: the first (NPAD - R) / 2 non-reliable rows become -inf
-      int need = (NPAD - (N - p.n_failing)) >> 1;
+      int need = (NPAD - (N - p.n_failing) + 1) >> 1;
       for (int w = 0; w < 4; ++w) {
         uint64_t nr = w < NSEG ? ~relmask[w] : 0ull, lm = 0ull;
         while (need > 0 && nr) {
@@ -248,16 +249,11 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
     p.qr[(int64_t)b * N + t] = qr_lds[t];
   }
   const float n = (float)R;
-  const int lo2 = (NPAD - R) >> 1;
-  const int ra = lo2 - seg * 64;        // sorted positions [ra, ra + R) hold the reliable values
   const uint64_t mymask = relmask[seg];
   const uint64_t mylow = lowmask[seg];
-  const bool odd2 = R & 1;
   int first_rel = 0;
-  if (!CONS) {
-    for (int w = 0; w < 4; ++w)
-      if (relmask[w]) { first_rel = 64 * w + __builtin_ctzll(relmask[w]); break; }
-  }
+  for (int w = 0; w < 4; ++w)
+    if (relmask[w]) { first_rel = 64 * w + __builtin_ctzll(relmask[w]); break; }
 
   // ------------------------------------------------------------ pass 2 (contract.cairo:476-500)
 #pragma nounroll
@@ -265,58 +261,43 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
     const int colA = s * W + 2 * cp;
     const bool vA = colA < D, vB = colA + 1 < D;
     const int vo = seg_off + (vA ? colA * 2 : 0);
-    const uint32_t mA = vA ? 0xffffffffu : 0u, mB = vB ? 0xffffffffu : 0u;
     uint64_t mm = mymask, ml = mylow;
-    int ral = ra;
-    asm volatile("" : "+v"(mm), "+v"(ml), "+v"(ral));
-    float shA, shB;
+    asm volatile("" : "+v"(mm), "+v"(ml));
+    // shifted power sums (shift = the first reliable row: no cancellation for clustered columns)
+    const uint32_t w0 = bload(rs, vA ? colA * 2 : 0, first_rel * rowb);
+    const float shA = bf16_lo(w0), shB = bf16_hi(w0);
     float s1A = 0.f, s2A = 0.f, s3A = 0.f, s4A = 0.f, s1B = 0.f, s2B = 0.f, s3B = 0.f, s4B = 0.f;
+    uint32_t wv[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) wv[i] = bload(rs, vo, i * rowb);
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      uint32_t w = wv[i];
+      // row-ordered accumulation: keeps LLVM from pairing / front-loading all 64 rows (VGPRs)
+      asm volatile("" : "+v"(w), "+v"(s1A), "+v"(s1B), "+v"(s2A), "+v"(s2B), "+v"(s3A), "+v"(s3B),
+                   "+v"(s4A), "+v"(s4B));
+      const uint32_t mk = bit_mask(mm, i);
+      const float yA = fand(bf16_lo(w) - shA, mk), yB = fand(bf16_hi(w) - shB, mk);
+      const float qA = yA * yA, qB = yB * yB;
+      s1A += yA; s2A += qA; s3A = __builtin_fmaf(qA, yA, s3A); s4A = __builtin_fmaf(qA, qA, s4A);
+      s1B += yB; s2B += qB; s3B = __builtin_fmaf(qB, yB, s3B); s4B = __builtin_fmaf(qB, qB, s4B);
+      if (CONS) {
+        // reliable rows keep their key; non-reliable rows become -inf (lowmask) / +inf sentinels
+        const uint32_t lm = bit_mask(ml, i);
+        wv[i] = (as_u32(pos_to_key(w)) & mk) | ~(mk | lm);
+      }
+    }
+    float cA = 0.f, cB = 0.f;  // pass-2 smooth median (constrained consensus)
     if (CONS) {
       u16x2 r[64];
 #pragma unroll
-      for (int i = 0; i < 64; ++i) {
-        const uint32_t rm = bit_mask(mm, i), lm = bit_mask(ml, i);
-        r[i] = as_k((as_u32(pos_to_key(bload(rs, vo, i * rowb))) & rm) | ~(rm | lm));
-      }
-      sort_group<NSEG, P>(r, seg);
+      for (int i = 0; i < 64; ++i) r[i] = as_k(wv[i]);
+      sort_group<NSEG, P>(r, seg);   // only the two middle outputs are live: pruned to a selection
       u16x2 klo, khi;
-      middle_pair<NSEG, P>(r, odd2, seg, lane, klo, khi);
+      middle_pair<NSEG, P>(r, seg, lane, klo, khi);
       const uint32_t lo = key_to_pos(klo), hi = key_to_pos(khi);
-      shA = 0.5f * (bf16_lo(lo) + bf16_lo(hi));
-      shB = 0.5f * (bf16_hi(lo) + bf16_hi(hi));
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int i = 0; i < 64; ++i) {
-        uint32_t w = as_u32(r[i]);
-        int ti = i - ral;
-        // keep the accumulation in row order: no SLP pairing / early key conversion of all 64 rows
-        asm volatile("" : "+v"(w), "+v"(ti), "+v"(s1A), "+v"(s1B), "+v"(s2A), "+v"(s2B), "+v"(s3A), "+v"(s3B),
-                     "+v"(s4A), "+v"(s4B));
-        w ^= 0x80008000u;                      // key_to_pos
-        const uint32_t mk = ~lt_mask(ti, 0) & lt_mask(ti, R);  // sentinels outside [ra, ra+R)
-        const float yA = fand(bf16_lo(w) - shA, mk), yB = fand(bf16_hi(w) - shB, mk);
-        const float qA = yA * yA, qB = yB * yB;
-        s1A += yA; s2A += qA; s3A = __builtin_fmaf(qA, yA, s3A); s4A = __builtin_fmaf(qA, qA, s4A);
-        s1B += yB; s2B += qB; s3B = __builtin_fmaf(qB, yB, s3B); s4B = __builtin_fmaf(qB, qB, s4B);
-      }
-    } else {
-      const uint32_t w0 = bload(rs, vA ? colA * 2 : 0, first_rel * rowb);
-      shA = bf16_lo(w0);
-      shB = bf16_hi(w0);
-      uint32_t wv[64];
-#pragma unroll
-      for (int i = 0; i < 64; ++i) wv[i] = bload(rs, vo, i * rowb);
-#pragma unroll
-      for (int i = 0; i < 64; ++i) {
-        uint32_t w = wv[i];
-        asm volatile("" : "+v"(w), "+v"(s1A), "+v"(s1B), "+v"(s2A), "+v"(s2B), "+v"(s3A), "+v"(s3B),
-                     "+v"(s4A), "+v"(s4B));
-        const uint32_t mk = bit_mask(mm, i);
-        const float yA = fand(bf16_lo(w) - shA, mk & mA), yB = fand(bf16_hi(w) - shB, mk & mB);
-        const float qA = yA * yA, qB = yB * yB;
-        s1A += yA; s2A += qA; s3A = __builtin_fmaf(qA, yA, s3A); s4A = __builtin_fmaf(qA, qA, s4A);
-        s1B += yB; s2B += qB; s3B = __builtin_fmaf(qB, yB, s3B); s4B = __builtin_fmaf(qB, qB, s4B);
-      }
+      cA = 0.5f * (bf16_lo(lo) + bf16_lo(hi));
+      cB = 0.5f * (bf16_hi(lo) + bf16_hi(hi));
     }
 #pragma unroll
     for (int t = 1; t < NSEG; t <<= 1) {
@@ -334,7 +315,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
         const bool v = h ? vB : vA;
         if (!v) continue;
         const float s1 = h ? s1B : s1A, s2 = h ? s2B : s2A, s3 = h ? s3B : s3A, s4 = h ? s4B : s4A;
-        const float sh = h ? shB : shA;
+        const float sh = h ? shB : shA, med = h ? cB : cA;
         const float dl = s1 / n, e2 = s2 / n, e3 = s3 / n, e4 = s4 / n;
         const float mu2 = e2 - dl * dl;
         const float mu3 = e3 - 3.f * dl * e2 + 2.f * dl * dl * dl;
@@ -349,7 +330,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
           zv = true;
         }
         const int64_t o = (int64_t)b * D + colA + h;
-        p.consensus[o] = CONS ? sh : sh + dl;
+        p.consensus[o] = CONS ? med : sh + dl;
         p.skew[o] = sk;
         p.kurt[o] = ku;
       }
