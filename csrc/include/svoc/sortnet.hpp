@@ -226,4 +226,104 @@ SVOC_DEV void middle_pair(const u16x2 (&r)[64], int seg, int lane, u16x2& lo, u1
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Median selection over a lane group (the fast kernels' hot path).
+//
+// Cross-lane stages use the gfx950 half-exchange instructions instead of ds_bpermute: one
+// v_permlane{16,32}_swap moves register x of the upper lanes and register y of the lower lanes in
+// a single VALU op.  Applied to a register pair (r[2k], r[2k+1]) it leaves every lane holding the
+// lower lane's value in x and the upper lane's value in y, so the compare-exchange is a plain
+// min + max in every lane (no lane-dependent select), and a second swap puts the results back.
+//
+// Bitonic direction without selects ("polarity"): lanes whose run must be descending store their
+// keys complemented (~key), so the one ascending in-lane network serves both directions.  A
+// cross-lane half-cleaner meets a lower lane of polarity d and an upper lane of polarity ~d: the
+// upper value is complemented after the swap (one v_not per pair), and both results leave in
+// polarity d -- exactly the direction the next in-lane merge needs.
+template <int XM>
+SVOC_DEV void xswap(uint32_t& x, uint32_t& y) {
+  static_assert(XM == 16 || XM == 32, "lane-half exchange distance");
+  if constexpr (XM == 32) {
+    const auto t = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+    x = t[0];
+    y = t[1];
+  } else {
+    const auto t = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    x = t[0];
+    y = t[1];
+  }
+}
+
+// Half-cleaner between lanes l and l ^ XM (lower lane keeps the minima); the upper lane's keys are
+// in the opposite polarity.  Afterwards both lanes hold keys in the lower lane's polarity.
+template <int XM>
+SVOC_DEV void xhc_swap(u16x2 (&r)[64]) {
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    uint32_t x = as_u32(r[2 * k]), y = as_u32(r[2 * k + 1]);
+    xswap<XM>(x, y);               // x: lower lane's key, y: upper lane's key (complemented)
+    y = ~y;
+    const u16x2 lo = kmin(as_k(x), as_k(y)), hi = kmax(as_k(x), as_k(y));
+    x = as_u32(lo);
+    y = as_u32(hi);
+    xswap<XM>(x, y);               // lower lanes get the minima, upper lanes the maxima
+    r[2 * k] = as_k(x);
+    r[2 * k + 1] = as_k(y);
+  }
+}
+
+// Final half-cleaner of a bitonic sequence whose lower half ends at the median: the two middle
+// order statistics are max(lower half) and min(upper half), so the compare-exchange results are
+// folded into a running max / min instead of being written back (no swap back, no merge).
+template <int XM>
+SVOC_DEV void xhc_middle(const u16x2 (&r)[64], u16x2& mx, u16x2& mn) {
+  mx = as_k(0u);
+  mn = as_k(0xffffffffu);
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    uint32_t x = as_u32(r[2 * k]), y = as_u32(r[2 * k + 1]);
+    xswap<XM>(x, y);
+    y = ~y;
+    mx = kmax(mx, kmin(as_k(x), as_k(y)));
+    mn = kmin(mn, kmax(as_k(x), as_k(y)));
+  }
+}
+
+// Load-time polarity of lane-group segment `seg` (XOR it into the keys before median_group).
+template <int NSEG>
+SVOC_DEV uint32_t group_polarity(int seg) {
+  if constexpr (NSEG == 2) return seg == 1 ? 0xffffffffu : 0u;
+  else if constexpr (NSEG == 4) return (seg == 1 || seg == 2) ? 0xffffffffu : 0u;
+  else return 0u;
+}
+
+// The two middle order statistics (positions NPAD/2 - 1 and NPAD/2) of the group's 64*NSEG keys,
+// returned in every lane of the group.  r must hold keys XOR group_polarity<NSEG>(seg).
+//   NSEG 1: odd-even merge sort, pruned by DCE to the two outputs (~414 compare-exchanges).
+//   NSEG 2: full in-lane sort, final cross-lane half-cleaner folded into max / min.
+//   NSEG 4: in-lane sort, stage-2 exchange (lane ^ 16) + bitonic merge, final stage folded.
+template <int NSEG>
+SVOC_DEV void median_group(u16x2 (&r)[64], u16x2& lo, u16x2& hi) {
+  sort64_oem(r);
+  if constexpr (NSEG == 1) {
+    lo = r[31];
+    hi = r[32];
+  } else {
+    if constexpr (NSEG == 4) {
+      xhc_swap<16>(r);
+      merge64(r);
+    }
+    u16x2 mx, mn;
+    xhc_middle<32>(r, mx, mn);               // final stage: lower half = lanes with bit 5 clear
+#pragma unroll
+    for (int m = 16; m <= 32; m <<= 1) {   // lanes of the group: ^16 (NSEG 4), ^32
+      if (NSEG == 2 && m == 16) continue;
+      mx = kmax(mx, shfl_xor_k(mx, m));
+      mn = kmin(mn, shfl_xor_k(mn, m));
+    }
+    lo = mx;
+    hi = mn;
+  }
+}
+
 }  // namespace svoc

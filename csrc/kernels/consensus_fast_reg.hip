@@ -78,6 +78,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
   const int nv = N - seg * 64;          // rows < nv are real
   const int nl = N + lo1 - seg * 64;    // rows in [nv, nl) are -inf, rows >= nl are +inf
   const int seg_off = seg * 64 * rowb;  // this lane's first row (bytes)
+  const uint32_t pol = group_polarity<NSEG>(seg);  // complemented keys for descending runs
 
   float acc[KEEP];
 #pragma unroll
@@ -107,9 +108,10 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
           r[i] = as_k((as_u32(to_key<CONS>(bload(rs, vo, i * rowb))) & (lt_mask(i, nvl) | hi_m)) | hi_m);
         }
       }
-      sort_group<NSEG, P>(r, seg);
+#pragma unroll
+      for (int i = 0; i < 64; ++i) r[i] = as_k(as_u32(r[i]) ^ pol);
       u16x2 klo, khi;
-      middle_pair<NSEG, P>(r, seg, lane, klo, khi);
+      median_group<NSEG>(r, klo, khi);
       const uint32_t lo = from_key<CONS>(klo), hi = from_key<CONS>(khi);
       cA = 0.5f * (bf16_lo(lo) + bf16_lo(hi));
       cB = 0.5f * (bf16_hi(lo) + bf16_hi(hi));
@@ -291,10 +293,9 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
     if (CONS) {
       u16x2 r[64];
 #pragma unroll
-      for (int i = 0; i < 64; ++i) r[i] = as_k(wv[i]);
-      sort_group<NSEG, P>(r, seg);   // only the two middle outputs are live: pruned to a selection
+      for (int i = 0; i < 64; ++i) r[i] = as_k(wv[i] ^ pol);
       u16x2 klo, khi;
-      middle_pair<NSEG, P>(r, seg, lane, klo, khi);
+      median_group<NSEG>(r, klo, khi);
       const uint32_t lo = key_to_pos(klo), hi = key_to_pos(khi);
       cA = 0.5f * (bf16_lo(lo) + bf16_lo(hi));
       cB = 0.5f * (bf16_hi(lo) + bf16_hi(hi));
