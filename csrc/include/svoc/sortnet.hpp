@@ -49,6 +49,15 @@ SVOC_DEV uint32_t key_to_pos(u16x2 k) { return as_u32(k) ^ 0x80008000u; }
 
 SVOC_DEV float bf16_lo(uint32_t w) { return __builtin_bit_cast(float, w << 16); }
 SVOC_DEV float bf16_hi(uint32_t w) { return __builtin_bit_cast(float, w & 0xffff0000u); }
+SVOC_DEV float fand(float x, uint32_t m) { return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, x) & m); }
+typedef float f32x2 __attribute__((ext_vector_type(2)));  // packed-FP32 (v_pk_*_f32) operand
+SVOC_DEV f32x2 bf16x2_to_f32x2(uint32_t w) { return f32x2{bf16_lo(w), bf16_hi(w)}; }
+// (element copies first: clang 20 mis-lowers __builtin_bit_cast applied directly to x.y -- the
+// second lane comes out as poison)
+SVOC_DEV f32x2 fand2(f32x2 x, uint32_t m) {
+  const float a = x.x, b = x.y;
+  return f32x2{fand(a, m), fand(b, m)};
+}
 
 // All-ones / zero lane masks built arithmetically (no v_cmp): a compare writes a VCC/SGPR pair, and
 // 64 unrolled rows of them exhaust the SGPR file (spills) and get hoisted out of loops.
@@ -58,7 +67,6 @@ SVOC_DEV uint32_t bit_mask(uint64_t m, int i) {  // bit i set
   const uint32_t w = i < 32 ? (uint32_t)m : (uint32_t)(m >> 32);
   return (uint32_t)__builtin_amdgcn_sbfe((int)w, i & 31, 1);
 }
-SVOC_DEV float fand(float x, uint32_t m) { return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, x) & m); }
 
 SVOC_DEV u16x2 shfl_xor_k(u16x2 v, int m) { return as_k((uint32_t)__shfl_xor((int)as_u32(v), m)); }
 SVOC_DEV u16x2 shfl_k(u16x2 v, int src) { return as_k((uint32_t)__shfl((int)as_u32(v), src)); }

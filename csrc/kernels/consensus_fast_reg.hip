@@ -122,12 +122,15 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
     }
     __builtin_amdgcn_sched_barrier(0);
     float part[64];
+    // columns past D contribute 0: their bf16 halves are masked to +0 and their centre is +0
+    const uint32_t mW = vA ? (vB ? 0xffffffffu : 0x0000ffffu) : 0u;
+    const f32x2 c2 = {vA ? cA : 0.f, vB ? cB : 0.f};
 #pragma unroll
     for (int i = 0; i < 64; ++i) {
-      const uint32_t w = bload(rs, vo, i * rowb);  // L2/MALL-hot re-read
-      const float yA = vA ? bf16_lo(w) - cA : 0.f;
-      const float yB = vB ? bf16_hi(w) - cB : 0.f;
-      part[i] = __builtin_fmaf(yA, yA, yB * yB);
+      const uint32_t w = bload(rs, vo, i * rowb) & mW;  // L2/MALL-hot re-read
+      const f32x2 y = bf16x2_to_f32x2(w) - c2;          // v_pk_add_f32
+      const f32x2 q = y * y;                              // v_pk_mul_f32
+      part[i] = q.x + q.y;
     }
 #pragma unroll
     for (int h = 32, msk = P / 2; msk >= 1; h >>= 1, msk >>= 1) {
@@ -267,28 +270,30 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
     asm volatile("" : "+v"(mm), "+v"(ml));
     // shifted power sums (shift = the first reliable row: no cancellation for clustered columns)
     const uint32_t w0 = bload(rs, vA ? colA * 2 : 0, first_rel * rowb);
-    const float shA = bf16_lo(w0), shB = bf16_hi(w0);
-    float s1A = 0.f, s2A = 0.f, s3A = 0.f, s4A = 0.f, s1B = 0.f, s2B = 0.f, s3B = 0.f, s4B = 0.f;
+    const f32x2 sh = {bf16_lo(w0), bf16_hi(w0)};
+    f32x2 s1 = {0.f, 0.f}, s2 = s1, s3 = s1, s4 = s1;   // packed (column A, column B) power sums
     uint32_t wv[64];
 #pragma unroll
     for (int i = 0; i < 64; ++i) wv[i] = bload(rs, vo, i * rowb);
 #pragma unroll
     for (int i = 0; i < 64; ++i) {
       uint32_t w = wv[i];
-      // row-ordered accumulation: keeps LLVM from pairing / front-loading all 64 rows (VGPRs)
-      asm volatile("" : "+v"(w), "+v"(s1A), "+v"(s1B), "+v"(s2A), "+v"(s2B), "+v"(s3A), "+v"(s3B),
-                   "+v"(s4A), "+v"(s4B));
-      const uint32_t mk = bit_mask(mm, i);
-      const float yA = fand(bf16_lo(w) - shA, mk), yB = fand(bf16_hi(w) - shB, mk);
-      const float qA = yA * yA, qB = yB * yB;
-      s1A += yA; s2A += qA; s3A = __builtin_fmaf(qA, yA, s3A); s4A = __builtin_fmaf(qA, qA, s4A);
-      s1B += yB; s2B += qB; s3B = __builtin_fmaf(qB, yB, s3B); s4B = __builtin_fmaf(qB, qB, s4B);
-      if (CONS) {
-        // reliable rows keep their key; non-reliable rows become -inf (lowmask) / +inf sentinels
-        const uint32_t lm = bit_mask(ml, i);
-        wv[i] = (as_u32(pos_to_key(w)) & mk) | ~(mk | lm);
-      }
+      uint32_t mk = bit_mask(mm, i);
+      // reliable rows keep their key; non-reliable rows become -inf (lowmask) / +inf sentinels
+      uint32_t key = CONS ? (as_u32(pos_to_key(w)) & mk) | ~(mk | bit_mask(ml, i)) : 0u;
+      // row-ordered accumulation: keeps LLVM from front-loading all 64 rows (VGPRs)
+      asm volatile("" : "+v"(w), "+v"(mk), "+v"(key), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
+      if (CONS) wv[i] = key;
+      f32x2 y = bf16x2_to_f32x2(w) - sh;
+      y = fand2(y, mk);
+      const f32x2 q = y * y;
+      s1 += y;
+      s2 += q;
+      s3 = __builtin_elementwise_fma(q, y, s3);
+      s4 = __builtin_elementwise_fma(q, q, s4);
     }
+    float s1A = s1.x, s2A = s2.x, s3A = s3.x, s4A = s4.x, s1B = s1.y, s2B = s2.y, s3B = s3.y, s4B = s4.y;
+    const float shA = sh.x, shB = sh.y;
     float cA = 0.f, cB = 0.f;  // pass-2 smooth median (constrained consensus)
     if (CONS) {
       u16x2 r[64];
