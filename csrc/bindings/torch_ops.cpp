@@ -61,7 +61,7 @@ void fast_round_checks(const at::Tensor& values, int64_t D, const at::Tensor& c1
 void fast_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t D,
                     int64_t n_failing, bool constrained, double max_spread, at::Tensor c1, at::Tensor cons,
                     at::Tensor skew, at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable,
-                    at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim) {
+                    at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim, bool legacy) {
   (void)wave_hint;
   fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
   const int64_t B = values.size(0), N = values.size(1), ld = values.size(2), is = values.stride(0);
@@ -99,13 +99,14 @@ void fast_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& a
   fb.status = status.data_ptr<int32_t>();
   fb.mode = (int)mode;
   fb.rel_dim = rel_dim;
+  fb.legacy = legacy;
   fast_round_batch_cpu(fb, cpu_threads());
 }
 
 void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t D,
                     int64_t n_failing, bool constrained, double max_spread, at::Tensor c1, at::Tensor cons,
                     at::Tensor skew, at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable,
-                    at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim) {
+                    at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim, bool legacy) {
   fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
   TORCH_CHECK(values.scalar_type() == at::kBFloat16, "GPU fast path stores values in bf16");
   const int64_t B = values.size(0), N = values.size(1), ld = values.size(2);
@@ -125,6 +126,7 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
   TORCH_CHECK(mode >= 0 && mode <= 2, "mode must be 0, 1 or 2");
   p.mode = (int)mode;
   p.rel_dim = (int)rel_dim;
+  p.legacy = legacy ? 1 : 0;
   p.c1 = c1.data_ptr<float>();
   p.consensus = cons.data_ptr<float>();
   p.skew = skew.data_ptr<float>();
@@ -158,9 +160,11 @@ void exact_checks(const at::Tensor& values, const at::Tensor& c1, const at::Tens
 
 void exact_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t n_failing,
                      bool constrained, int64_t max_spread, at::Tensor c1, at::Tensor cons, at::Tensor skew,
-                     at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable, at::Tensor status) {
+                     at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable, at::Tensor status,
+                     bool legacy) {
   exact_checks(values, c1, cons, skew, kurt, rel, qr, reliable, status);
   ExactBatch eb{};
+  eb.legacy = legacy;
   eb.values = values.data_ptr<int64_t>();
   eb.B = values.size(0); eb.N = values.size(1); eb.D = values.size(2);
   eb.active = active_ptr(active, eb.B, values.device());
@@ -180,9 +184,11 @@ void exact_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& 
 
 void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t n_failing,
                      bool constrained, int64_t max_spread, at::Tensor c1, at::Tensor cons, at::Tensor skew,
-                     at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable, at::Tensor status) {
+                     at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable, at::Tensor status,
+                     bool legacy) {
   exact_checks(values, c1, cons, skew, kurt, rel, qr, reliable, status);
   ExactParams p{};
+  p.legacy = legacy ? 1 : 0;
   p.values = values.data_ptr<int64_t>();
   p.B = (int)values.size(0); p.N = (int)values.size(1); p.D = (int)values.size(2);
   TORCH_CHECK(p.N >= 1 && p.N <= 256, "GPU exact path supports N <= 256");
@@ -210,11 +216,11 @@ TORCH_LIBRARY(svoc, m) {
   m.def(
       "fast_round(Tensor values, Tensor? active, int D, int n_failing, bool constrained, float max_spread, "
       "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "
-      "Tensor(g!) reliable, Tensor(h!) status, int wave_hint=0, int mode=0, int rel_dim=0) -> ()");
+      "Tensor(g!) reliable, Tensor(h!) status, int wave_hint=0, int mode=0, int rel_dim=0, bool legacy=False) -> ()");
   m.def(
       "exact_round(Tensor values, Tensor? active, int n_failing, bool constrained, int max_spread, "
       "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "
-      "Tensor(g!) reliable, Tensor(h!) status) -> ()");
+      "Tensor(g!) reliable, Tensor(h!) status, bool legacy=False) -> ()");
   svoc::register_extra_defs(m);
 }
 

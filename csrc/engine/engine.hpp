@@ -36,10 +36,12 @@ struct ExactBatch {
   int64_t* qr;         // [B, N]
   int64_t* c1;         // [B, D] or null
   int32_t* status;     // [B]
+  bool legacy = false;  // obsolete contracts (contract_nd.cairo / contract_1d_constrained.cairo)
 };
 
+// legacy: reliability W - 2 sqrt(mean qr) without the /D (contract_nd.cairo:418,437) and no moments.
 int exact_round_one(const int64_t* X, int64_t N, int64_t D, int64_t n_failing, bool constrained,
-                    int64_t max_spread, ExactOut& o);
+                    int64_t max_spread, ExactOut& o, bool legacy = false);
 void exact_round_batch_cpu(const ExactBatch& b, int threads);
 
 // ---- fast (float compute, bf16/fp32 storage) ---------------------------------------------------
@@ -72,12 +74,13 @@ struct FastBatch {
   int32_t* status;
   int mode = 0;
   int64_t rel_dim = 0;
+  bool legacy = false;
 };
 
 // mode 0: full round; 1: pass 1 only (c1 + qr partials); 2: pass 2 from o.qr (already reduced).
 // rel_dim: divisor of the constrained reliability (0 = D).
 int fast_round_one(const float* X, int64_t N, int64_t D, int64_t n_failing, bool constrained,
-                   float max_spread, FastOut& o, int mode = 0, int64_t rel_dim = 0);
+                   float max_spread, FastOut& o, int mode = 0, int64_t rel_dim = 0, bool legacy = false);
 void fast_round_batch_cpu(const FastBatch& b, int threads);
 
 }  // namespace svoc

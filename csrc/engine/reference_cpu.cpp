@@ -53,8 +53,9 @@ i128 average_exact(const std::vector<i128>& v, int& st) {  // math.cairo:240-254
 }  // namespace
 
 int exact_round_one(const int64_t* X, int64_t N, int64_t D, int64_t n_failing, bool constrained,
-                    int64_t max_spread, ExactOut& o) {
+                    int64_t max_spread, ExactOut& o, bool legacy) {
   int st = ST_OK;
+  const int64_t rdim = legacy ? 1 : D;
   std::vector<i128> col(N);
   // ---- pass 1: essence (contract.cairo:455-459)
   for (int64_t d = 0; d < D && st == ST_OK; ++d) {
@@ -70,7 +71,7 @@ int exact_round_one(const int64_t* X, int64_t N, int64_t D, int64_t n_failing, b
     qr[i] = acc;
   }
   i128 mean_qr = average_exact(qr, st);
-  i128 rel1 = constrained ? constrained_reliability(mean_qr, D, st)
+  i128 rel1 = constrained ? constrained_reliability(mean_qr, rdim, st)
                           : unconstrained_reliability(wsqrt(mean_qr, st), max_spread, st);
   if (st) return st;
   if (!in_unit_interval(rel1)) return ST_RELIABILITY_INTERVAL;
@@ -97,10 +98,17 @@ int exact_round_one(const int64_t* X, int64_t N, int64_t D, int64_t n_failing, b
   std::vector<i128> qr2(R);
   for (int64_t k = 0; k < R; ++k) qr2[k] = qr[rows[k]];
   i128 mean_qr2 = average_exact(qr2, st);
-  i128 rel2 = constrained ? constrained_reliability(mean_qr2, D, st)
+  i128 rel2 = constrained ? constrained_reliability(mean_qr2, rdim, st)
                           : unconstrained_reliability(wsqrt(mean_qr2, st), max_spread, st);
   if (st) return st;
   if (!in_unit_interval(rel2)) return ST_RELIABILITY_INTERVAL;
+  if (legacy) {  // the obsolete contracts stop here: no skewness / kurtosis storage
+    for (int64_t d = 0; d < D; ++d) o.skew[d] = o.kurt[d] = 0;
+    for (int64_t i = 0; i < N; ++i) o.qr[i] = (int64_t)qr[i];
+    o.rel1 = (int64_t)rel1;
+    o.rel2 = (int64_t)rel2;
+    return ST_OK;
+  }
   // moments (math.cairo:208-222, 320-398) -- means, variances, skewness(all d), kurtosis(all d)
   std::vector<i128> means(D), vars(D);
   for (int64_t d = 0; d < D && st == ST_OK; ++d) {
@@ -145,7 +153,7 @@ void exact_round_batch_cpu(const ExactBatch& b, int threads) {
     std::vector<int64_t> c1(D), cons(D), sk(D), ku(D), qr(N);
     std::vector<uint8_t> rel(N);
     ExactOut o{c1.data(), qr.data(), rel.data(), cons.data(), sk.data(), ku.data(), 0, 0};
-    int st = exact_round_one(b.values + i * N * D, N, D, b.n_failing, b.constrained, b.max_spread, o);
+    int st = exact_round_one(b.values + i * N * D, N, D, b.n_failing, b.constrained, b.max_spread, o, b.legacy);
     b.status[i] = st;
     if (st != ST_OK) return;  // revert: outputs untouched
     std::memcpy(b.consensus + i * D, cons.data(), D * sizeof(int64_t));
@@ -164,12 +172,12 @@ void exact_round_batch_cpu(const ExactBatch& b, int threads) {
 // ------------------------------------------------------------------------------------------------
 
 int fast_round_one(const float* X, int64_t N, int64_t D, int64_t n_failing, bool constrained,
-                   float max_spread, FastOut& o, int mode, int64_t rel_dim) {
+                   float max_spread, FastOut& o, int mode, int64_t rel_dim, bool legacy) {
   if (n_failing > N) return ST_USIZE_UNDERFLOW;
   if (N < 2) return ST_INDEX_OOB;
   std::vector<float> col(N);
   const int64_t m = N / 2;
-  const double rd = (double)(rel_dim > 0 ? rel_dim : D);
+  const double rd = legacy ? 1.0 : (double)(rel_dim > 0 ? rel_dim : D);
   for (int64_t d = 0; d < D && mode != 2; ++d) {
     for (int64_t i = 0; i < N; ++i) col[i] = X[i * D + d];
     std::nth_element(col.begin(), col.begin() + m, col.end());
@@ -209,7 +217,7 @@ int fast_round_one(const float* X, int64_t N, int64_t D, int64_t n_failing, bool
     if (o.reliable[i]) sum_qr2 += o.qr[i];
   float rel2 = rel_of(sum_qr2 / (double)R);
   if (!(rel2 >= 0.f && rel2 <= 1.f)) return ST_RELIABILITY_INTERVAL;
-  if (R < 4) return ST_TOO_FEW_RELIABLE;
+  if (R < 4 && !legacy) return ST_TOO_FEW_RELIABLE;
   col.resize(R);
   const int64_t m2 = R / 2;
   for (int64_t d = 0; d < D; ++d) {
@@ -227,12 +235,16 @@ int fast_round_one(const float* X, int64_t N, int64_t D, int64_t n_failing, bool
       s4 += y * y * y * y;
     }
     double var = s2 / (double)R;
-    if (var <= 0.0) return ST_ZERO_VARIANCE;
-    double sd = std::sqrt(var);
-    double z3 = s3 / (sd * sd * sd), z4 = s4 / (var * var);
-    double n = (double)R;
-    o.skew[d] = (float)(z3 * n / ((n - 1) * (n - 2)));
-    o.kurt[d] = (float)(((z4 * n * (n + 1)) / (n - 1) - 3.0 * (n - 1) * (n - 1)) / ((n - 2) * (n - 3)));
+    if (legacy) {
+      o.skew[d] = o.kurt[d] = 0.f;
+    } else {
+      if (var <= 0.0) return ST_ZERO_VARIANCE;
+      double sd = std::sqrt(var);
+      double z3 = s3 / (sd * sd * sd), z4 = s4 / (var * var);
+      double n = (double)R;
+      o.skew[d] = (float)(z3 * n / ((n - 1) * (n - 2)));
+      o.kurt[d] = (float)(((z4 * n * (n + 1)) / (n - 1) - 3.0 * (n - 1) * (n - 1)) / ((n - 2) * (n - 3)));
+    }
     if (constrained) {
       std::nth_element(col.begin(), col.begin() + m2, col.end());
       float hi = col[m2];
@@ -256,7 +268,7 @@ void fast_round_batch_cpu(const FastBatch& b, int threads) {
     b.load(b.values, i, x.data());
     if (b.mode == 2) std::memcpy(qr.data(), b.qr + i * N, N * sizeof(float));
     FastOut o{c1.data(), qr.data(), rel.data(), cons.data(), sk.data(), ku.data(), 0.f, 0.f};
-    int st = fast_round_one(x.data(), N, D, b.n_failing, b.constrained, b.max_spread, o, b.mode, b.rel_dim);
+    int st = fast_round_one(x.data(), N, D, b.n_failing, b.constrained, b.max_spread, o, b.mode, b.rel_dim, b.legacy);
     b.status[i] = st;
     if (b.c1 && b.n_failing <= N && N >= 2 && b.mode != 2) std::memcpy(b.c1 + i * D, c1.data(), D * sizeof(float));
     if (b.mode == 1) {

@@ -25,6 +25,7 @@ struct FastParams {
   float* qr;                // [B, N]
   uint8_t* reliable;        // [B, N]
   int32_t* status;          // [B]
+  int legacy;               // obsolete-contract variant: reliability without /D, no moments (C30/C31)
 };
 
 struct ExactParams {
@@ -42,6 +43,7 @@ struct ExactParams {
   int64_t* qr;              // [B, N]
   uint8_t* reliable;        // [B, N]
   int32_t* status;          // [B]
+  int legacy;               // obsolete-contract variant (see FastParams)
 };
 
 }  // namespace svoc

@@ -131,7 +131,8 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
 #pragma unroll
   for (int j = 0; j < RPL; ++j) sum_qr = add(sum_qr, wave_sum(qr[j], st), st);
   const i128 mean_qr = idiv(sum_qr, (i128)N, st);
-  const i128 rel1 = p.constrained ? constrained_reliability(mean_qr, D, st)
+  const int64_t rdim = p.legacy ? 1 : D;  // obsolete contracts: no /D (contract_nd.cairo:418)
+  const i128 rel1 = p.constrained ? constrained_reliability(mean_qr, rdim, st)
                                   : unconstrained_reliability(wsqrt(mean_qr, st), p.max_spread, st);
   if (st == ST_OK && !in_unit_interval(rel1)) st = ST_RELIABILITY_INTERVAL;
   if (st == ST_OK && p.n_failing > N) st = ST_USIZE_UNDERFLOW;
@@ -178,11 +179,14 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
 #pragma unroll
   for (int j = 0; j < RPL; ++j) s2 = add(s2, wave_sum(rel[j] ? qr[j] : 0, st), st);
   const i128 mean_qr2 = idiv(s2, (i128)R, st);
-  const i128 rel2 = p.constrained ? constrained_reliability(mean_qr2, D, st)
+  const i128 rel2 = p.constrained ? constrained_reliability(mean_qr2, rdim, st)
                                   : unconstrained_reliability(wsqrt(mean_qr2, st), p.max_spread, st);
   if (st == ST_OK && !in_unit_interval(rel2)) st = ST_RELIABILITY_INTERVAL;
+  if (p.legacy) {  // obsolete contracts store no moments
+    for (int d = lane; d < D; d += 64) sk[d] = ku[d] = 0;
+  }
   // ---- moments (math.cairo:208-222, 320-398), stage by stage like the CPU engine
-  for (int d = 0; d < D && st == ST_OK; ++d) {
+  for (int d = 0; d < D && st == ST_OK && !p.legacy; ++d) {
     i128 s = 0;
 #pragma unroll
     for (int j = 0; j < RPL; ++j) {
@@ -193,7 +197,7 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
     if (lane == 0) means[d] = (int64_t)mu;
   }
   __syncthreads();
-  for (int d = 0; d < D && st == ST_OK; ++d) {
+  for (int d = 0; d < D && st == ST_OK && !p.legacy; ++d) {
     i128 s = 0;
     int l2 = ST_OK;
 #pragma unroll
@@ -207,7 +211,7 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
     if (lane == 0) vars[d] = (int64_t)v;
   }
   __syncthreads();
-  for (int pass = 0; pass < 2; ++pass) {  // 0: skewness for all d, 1: kurtosis for all d
+  for (int pass = 0; pass < 2 && !p.legacy; ++pass) {  // 0: skewness for all d, 1: kurtosis for all d
     for (int d = 0; d < D && st == ST_OK; ++d) {
       const i128 sd = wsqrt(vars[d], st);
       i128 s = 0;

@@ -257,7 +257,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
     }
     int st = ST_OK;
     float rel1, rel2 = 0.f;
-    const float rd = (float)(p.rel_dim > 0 ? p.rel_dim : D);
+    const float rd = p.legacy ? 1.f : (float)(p.rel_dim > 0 ? p.rel_dim : D);
     if (CONS) rel1 = 1.f - 2.f * sqrtf(sa / (float)N / rd);                  // contract.cairo:436-439
     else rel1 = 1.f - fminf(p.max_spread, sqrtf(sa / (float)N)) / p.max_spread;  // :365-368
     if (!(rel1 >= 0.f && rel1 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
@@ -266,7 +266,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
       if (CONS) rel2 = 1.f - 2.f * sqrtf(sr / (float)R / rd);
       else rel2 = 1.f - fminf(p.max_spread, sqrtf(sr / (float)R)) / p.max_spread;
       if (!(rel2 >= 0.f && rel2 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
-      else if (R < 4) st = ST_TOO_FEW_RELIABLE;
+      else if (R < 4 && !p.legacy) st = ST_TOO_FEW_RELIABLE;
     }
     misc_f[0] = rel1;
     misc_f[1] = rel2;
@@ -382,10 +382,10 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
         }
         const int64_t o = (int64_t)b * D + colA + h;
         p.consensus[o] = CONS ? sh : sh + dl;
-        p.skew[o] = sk;
-        p.kurt[o] = ku;
+        p.skew[o] = p.legacy ? 0.f : sk;
+        p.kurt[o] = p.legacy ? 0.f : ku;
       }
-      if (zv) misc_i[1] = 1;
+      if (zv && !p.legacy) misc_i[1] = 1;
     }
   }
   __syncthreads();

@@ -226,7 +226,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
         lowmask[w] = lm;
       }
       int st = ST_OK;
-      const float rd = (float)(p.rel_dim > 0 ? p.rel_dim : D);
+      const float rd = p.legacy ? 1.f : (float)(p.rel_dim > 0 ? p.rel_dim : D);
       float rel1, rel2 = 0.f;
       if (CONS) rel1 = 1.f - 2.f * sqrtf(s_all / (float)N / rd);
       else rel1 = 1.f - fminf(p.max_spread, sqrtf(s_all / (float)N)) / p.max_spread;
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
         if (CONS) rel2 = 1.f - 2.f * sqrtf(s_rel / (float)R / rd);
         else rel2 = 1.f - fminf(p.max_spread, sqrtf(s_rel / (float)R)) / p.max_spread;
         if (!(rel2 >= 0.f && rel2 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
-        else if (R < 4) st = ST_TOO_FEW_RELIABLE;
+        else if (R < 4 && !p.legacy) st = ST_TOO_FEW_RELIABLE;  // legacy: no moments
       }
       misc_f[0] = rel1;
       misc_f[1] = rel2;
@@ -337,10 +337,10 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
         }
         const int64_t o = (int64_t)b * D + colA + h;
         p.consensus[o] = CONS ? med : sh + dl;
-        p.skew[o] = sk;
-        p.kurt[o] = ku;
+        p.skew[o] = p.legacy ? 0.f : sk;
+        p.kurt[o] = p.legacy ? 0.f : ku;
       }
-      if (zv) misc_i[1] = 1;
+      if (zv && !p.legacy) misc_i[1] = 1;
     }
   }
   __syncthreads();

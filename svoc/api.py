@@ -177,3 +177,58 @@ class OracleConsensus:
 
     def get_reliability(self) -> Tuple[int, int]:
         return self.get_first_pass_consensus_reliability(), self.get_second_pass_consensus_reliability()
+
+
+class LegacyOracleConsensus(OracleConsensus):
+    """The obsolete contracts' ABI (contract/obsolete/src/): ``contract_nd.cairo`` (``variant=
+    "nd_legacy"``, WsadVector = i128 values in and out) and ``contract_1d_constrained.cairo``
+    (``variant="1d_legacy"``, one i128 per oracle, constrained, dimension 1).
+
+    Same state machine and governance as the current contract; the round differs as documented in
+    :func:`svoc.reference.consensus_round` (``legacy=True``): no ``/D`` in the constrained
+    reliability, no skewness / kurtosis (the getters do not exist in those ABIs).
+    """
+
+    def __init__(self, admins: Sequence[int], enable_oracle_replacement: bool, required_majority: int,
+                 n_failing_oracles: int, constrained: bool, unconstrained_max_spread: int, dimension: int,
+                 oracles: Sequence[int], device="cpu", mode: str = "exact", variant: str = "nd_legacy"):
+        if variant not in ("nd_legacy", "1d_legacy"):
+            raise ValueError("variant must be 'nd_legacy' or '1d_legacy'")
+        ms = int(unconstrained_max_spread)                     # i128 constructor argument
+        cfg = ConsensusConfig(n_oracles=len(oracles), dimension=dimension, n_failing_oracles=n_failing_oracles,
+                              constrained=bool(constrained), unconstrained_max_spread=ms / WSAD,
+                              n_admins=len(admins), required_majority=required_majority,
+                              enable_oracle_replacement=bool(enable_oracle_replacement),
+                              unconstrained_max_spread_wsad=ms, variant=variant)
+        cfg.validate()
+        self._max_spread_wsad = ms
+        self._svc = ConsensusService(cfg, 1, list(admins), list(oracles), device=device, mode=mode)
+        self._b = 0
+        self._scalar = variant == "1d_legacy"
+
+    def _out(self, t: torch.Tensor) -> List[int]:
+        if self.engine.mode == "exact":
+            return [int(x) for x in t.tolist()]
+        return [int(x) for x in torch.trunc(t.double() * WSAD).to(torch.int64).tolist()]
+
+    def update_prediction(self, caller: int, prediction) -> Status:
+        """``update_prediction(WsadVector)`` (contract_nd.cairo:538) / ``(i128)`` (1-D, :391)."""
+        vals = [int(prediction)] if self._scalar else [int(v) for v in prediction]
+        pred = vals if self.engine.mode == "exact" else [v / WSAD for v in vals]
+        st = self._svc.update_predictions([(self._b, caller, pred)])[0]
+        self._raise(st)
+        return st
+
+    def get_consensus_value(self):
+        v = self._out(self.engine.consensus[self._b])
+        return v[0] if self._scalar else v
+
+    def get_oracle_value_list(self, caller: int):
+        rows = super().get_oracle_value_list(caller)
+        return [(a, (v[0] if self._scalar else v), e, r) for a, v, e, r in rows]
+
+    def get_skewness(self):
+        raise AttributeError("the obsolete contracts store no skewness")
+
+    def get_kurtosis(self):
+        raise AttributeError("the obsolete contracts store no kurtosis")

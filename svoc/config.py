@@ -25,6 +25,10 @@ class ConsensusConfig:
     enable_oracle_replacement: bool = True
     # exact wsad value of the spread when it must round-trip bit for bit (set by the ABI facade)
     unconstrained_max_spread_wsad: Optional[int] = None
+    # contract generation: "nds" = contract/src/contract.cairo (default); "nd_legacy" =
+    # contract/obsolete/src/contract_nd.cairo; "1d_legacy" = contract_1d_constrained.cairo (D = 1,
+    # constrained).  The obsolete ones compute no moments and no /D in the constrained reliability.
+    variant: str = "nds"
 
     def validate(self) -> None:
         if self.n_oracles < 1 or self.dimension < 1:
@@ -33,6 +37,15 @@ class ConsensusConfig:
             raise ValueError("n_admins must be in [0, 64] (bit-packed vote rows)")
         # unconstrained_max_spread == 0 is accepted: like the contract, every round then reverts
         # with a division by zero (contract.cairo:367)
+        if self.variant not in ("nds", "nd_legacy", "1d_legacy"):
+            raise ValueError(f"unknown contract variant {self.variant!r}")
+        if self.variant == "1d_legacy" and (self.dimension != 1 or not self.constrained):
+            raise ValueError("the 1-D obsolete contract is constrained with dimension 1")
+
+    @property
+    def legacy(self) -> bool:
+        """Obsolete-contract semantics (contract_nd.cairo:418,437): no /D, no moments."""
+        return self.variant != "nds"
 
     @property
     def max_spread_wsad(self) -> int:

@@ -119,12 +119,13 @@ class ConsensusEngine:
         if self.mode == "fast":
             self._ops.fast_round(self.values, self._active, self.D, self.cfg.n_failing_oracles,
                                  self.cfg.constrained, float(mx), self.c1, self.consensus, self.skew,
-                                 self.kurt, self.rel, self.qr, self.reliable, self.status, self.wave_hint)
+                                 self.kurt, self.rel, self.qr, self.reliable, self.status, self.wave_hint,
+                                 0, 0, self.cfg.legacy)
             ok = (self.status == Status.OK) | (self.status == Status.ZERO_VARIANCE)
         else:
             self._ops.exact_round(self.values, self._active, self.cfg.n_failing_oracles, self.cfg.constrained,
                                   self.cfg.max_spread_wsad, self.c1, self.consensus, self.skew, self.kurt,
-                                  self.rel, self.qr, self.reliable, self.status)
+                                  self.rel, self.qr, self.reliable, self.status, self.cfg.legacy)
             ok = self.status == Status.OK
         self.consensus_active |= act & ok
         self.touched.zero_()

@@ -26,10 +26,14 @@ def smooth_median(x: torch.Tensor, count: torch.Tensor | int, dim: int = 1) -> t
     return 0.5 * (lo + hi)
 
 
-def fast_round(values: torch.Tensor, n_failing: int, constrained: bool, max_spread: float = 1.0) -> Dict[str, torch.Tensor]:
-    """values: [B, N, D] (any float dtype; computed in fp32). Returns a dict of fp32 outputs."""
+def fast_round(values: torch.Tensor, n_failing: int, constrained: bool, max_spread: float = 1.0,
+               legacy: bool = False) -> Dict[str, torch.Tensor]:
+    """values: [B, N, D] (any float dtype; computed in fp32). Returns a dict of fp32 outputs.
+
+    legacy: obsolete-contract variant (contract_nd.cairo:418,437): reliability without /D, no moments."""
     x = values.float()
-    B, N, D = x.shape
+    B, N, D0 = x.shape
+    D = 1 if legacy else D0
     c1 = smooth_median(x, N)                                  # [B, D]
     qr = ((x - c1[:, None, :]) ** 2).sum(-1)                  # [B, N]
     mean_qr = qr.double().mean(-1)
@@ -69,5 +73,7 @@ def fast_round(values: torch.Tensor, n_failing: int, constrained: bool, max_spre
     z4 = n * m4 / torch.where(safe, m2, 1.0) ** 2
     skew = torch.where(safe, z3 * n / ((n - 1) * (n - 2)), 0.0)
     kurt = torch.where(safe, ((z4 * n * (n + 1)) / (n - 1) - 3 * (n - 1) ** 2) / ((n - 2) * (n - 3)), 0.0)
+    if legacy:
+        skew, kurt = torch.zeros_like(skew), torch.zeros_like(kurt)
     return dict(c1=c1, qr=qr, reliable=reliable, consensus=consensus.float(), rel=torch.stack([rel1, rel2], -1).float(),
                 skew=skew.float(), kurt=kurt.float())

@@ -36,10 +36,11 @@ def run_round_sharded(engine, d_global: int, group=None, world: int = 1) -> None
     mx = float(e.cfg.unconstrained_max_spread)
     args = (e.values, e._active, e.D, e.cfg.n_failing_oracles, e.cfg.constrained, mx, e.c1, e.consensus,
             e.skew, e.kurt, e.rel, e.qr, e.reliable, e.status, e.wave_hint)
-    e._ops.fast_round(*args, 1, d_global)          # pass 1: local c1 + qr partials
+    lg = e.cfg.legacy
+    e._ops.fast_round(*args, 1, d_global, lg)      # pass 1: local c1 + qr partials
     if world > 1:
         dist.all_reduce(e.qr, op=dist.ReduceOp.SUM, group=group)
-    e._ops.fast_round(*args, 2, d_global)          # pass 2 from the global qr
+    e._ops.fast_round(*args, 2, d_global, lg)      # pass 2 from the global qr
     ok = (e.status == Status.OK) | (e.status == Status.ZERO_VARIANCE)
     e.consensus_active |= e._active.bool() & ok
     e.touched.zero_()

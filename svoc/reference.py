@@ -199,13 +199,16 @@ def unconstrained_reliability(sd: int, max_spread: int) -> int:
 
 
 def consensus_round(values: Sequence[Sequence[int]], n_failing: int, constrained: bool,
-                    max_spread: int = 0) -> RoundResult:
+                    max_spread: int = 0, legacy: bool = False) -> RoundResult:
     """Both passes of the reference algorithm on a full [N][D] table of wsad integers.
 
-    Raises :class:`ConsensusRevert` wherever the contract would panic.
+    Raises :class:`ConsensusRevert` wherever the contract would panic.  ``legacy`` selects the
+    obsolete contracts (contract/obsolete/src/contract_nd.cairo:395-443, contract_1d_constrained.cairo:
+    250-295): constrained reliability ``W - 2 sqrt(mean qr)`` without the ``/D``
+    (contract_nd.cairo:418,437) and no skewness / kurtosis (returned as zeros, never reverting).
     """
     n = len(values)
-    dim = len(values[0])
+    dim = 1 if legacy else len(values[0])
     # ---- pass 1 (contract.cairo:451-473 / 379-402)
     cols = columns(values)
     c1 = [smooth_median(c) for c in cols]
@@ -235,6 +238,9 @@ def consensus_round(values: Sequence[Sequence[int]], n_failing: int, constrained
     else:
         rel2 = unconstrained_reliability(wsqrt(average(qr2)), max_spread)
     interval_check(rel2)
+    if legacy:
+        zeros = [0] * len(rcols)
+        return RoundResult(c1, qr, [i for i, _ in ordered], reliable, consensus, rel1, rel2, zeros, list(zeros))
     means = [average(c) for c in rcols]
     variances = [variance(c, m) for c, m in zip(rcols, means)]
     skew = [skewness(c, m, v) for c, m, v in zip(rcols, means, variances)]
@@ -262,8 +268,10 @@ class ReferenceContract:
 
     def __init__(self, admins: Sequence[int], enable_oracle_replacement: bool,
                  required_majority: int, n_failing_oracles: int, constrained: bool,
-                 unconstrained_max_spread: int, dimension: int, oracles: Sequence[int]):
-        # constructor, contract.cairo:235-265
+                 unconstrained_max_spread: int, dimension: int, oracles: Sequence[int],
+                 legacy: bool = False):
+        # constructor, contract.cairo:235-265 (legacy: contract/obsolete/src/contract_nd.cairo)
+        self.legacy = bool(legacy)
         self.dimension = dimension
         self.admins = list(admins)
         self.oracles = [OracleInfo(a) for a in oracles]
@@ -318,7 +326,7 @@ class ReferenceContract:
         if self.n_active_oracles != len(self.oracles):
             return Status.NOT_ACTIVE
         r = consensus_round(self.values, self.n_failing_oracles, self.constrained,
-                            self.unconstrained_max_spread)
+                            self.unconstrained_max_spread, self.legacy)
         for i, o in enumerate(self.oracles):
             o.reliable = r.reliable[i]
         self.consensus_value = r.consensus
@@ -434,9 +442,9 @@ class ReferenceContract:
         return self.propositions[which_admin]
 
 
-def round_status(values, n_failing, constrained, max_spread=0) -> Tuple[Status, Optional[RoundResult]]:
+def round_status(values, n_failing, constrained, max_spread=0, legacy=False) -> Tuple[Status, Optional[RoundResult]]:
     """Functional wrapper: (status, result-or-None) instead of raising."""
     try:
-        return Status.OK, consensus_round(values, n_failing, constrained, max_spread)
+        return Status.OK, consensus_round(values, n_failing, constrained, max_spread, legacy)
     except ConsensusRevert as e:
         return e.status, None

@@ -21,19 +21,20 @@ def alloc_exact_out(B, N, D, device):
         status=torch.full((B,), -1, dtype=torch.int32, device=device))
 
 
-def run_fast(values, D, n_failing, constrained, max_spread=1.0, active=None, wave_hint=0):
+def run_fast(values, D, n_failing, constrained, max_spread=1.0, active=None, wave_hint=0, legacy=False):
     B, N = values.shape[:2]
     o = alloc_fast_out(B, N, D, values.device)
     svops.ops().fast_round(values, active, D, n_failing, constrained, max_spread, o["c1"], o["consensus"],
-                           o["skew"], o["kurt"], o["rel"], o["qr"], o["reliable"], o["status"], wave_hint)
+                           o["skew"], o["kurt"], o["rel"], o["qr"], o["reliable"], o["status"], wave_hint,
+                           0, 0, legacy)
     return o
 
 
-def run_exact(values, n_failing, constrained, max_spread=0, active=None):
+def run_exact(values, n_failing, constrained, max_spread=0, active=None, legacy=False):
     B, N, D = values.shape
     o = alloc_exact_out(B, N, D, values.device)
     svops.ops().exact_round(values, active, n_failing, constrained, max_spread, o["c1"], o["consensus"],
-                            o["skew"], o["kurt"], o["rel"], o["qr"], o["reliable"], o["status"])
+                            o["skew"], o["kurt"], o["rel"], o["qr"], o["reliable"], o["status"], legacy)
     return o
 
 

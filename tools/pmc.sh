@@ -1,11 +1,13 @@
 #!/bin/bash
-# PMC counters for the fused consensus kernel (kernel-trace + pmc only; no sys/runtime traces).
+# PMC counters for the consensus kernels (kernel-trace + pmc only; no sys/runtime traces).
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"; R=$(pwd); mkdir -p gpurun_out
 CFG=${CFG:-c2}
+SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"
+      "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_INSTS_SMEM SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE SQ_INST_LEVEL_LDS SQ_INSTS_VMEM")
+[ -n "${MEMSET:-}" ] && SETS+=("$MEMSET")
 i=0
-for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" \
-           "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_INSTS_SMEM SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE SQ_INST_LEVEL_LDS SQ_INSTS_VMEM"; do
+for set in "${SETS[@]}"; do
   i=$((i+1))
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex consensus_fast \
      --output-format csv -d $R/gpurun_out/pmc_${CFG}_$i -o run -- python3 $R/bench.py --config $CFG --steps 3 --warmup 1 --graph 0 ${EXTRA:-} \
