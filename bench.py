@@ -28,6 +28,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 CONFIGS = {
+    # f = 0: with 4 oracles any f >= 1 leaves R <= 3 reliable and the contract's kurtosis divides
+    # by (n-2)(n-3) = 0 (math.cairo:362) -- every round would revert
+    "c1": dict(model="plumbing: 4 oracles x 2 dims, one exact (wsad) round per step on the CPU engine", N=4, D=2,
+               f=0, batch=1, update_frac=0.0, device="cpu", mode="exact", dtype="int64-wsad"),
     "c3": dict(model="svoc-consensus N=256 D=4096 streaming (f=32, constrained)", N=256, D=4096, f=32,
                batch=1024, update_frac=0.25),
     "c2": dict(model="svoc-consensus N=64 D=1024 batched (f=8, constrained)", N=64, D=1024, f=8,
@@ -49,6 +53,9 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="instances per GPU (default per config)")
     ap.add_argument("--wave-hint", type=int, default=0)
     ap.add_argument("--graph", type=int, default=1, help="capture the step in a HIP graph")
+    ap.add_argument("--log", default=None, help="append the result record to this JSON-lines file")
+    ap.add_argument("--kernel-table", type=int, default=0, help="profile N extra steps (torch.profiler) "
+                    "after the timed region and add the per-kernel table to the log record")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -57,16 +64,20 @@ def main():
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    c = CONFIGS[args.config]
+    dev = torch.device("cuda", local) if c.get("device", "cuda") == "cuda" else torch.device("cpu")
 
     from svoc.config import ConsensusConfig
     from svoc.engine import ConsensusEngine
     from svoc.parallel.dp import DataParallelConsensus
 
-    c = CONFIGS[args.config]
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
     B = args.batch or c["batch"]
     cfg = ConsensusConfig(n_oracles=c["N"], dimension=c["D"], n_failing_oracles=c["f"], constrained=True)
-    eng = ConsensusEngine(cfg, batch=B, device=dev, mode="fast")
+    eng = ConsensusEngine(cfg, batch=B, device=dev, mode=c.get("mode", "fast"))
     eng.wave_hint = args.wave_hint
     dp = DataParallelConsensus(eng, rank=rank, world=world)
     eng.randomize(seed=1000 + rank)
@@ -126,10 +137,10 @@ def main():
     for i in range(args.warmup):
         step(i)
         dp.reduce()
-    torch.cuda.synchronize(dev)
+    sync()
 
     graph = None
-    if args.graph:
+    if args.graph and dev.type == "cuda":
         # the stream cycles with period `pool`: capture one period and replay it
         period = stream.pool if stream is not None else (2 if (pipe is not None or gov is not None) else 1)
         s = torch.cuda.Stream(device=dev)
@@ -138,7 +149,7 @@ def main():
             for i in range(period):
                 step(i)
         torch.cuda.current_stream(dev).wait_stream(s)
-        torch.cuda.synchronize(dev)
+        sync()
         try:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
@@ -152,7 +163,7 @@ def main():
 
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     if graph is not None:
         reps, rem = divmod(args.steps, graph_period)
@@ -168,7 +179,7 @@ def main():
             step(i)
             dp.reduce()
         steps_done = args.steps
-    torch.cuda.synchronize(dev)
+    sync()
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
@@ -184,14 +195,25 @@ def main():
         out = {
             "metric": METRIC, "value": value, "unit": "consensus rounds/s", "n_gpus": world,
             "steps": steps_done, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": c.get("dtype", "bf16"), "data": "synthetic",
             "config": {"model": c["model"], "global_batch": B * world, "seq_len": c["D"],
                        "parallelism": f"dp{world}", "n_oracles": c["N"], "dimension": c["D"],
                        "n_failing": c["f"], "updates_per_instance_per_step": U_per_inst,
                        "oracle_updates_per_s": (U_per_inst * rounds / el) if U_per_inst else 0.0,
                        "hip_graph": graph is not None, "ok_fraction": ok, **extra},
         }
+        if args.config in ("c2", "c3"):
+            from svoc.utils.metrics import algorithmic_bytes_per_round
+            out["config"]["hbm_gbps_algorithmic"] = algorithmic_bytes_per_round(c["N"], c["D"]) * rounds / el / 1e9
         print(json.dumps(out))
+        if args.log:
+            from svoc.utils.metrics import JsonlLogger, engine_health, kernel_table
+            rec = dict(out)
+            rec["health"] = engine_health(eng)
+            if args.kernel_table:
+                rec["kernels"] = kernel_table(lambda: step(0), steps=args.kernel_table)
+            with JsonlLogger(args.log, rank) as lg:
+                lg.log("bench", **rec)
     if world > 1:
         dist.destroy_process_group()
 

@@ -1,0 +1,156 @@
+// Host self-test of the native CPU runtime, built with sanitizers by tools/sanitize_host.sh
+// (AddressSanitizer + UBSan, and ThreadSanitizer for the threaded batch loops).  GPU sanitizers are
+// not available on the target pool, so the host code paths shared with the kernels (wsad.hpp,
+// governance.hpp) and the host-only engines / checkpoint IO are exercised here instead.
+//
+// Checks: the reference fixture's golden outputs (contract/tests/test_contract.cairo:
+// 150-158), threaded batch == sequential single-instance results (exact and fast engines),
+// governance state machine invariants, and a .svoc save/load round trip with CRC verification.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "engine.hpp"
+#include "svoc/governance.hpp"
+#include "svoc_io.hpp"
+
+using namespace svoc;
+
+static int failures = 0;
+#define CHECK(c)                                                       \
+  do {                                                                 \
+    if (!(c)) {                                                        \
+      std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      ++failures;                                                      \
+    }                                                                  \
+  } while (0)
+
+static void golden_fixture() {
+  const int64_t X[7][2] = {{492954, 334814}, {437692, 410445}, {967794, 564219}, {431029, 387225},
+                           {487609, 337990}, {284178, 485072}, {990059, 558600}};
+  int64_t c1[2], qr[7], cons[2], sk[2], ku[2];
+  uint8_t rel[7];
+  ExactOut o{c1, qr, rel, cons, sk, ku, 0, 0};
+  const int st = exact_round_one(&X[0][0], 7, 2, 2, true, 0, o);
+  CHECK(st == ST_OK);
+  CHECK(c1[0] == 462650 && c1[1] == 398835);
+  CHECK(cons[0] == 434360 && cons[1] == 362607);
+  CHECK(o.rel1 == 573480 && o.rel2 == 857846);
+  CHECK(sk[0] == -2294596 && sk[1] == 1263429);
+  CHECK(ku[0] == 9083020 && ku[1] == 4989576);
+  const uint8_t exp_rel[7] = {1, 1, 0, 1, 1, 1, 0};
+  CHECK(std::memcmp(rel, exp_rel, 7) == 0);
+  // documented panics become status codes: sqrt(1 ulp) divides by zero (math.cairo:277)
+  int s2 = ST_OK;
+  (void)wsqrt(1, s2);
+  CHECK(s2 == ST_DIV_BY_ZERO);
+}
+
+static void batch_vs_single(int threads) {
+  std::mt19937_64 rng(7);
+  const int64_t B = 64, N = 33, D = 5;
+  std::vector<int64_t> X(B * N * D);
+  for (auto& v : X) v = 300000 + (int64_t)(rng() % 400000);
+  std::vector<int64_t> cons(B * D), sk(B * D), ku(B * D), qr(B * N), c1(B * D), rel(B * 2);
+  std::vector<uint8_t> reliable(B * N);
+  std::vector<int32_t> status(B);
+  ExactBatch eb{};
+  eb.values = X.data(); eb.B = B; eb.N = N; eb.D = D; eb.n_failing = 4; eb.constrained = true;
+  eb.consensus = cons.data(); eb.rel = rel.data(); eb.skew = sk.data(); eb.kurt = ku.data();
+  eb.reliable = reliable.data(); eb.qr = qr.data(); eb.c1 = c1.data(); eb.status = status.data();
+  exact_round_batch_cpu(eb, threads);
+  for (int64_t b = 0; b < B; ++b) {
+    std::vector<int64_t> c(D), q(N), cs(D), s(D), k(D);
+    std::vector<uint8_t> r(N);
+    ExactOut o{c.data(), q.data(), r.data(), cs.data(), s.data(), k.data(), 0, 0};
+    const int st = exact_round_one(X.data() + b * N * D, N, D, 4, true, 0, o);
+    CHECK(st == status[b]);
+    if (st == ST_OK) {
+      CHECK(std::memcmp(cs.data(), cons.data() + b * D, D * 8) == 0);
+      CHECK(std::memcmp(k.data(), ku.data() + b * D, D * 8) == 0);
+      CHECK(o.rel2 == rel[b * 2 + 1]);
+    }
+  }
+  // fast engine, threaded
+  std::vector<float> xf(B * N * D);
+  for (size_t i = 0; i < xf.size(); ++i) xf[i] = (float)X[i] * 1e-6f;
+  std::vector<float> f_c1(B * D), f_cons(B * D), f_rel(B * 2), f_sk(B * D), f_ku(B * D), f_qr(B * N);
+  std::vector<uint8_t> f_reliable(B * N);
+  std::vector<int32_t> f_status(B);
+  FastBatch fb;
+  fb.values = xf.data();
+  fb.load = [&](const void* base, int64_t i, float* dst) {
+    std::memcpy(dst, (const float*)base + i * N * D, N * D * sizeof(float));
+  };
+  fb.active = nullptr; fb.B = B; fb.N = N; fb.D = D; fb.n_failing = 4; fb.constrained = true;
+  fb.max_spread = 1.f; fb.c1 = f_c1.data(); fb.consensus = f_cons.data(); fb.rel = f_rel.data();
+  fb.skew = f_sk.data(); fb.kurt = f_ku.data(); fb.reliable = f_reliable.data(); fb.qr = f_qr.data();
+  fb.status = f_status.data();
+  fast_round_batch_cpu(fb, threads);
+  for (int64_t b = 0; b < B; ++b) CHECK(f_status[b] == ST_OK || f_status[b] == ST_ZERO_VARIANCE);
+}
+
+static void governance_flow() {
+  const int A = 3, N = 4;
+  int64_t admins[A * 4] = {0}, oracles[N * 4] = {0}, prop_addr[A * 4] = {0};
+  uint64_t votes[A] = {0};
+  int8_t prop_tag[A] = {0};
+  int32_t prop_idx[A] = {0};
+  for (int a = 0; a < A; ++a) admins[a * 4] = 100 + a;
+  for (int o = 0; o < N; ++o) oracles[o * 4] = 500 + o;
+  GovState g{};
+  g.admins = admins; g.oracle_addr = oracles; g.votes = votes; g.prop_tag = prop_tag;
+  g.prop_idx = prop_idx; g.prop_addr = prop_addr; g.B = 1; g.A = A; g.N = N; g.enable = 1; g.majority = 2;
+  int64_t inst[1] = {0}, caller[4] = {100, 0, 0, 0}, a1[1] = {2}, addr[4] = {999, 0, 0, 0};
+  int32_t kind[1] = {0}, a0[1] = {1}, st[1] = {0};
+  uint8_t applied[1] = {0};
+  GovAction act{};
+  act.inst = inst; act.caller = caller; act.kind = kind; act.arg0 = a0; act.arg1 = a1; act.addr = addr;
+  act.status = st; act.applied = applied; act.K = 1;
+  CHECK(gov_apply_one(g, act, 0) == ST_OK);  // admin 0 proposes oracle 2 -> 999 (self-vote)
+  caller[0] = 101; kind[0] = 1; a0[0] = 0; a1[0] = 1;
+  CHECK(gov_apply_one(g, act, 0) == ST_OK);  // admin 1 supports: majority 2 reached
+  CHECK(applied[0] == 1 && oracles[2 * 4] == 999);
+  caller[0] = 77;
+  CHECK(gov_apply_one(g, act, 0) == ST_NOT_ADMIN);
+}
+
+static void io_roundtrip() {
+  std::vector<io::Section> secs(2);
+  secs[0].name = "values"; secs[0].dtype = io::DType::I64; secs[0].shape = {2, 3};
+  for (int i = 0; i < 6; ++i) {
+    int64_t v = (int64_t)i * -123456789;
+    const uint8_t* p = (const uint8_t*)&v;
+    secs[0].bytes.insert(secs[0].bytes.end(), p, p + 8);
+  }
+  int64_t w[2] = {-5, 1234567};
+  secs[1].name = "wide"; secs[1].dtype = io::DType::I128; secs[1].shape = {2};
+  secs[1].bytes = io::i64_to_i128(w, 2);
+  const std::string path = std::string(std::getenv("TMPDIR") ? std::getenv("TMPDIR") : "/tmp") + "/svoc_selftest.svoc";
+  io::save(path, "{\"selftest\": true}", secs);
+  std::vector<io::Section> back;
+  const std::string meta = io::load(path, back);
+  CHECK(meta.find("selftest") != std::string::npos);
+  CHECK(back.size() == 2 && back[0].bytes == secs[0].bytes && back[1].bytes == secs[1].bytes);
+  int64_t w2[2];
+  io::i128_to_i64(back[1].bytes.data(), 2, w2);
+  CHECK(w2[0] == -5 && w2[1] == 1234567);
+  std::remove(path.c_str());
+}
+
+int main(int argc, char** argv) {
+  const int threads = argc > 1 ? std::atoi(argv[1]) : 8;
+  golden_fixture();
+  batch_vs_single(threads);
+  governance_flow();
+  io_roundtrip();
+  if (failures) {
+    std::fprintf(stderr, "%d check(s) failed\n", failures);
+    return 1;
+  }
+  std::printf("engine selftest OK (threads=%d)\n", threads);
+  return 0;
+}
