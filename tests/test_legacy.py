@@ -150,10 +150,15 @@ def test_legacy_gpu_exact_and_fast(constrained):
     for k in ("status", "consensus", "rel", "qr", "skew", "kurt", "reliable"):
         assert torch.equal(oc[k], og[k].cpu()), k
     from helpers import beta_oracles
-    xb, _ = beta_oracles(12, 64, 300, 8, seed=2)
+    # without /D a constrained round only passes the interval check for small D (RMS over all
+    # dims <= 0.5): D = 3 constrained, D = 300 unconstrained
+    D = 3 if constrained else 300
+    xb, _ = beta_oracles(12, 64, D, 8, seed=2)
     for hint in (0, 1):
-        o = run_fast(xb.cuda(), 300, 8, constrained, 1.0, wave_hint=hint, legacy=True)
-        r = torch_ref.fast_round(xb.cuda()[:, :, :300], 8, constrained, 1.0, legacy=True)
+        o = run_fast(xb.cuda(), D, 8, constrained, 30.0, wave_hint=hint, legacy=True)
+        r = torch_ref.fast_round(xb.cuda()[:, :, :D], 8, constrained, 30.0, legacy=True)
+        oc = run_fast(xb, D, 8, constrained, 30.0, legacy=True)
+        assert torch.equal(o["status"].cpu(), oc["status"])
         ok = o["status"] == 0
         assert ok.all()
         torch.testing.assert_close(o["rel"], r["rel"], rtol=1e-4, atol=1e-4)
