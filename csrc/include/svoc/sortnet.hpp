@@ -99,17 +99,20 @@ SVOC_DEV void sort64(u16x2 (&r)[64]) {
 // bitonic's 672, and when only a few outputs are consumed (the two middle order statistics) dead
 // code elimination prunes it to ~414 (bitonic: 543).  The comparator list is a compile-time table;
 // the fully unrolled loop indexes registers with constants only.
-struct CmpNet64 {
-  unsigned char a[543], b[543];
+template <int NN>
+struct CmpNet {
+  static constexpr int kMax = NN * 16;  // >= comparators of Batcher's network for NN <= 64
+  unsigned char a[kMax], b[kMax];
   int n;
 };
-constexpr CmpNet64 make_oem64() {
-  CmpNet64 t{};
+template <int NN>
+constexpr CmpNet<NN> make_oem() {
+  CmpNet<NN> t{};
   int c = 0;
-  for (int p = 1; p < 64; p <<= 1)
+  for (int p = 1; p < NN; p <<= 1)
     for (int k = p; k >= 1; k >>= 1)
-      for (int j = k % p; j + k < 64; j += 2 * k)
-        for (int i = 0; i < k && i + j + k < 64; ++i)
+      for (int j = k % p; j + k < NN; j += 2 * k)
+        for (int i = 0; i < k && i + j + k < NN; ++i)
           if ((i + j) / (2 * p) == (i + j + k) / (2 * p)) {
             t.a[c] = (unsigned char)(i + j);
             t.b[c] = (unsigned char)(i + j + k);
@@ -118,15 +121,20 @@ constexpr CmpNet64 make_oem64() {
   t.n = c;
   return t;
 }
-SVOC_DEV void sort64_oem(u16x2 (&r)[64]) {
-  constexpr CmpNet64 T = make_oem64();
-  static_assert(T.n == 543, "odd-even merge sort of 64");
+// In-register odd-even merge sort of NN keys (NN a power of two <= 64).
+template <int NN, class K>
+SVOC_DEV void sort_oem(K (&r)[NN]) {
+  constexpr CmpNet<NN> T = make_oem<NN>();
 #pragma unroll
-  for (int c = 0; c < 543; ++c) {
-    const u16x2 x = r[T.a[c]], y = r[T.b[c]];
+  for (int c = 0; c < T.n; ++c) {
+    const K x = r[T.a[c]], y = r[T.b[c]];
     r[T.a[c]] = kmin(x, y);
     r[T.b[c]] = kmax(x, y);
   }
+}
+SVOC_DEV void sort64_oem(u16x2 (&r)[64]) {
+  static_assert(make_oem<64>().n == 543, "odd-even merge sort of 64");
+  sort_oem<64>(r);
 }
 
 // Ascending half-cleaner cascade (strides 32..1): sorts a bitonic lane-local sequence.

@@ -25,7 +25,9 @@ def _cmp_fast(o, r, ok):
 
 _SHAPES = [(7, 6, 2, True), (64, 1024, 8, True), (64, 1000, 8, False), (50, 300, 5, True),
            (128, 512, 16, True), (100, 260, 10, False), (256, 4096, 32, True), (256, 600, 32, False),
-           (200, 136, 20, True), (20, 8, 15, True)]
+           (200, 136, 20, True), (20, 8, 15, True),
+           # small-instance kernel (N <= 16, D <= 128) under hint 0
+           (7, 6, 2, False), (16, 100, 3, True), (9, 1, 2, True), (12, 128, 4, False), (8, 33, 2, True)]
 
 
 # hint 0: register-streaming fused kernel (default); -1: its split two-launch form; -3 / -4: 8 / 2
@@ -46,6 +48,23 @@ def test_fast_hip_vs_torch(N, D, f, constrained, hint):
     # the CPU engine agrees on status
     oc = run_fast(x, D, f, constrained, 1.0)
     assert torch.equal(oc["status"], o["status"].cpu())
+
+
+def test_fast_small_kernel_batch_edges():
+    """Deployed config 7 x 6: partial last workgroup, inactive instances, reverts, vs the CPU engine."""
+    B, N, D = 1000, 7, 6
+    x, _ = beta_oracles(B, N, D, 2, seed=21)
+    x[5] = 0.0                               # zero variance (non-fatal flag)
+    x[6, :4, :D] = 0.0                       # rel1 < 0 -> RELIABILITY_INTERVAL
+    x[6, 4:, :D] = 1.0
+    active = (torch.arange(B) % 7 != 3).to(torch.uint8)
+    o = run_fast(x.to(DEV), D, 2, True, 1.0, active=active.to(DEV))
+    oc = run_fast(x, D, 2, True, 1.0, active=active)
+    assert torch.equal(o["status"].cpu(), oc["status"])
+    ok = o["status"].cpu() == 0
+    assert ok.sum() > 800
+    r = torch_ref.fast_round(x[:, :, :D], 2, True, 1.0)
+    _cmp_fast({k: v.cpu() for k, v in o.items()}, r, ok)
 
 
 def test_fast_hip_active_mask_and_revert():
