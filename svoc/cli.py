@@ -52,6 +52,7 @@ Commands :
     - (S) update_proposition <caller_admin> <old_oracle> <new_oracle>
     - (S) vote_for_a_proposition <caller_admin> <which_admin> yes/no
     - save <path> / load <path>           [.svoc checkpoint of the engine state]
+    - report <path>                       [static HTML: scatter per label pair, reliability bars]
 For <admin> <oracle> arguments, you can either specify the index or the address starting with "0x".
 (S) = the consensus engine (the reference's Sepolia contract).
 """
@@ -196,6 +197,11 @@ class Client:
                     return "usage: vote_for_a_proposition <caller_admin> <which_admin> yes/no"
                 applied = c.vote_for_a_proposition(caller, which, ok)
                 return "vote recorded" + (" -> oracle replaced" if applied else "")
+            if cmd == "report" and args:
+                from .utils.report import write_report
+                labels = ORACLE_LABELS[: self.dimension] if self.dimension <= len(ORACLE_LABELS) else None
+                write_report(args[0], c.engine, [0], labels, c.get_oracle_list())
+                return f"report written to {args[0]}"
             if cmd in ("save", "load") and args:
                 from . import state
                 if cmd == "save":

@@ -27,3 +27,13 @@ def test_fetch_commit_resume_governance(tmp_path):
     assert cl.query("oracle_list").splitlines()[6] == "0x1234"
     assert "unknown" in cl.query("frobnicate")
     assert "Commands" in cl.query("help")
+
+
+def test_report_html(tmp_path):
+    cl = Client(device="cpu", mode="exact", db_path=str(tmp_path / "db.sqlite"), seed=1)
+    cl.query("fetch")
+    cl.query("commit")
+    out = tmp_path / "r.html"
+    assert cl.query(f"report {out}").startswith("report written")
+    doc = out.read_text()
+    assert doc.count("<svg") == 3 and "reliability (second pass)" in doc and "optimism / anger" in doc
