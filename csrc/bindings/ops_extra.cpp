@@ -116,18 +116,21 @@ void register_extra_defs(torch::Library& m) {
   register_governance_defs(m);
   register_generator_defs(m);
   register_io_defs(m);
+  register_bookkeeping_defs(m);
 }
 
 void register_extra_cpu(torch::Library& m) {
   m.impl("apply_updates", &apply_updates_cpu);
   register_governance_cpu(m);
   register_generator_cpu(m);
+  register_bookkeeping_cpu(m);
 }
 
 void register_extra_hip(torch::Library& m) {
   m.impl("apply_updates", &apply_updates_hip);
   register_governance_hip(m);
   register_generator_hip(m);
+  register_bookkeeping_hip(m);
 }
 
 }  // namespace svoc

@@ -18,4 +18,7 @@ void register_generator_cpu(torch::Library& m);
 void register_generator_hip(torch::Library& m);
 void register_io_defs(torch::Library& m);
 void register_io_cpu(torch::Library& m);
+void register_bookkeeping_defs(torch::Library& m);
+void register_bookkeeping_cpu(torch::Library& m);
+void register_bookkeeping_hip(torch::Library& m);
 }  // namespace svoc

@@ -2,7 +2,8 @@
 // (constrained inputs must lie in [0, 1] / [0, WSAD]: 'interval error', math.cairo:298-310),
 // pick the last valid writer per (instance, oracle) with an atomicMax on the update sequence
 // number (coalescing is exact: survey §2.8-13), copy the winning rows with 16-B vector stores,
-// flip `enabled` and bump n_active_oracles on first commit.  Three launches, no host sync.
+// flip `enabled` and bump n_active_oracles on first commit.  Three launches, no host sync; each
+// update gets L lanes sized to its row, so tiny rows pack 64 updates per wave.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -28,52 +29,73 @@ __device__ __forceinline__ bool bf16_unit(uint32_t raw16) {  // 0 <= x <= 1 (and
   return raw16 <= 0x3f80u || raw16 == 0x8000u;
 }
 
-// one wave per update: validate (wave-parallel over D, 16-B loads when rows allow), then claim the
-// (instance, oracle) slot with an atomicMax on the update's sequence number
-__global__ __launch_bounds__(256) void upd_validate_kernel(UpdateParams p) {
-  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+// L lanes per update (L = power of two covering the row in 16-B chunks, capped at 64): a wave
+// serves 64/L updates, so the deployed 7 x 6 config (12-B rows) runs 64 updates per wave instead of
+// one, and wide rows (c3: 8 KiB) get a whole wave each.  True iff all L lanes of the group agree.
+template <int L>
+__device__ __forceinline__ bool group_all(bool ok) {
+  const uint64_t bad = __ballot(!ok);
   const int lane = threadIdx.x & 63;
-  if (u >= p.U) return;
-  const int64_t b = p.inst[u], o = p.oracle[u];
+  const uint64_t gm = (L == 64) ? ~0ull : (((1ull << L) - 1ull) << (lane & ~(L - 1)));
+  return (bad & gm) == 0;
+}
+
+// validate every update, then claim its (instance, oracle) slot with an atomicMax on the update's
+// sequence number: the last valid writer wins (coalescing is exact: survey §2.8-13)
+template <int L>
+__global__ __launch_bounds__(256) void upd_validate_kernel(UpdateParams p) {
+  const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
+  const int sub = threadIdx.x & (L - 1);
+  const bool in = u < p.U;
   int st = ST_OK;
-  if (b < 0 || b >= p.B || o < 0 || o >= p.N) st = ST_NOT_ORACLE;
-  if (st == ST_OK && p.constrained) {
-    bool ok = true;
+  int64_t b = 0, o = 0;
+  if (in) {
+    b = p.inst[u];
+    o = p.oracle[u];
+    if (b < 0 || b >= p.B || o < 0 || o >= p.N) st = ST_NOT_ORACLE;
+  }
+  bool ok = true;
+  if (in && st == ST_OK && p.constrained) {
     const uint16_t* row = (const uint16_t*)p.upd + u * p.D;
     if (p.dtype == 0 && (p.D & 7) == 0 && (((uintptr_t)row) & 15) == 0) {
-      for (int c = lane; c < p.D / 8; c += 64) {
+      for (int c = sub; c < p.D / 8; c += L) {
         const uint4 v = ((const uint4*)row)[c];
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) ok = ok && bf16_unit(w[k] & 0xffffu) && bf16_unit(w[k] >> 16);
       }
     } else {
-      for (int d = lane; d < p.D; d += 64) ok = ok && in_range(p, u, d);
+      for (int d = sub; d < p.D; d += L) ok = ok && in_range(p, u, d);
     }
-    if (!__all(ok)) st = ST_INTERVAL_INPUT;
   }
-  if (lane == 0) {
+  ok = group_all<L>(ok);  // all lanes reach the ballot (no early return above)
+  if (in && sub == 0) {
+    if (st == ST_OK && !ok) st = ST_INTERVAL_INPUT;
     p.upd_status[u] = st;
     if (st == ST_OK) atomicMax(&p.winner[b * p.N + o], (int)u);
   }
 }
 
-// one workgroup per update: the winner copies its row
+// the winner of each slot copies its row (16-B vectors when aligned), flips `enabled`, bumps
+// n_active_oracles on an oracle's first commit (contract.cairo:331-343) and marks the instance
+template <int L>
 __global__ __launch_bounds__(256) void upd_apply_kernel(UpdateParams p) {
-  const int64_t u = blockIdx.x;
-  if (p.upd_status[u] != ST_OK) return;
+  const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
+  const int sub = threadIdx.x & (L - 1);
+  if (u >= p.U || p.upd_status[u] != ST_OK) return;
   const int64_t b = p.inst[u], o = p.oracle[u];
   if (p.winner[b * p.N + o] != (int)u) return;  // superseded by a later update: coalesced
   const int64_t row_bytes = (int64_t)p.D * p.elem_bytes;
   unsigned char* dst = (unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes;
   const unsigned char* src = (const unsigned char*)p.upd + u * row_bytes;
   if (((uintptr_t)dst & 15) == 0 && ((uintptr_t)src & 15) == 0 && (row_bytes & 15) == 0) {
-    for (int64_t i = threadIdx.x; i < row_bytes / 16; i += blockDim.x)
-      ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    for (int64_t i = sub; i < row_bytes / 16; i += L) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+  } else if (((uintptr_t)dst & 3) == 0 && ((uintptr_t)src & 3) == 0 && (row_bytes & 3) == 0) {
+    for (int64_t i = sub; i < row_bytes / 4; i += L) ((uint32_t*)dst)[i] = ((const uint32_t*)src)[i];
   } else {
-    for (int64_t i = threadIdx.x; i < row_bytes; i += blockDim.x) dst[i] = src[i];
+    for (int64_t i = sub; i < row_bytes; i += L) dst[i] = src[i];
   }
-  if (threadIdx.x == 0) {
+  if (sub == 0) {
     if (!p.enabled[b * p.N + o]) {
       p.enabled[b * p.N + o] = 1;
       atomicAdd(&p.n_active[b], 1);
@@ -88,14 +110,28 @@ __global__ __launch_bounds__(256) void upd_reset_kernel(UpdateParams p) {
   p.winner[p.inst[u] * p.N + p.oracle[u]] = -1;
 }
 
+template <int L>
+static int launch_updates(const UpdateParams& p, hipStream_t stream) {
+  const int64_t blocks = ((int64_t)p.U * L + 255) / 256;
+  hipLaunchKernelGGL(upd_validate_kernel<L>, dim3((unsigned)blocks), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL(upd_apply_kernel<L>, dim3((unsigned)blocks), dim3(256), 0, stream, p);
+  hipLaunchKernelGGL(upd_reset_kernel, dim3((unsigned)((p.U + 255) / 256)), dim3(256), 0, stream, p);
+  return (int)hipGetLastError();
+}
+
 }  // namespace svoc
 
 using namespace svoc;
 
 extern "C" int svoc_apply_updates(const UpdateParams* p, hipStream_t stream) {
   if (p->U <= 0) return 0;
-  hipLaunchKernelGGL(upd_validate_kernel, dim3((p->U + 3) / 4), dim3(256), 0, stream, *p);
-  hipLaunchKernelGGL(upd_apply_kernel, dim3(p->U), dim3(256), 0, stream, *p);
-  hipLaunchKernelGGL(upd_reset_kernel, dim3((p->U + 255) / 256), dim3(256), 0, stream, *p);
-  return (int)hipGetLastError();
+  if ((int64_t)p->U * 64 / 256 >= 0x7fffffffll) return -1;
+  const int64_t chunks = ((int64_t)p->D * p->elem_bytes + 15) / 16;  // 16-B pieces per row
+  if (chunks <= 1) return launch_updates<1>(*p, stream);
+  if (chunks <= 2) return launch_updates<2>(*p, stream);
+  if (chunks <= 4) return launch_updates<4>(*p, stream);
+  if (chunks <= 8) return launch_updates<8>(*p, stream);
+  if (chunks <= 16) return launch_updates<16>(*p, stream);
+  if (chunks <= 32) return launch_updates<32>(*p, stream);
+  return launch_updates<64>(*p, stream);
 }

@@ -79,6 +79,9 @@ class ConsensusEngine:
         self._active = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.wave_hint = 0
         self.rounds = 0
+        # health counters folded in by every round's epilogue: [rel2 sum (2^-32 units fast / wsad
+        # exact), committed, processed, reverted]
+        self.metrics_fx = torch.zeros(4, dtype=torch.int64, device=dev)
 
     # ------------------------------------------------------------------ sizing
     @staticmethod
@@ -111,25 +114,31 @@ class ConsensusEngine:
 
     # ------------------------------------------------------------------ rounds
     def run_round(self, only_touched: bool = True) -> None:
-        """Consensus round for every instance that is fully active (and touched, by default)."""
-        full = self.n_active == self.N
-        act = full & (self.touched.bool() if only_touched else torch.ones_like(full))
-        self._active.copy_(act)
+        """Consensus round for every instance that is fully active (and touched, by default).
+
+        Three launches: the prologue selects the instances (n_active == N, touched), the fused
+        round kernel, and the epilogue commits consensus_active, clears touched and folds the
+        round's health counters into :attr:`metrics_fx` (integers: deterministic sums)."""
+        self._ops.round_prologue(self.n_active, self.touched, self.N, bool(only_touched), self._active)
         mx = self.cfg.unconstrained_max_spread
         if self.mode == "fast":
             self._ops.fast_round(self.values, self._active, self.D, self.cfg.n_failing_oracles,
                                  self.cfg.constrained, float(mx), self.c1, self.consensus, self.skew,
                                  self.kurt, self.rel, self.qr, self.reliable, self.status, self.wave_hint,
                                  0, 0, self.cfg.legacy)
-            ok = (self.status == Status.OK) | (self.status == Status.ZERO_VARIANCE)
         else:
             self._ops.exact_round(self.values, self._active, self.cfg.n_failing_oracles, self.cfg.constrained,
                                   self.cfg.max_spread_wsad, self.c1, self.consensus, self.skew, self.kurt,
                                   self.rel, self.qr, self.reliable, self.status, self.cfg.legacy)
-            ok = self.status == Status.OK
-        self.consensus_active |= act & ok
-        self.touched.zero_()
+        self._ops.round_epilogue(self._active, self.status, self.rel, self.consensus_active, self.touched,
+                                 self.metrics_fx)
         self.rounds += 1
+
+    def metrics(self) -> torch.Tensor:
+        """[sum rel2 of committed rounds, committed, processed, reverted] as float64 (device)."""
+        m = self.metrics_fx.double()
+        m[0] *= (2.0 ** -32) if self.mode == "fast" else 1e-6
+        return m
 
     def step(self, inst, oracle, vals) -> torch.Tensor:
         """update_prediction for a batch of (instance, oracle, prediction) + the consensus rounds.

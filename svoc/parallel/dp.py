@@ -27,7 +27,7 @@ class DataParallelConsensus:
         self.group = group
         dev = engine.device
         # [rel2 sum over committed rounds, committed rounds, processed rounds, reverted rounds]
-        self._local = torch.zeros(4, dtype=torch.float64, device=dev)
+        self._fx = torch.zeros(4, dtype=torch.int64, device=dev)
         self._global = torch.zeros(4, dtype=torch.float64, device=dev)
 
     # -- sharding ---------------------------------------------------------------------------------
@@ -40,20 +40,18 @@ class DataParallelConsensus:
 
     # -- metrics ----------------------------------------------------------------------------------
     def accumulate(self) -> None:
-        """Fold the last round's outcome into the local metric buffer (device-only, capturable)."""
-        e = self.engine
-        act = e._active.bool()
-        ok = act & ((e.status == Status.OK) | (e.status == Status.ZERO_VARIANCE))
-        rel2 = e.rel[:, 1].double()
-        upd = torch.stack([torch.where(ok, rel2, 0).sum(), ok.sum().double(), act.sum().double(),
-                           (act & ~ok).sum().double()])
-        self._local += upd
+        """Kept for API compatibility: every round's epilogue kernel already folds its outcome into
+        ``engine.metrics_fx`` (integer counters, device-only, capturable)."""
 
     def reduce(self) -> torch.Tensor:
-        """One all-reduce of the accumulated metrics (RCCL on GPU)."""
-        self._global.copy_(self._local)
+        """One all-reduce of the integer counters (RCCL on GPU), then float64 metrics:
+        [sum rel2 of committed rounds, committed, processed, reverted]."""
+        e = self.engine
+        self._fx.copy_(e.metrics_fx)
         if self.world > 1:
-            dist.all_reduce(self._global, op=dist.ReduceOp.SUM, group=self.group)
+            dist.all_reduce(self._fx, op=dist.ReduceOp.SUM, group=self.group)
+        self._global.copy_(self._fx)
+        self._global[0] *= (2.0 ** -32) if e.mode == "fast" else 1e-6
         return self._global
 
     def step_metrics(self) -> None:

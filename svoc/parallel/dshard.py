@@ -31,8 +31,7 @@ def run_round_sharded(engine, d_global: int, group=None, world: int = 1) -> None
     if engine.mode != "fast":
         raise NotImplementedError("D-sharding is implemented for the fast (float) engine")
     e = engine
-    full = e.n_active == e.N
-    e._active.copy_(full & e.touched.bool())
+    e._ops.round_prologue(e.n_active, e.touched, e.N, True, e._active)
     mx = float(e.cfg.unconstrained_max_spread)
     args = (e.values, e._active, e.D, e.cfg.n_failing_oracles, e.cfg.constrained, mx, e.c1, e.consensus,
             e.skew, e.kurt, e.rel, e.qr, e.reliable, e.status, e.wave_hint)
@@ -41,7 +40,5 @@ def run_round_sharded(engine, d_global: int, group=None, world: int = 1) -> None
     if world > 1:
         dist.all_reduce(e.qr, op=dist.ReduceOp.SUM, group=group)
     e._ops.fast_round(*args, 2, d_global, lg)      # pass 2 from the global qr
-    ok = (e.status == Status.OK) | (e.status == Status.ZERO_VARIANCE)
-    e.consensus_active |= e._active.bool() & ok
-    e.touched.zero_()
+    e._ops.round_epilogue(e._active, e.status, e.rel, e.consensus_active, e.touched, e.metrics_fx)
     e.rounds += 1

@@ -53,6 +53,9 @@ def test_data_parallel_gloo():
         r = [torch.load(os.path.join(d, f"dp{i}.pt"), weights_only=True) for i in range(world)]
     assert torch.equal(r[0]["g"], r[1]["g"])
     assert r[0]["g"][2].item() == 6            # 2 ranks x 3 instances processed
+    # rel2 sum over committed rounds (fixed-point 2^-32 counters, all-reduced as integers)
+    rel2 = torch.cat([r[0]["rel"][:, 1], r[1]["rel"][:, 1]]).double().sum().item()
+    assert abs(r[0]["g"][0].item() - rel2) < 1e-6 and r[0]["g"][1].item() == 6
     full = r[0]["summ"]["consensus"]
     assert torch.allclose(full[:3].float(), r[0]["local"].float())
     assert torch.allclose(full[3:].float(), r[1]["local"].float())
