@@ -1,0 +1,119 @@
+// torch.ops.svoc.add_layernorm: fused residual add + LayerNorm for the sentiment encoder.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <cmath>
+#include <limits>
+
+#include "svoc/ops.hpp"
+
+extern "C" int svoc_add_layernorm_bf16(const void* x, const void* y, const void* w, const void* b, void* out,
+                                       int64_t rows, int H, float eps, hipStream_t stream);
+
+namespace svoc {
+namespace {
+
+at::Tensor add_layernorm_ref(const at::Tensor& x, const at::Tensor& y, const at::Tensor& w, const at::Tensor& b,
+                             double eps) {
+  const int64_t H = x.size(-1);
+  return at::layer_norm(x + y, {H}, w, b, eps);
+}
+
+at::Tensor add_layernorm_cpu(const at::Tensor& x, const at::Tensor& y, const at::Tensor& w, const at::Tensor& b,
+                             double eps) {
+  return add_layernorm_ref(x, y, w, b, eps);
+}
+
+bool hip_supported(int64_t H) { return H == 256 || H == 512 || H == 768 || H == 1024; }
+
+at::Tensor add_layernorm_hip(const at::Tensor& x, const at::Tensor& y, const at::Tensor& w, const at::Tensor& b,
+                             double eps) {
+  TORCH_CHECK(x.sizes() == y.sizes(), "add_layernorm: x and y shapes differ");
+  const int64_t H = x.size(-1);
+  TORCH_CHECK(w.numel() == H && b.numel() == H, "add_layernorm: weight/bias must have H elements");
+  const bool fast = x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 &&
+                    w.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && hip_supported(H);
+  if (!fast) return add_layernorm_ref(x, y, w, b, eps);  // other dtypes / widths: ATen (documented)
+  auto xc = x.contiguous(), yc = y.contiguous(), wc = w.contiguous(), bc = b.contiguous();
+  auto out = at::empty_like(xc);
+  const int rc = svoc_add_layernorm_bf16(xc.data_ptr(), yc.data_ptr(), wc.data_ptr(), bc.data_ptr(), out.data_ptr(),
+                                         xc.numel() / H, (int)H, (float)eps,
+                                         c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  TORCH_CHECK(rc == 0, "svoc_add_layernorm_bf16 failed: ", rc);
+  return out;
+}
+
+}  // namespace
+
+void register_attention_defs(torch::Library& m);
+void register_attention_cpu(torch::Library& m);
+void register_attention_hip(torch::Library& m);
+
+void register_encoder_defs(torch::Library& m) {
+  m.def("add_layernorm(Tensor x, Tensor y, Tensor weight, Tensor bias, float eps) -> Tensor");
+  register_attention_defs(m);
+}
+void register_encoder_cpu(torch::Library& m) {
+  m.impl("add_layernorm", &add_layernorm_cpu);
+  register_attention_cpu(m);
+}
+void register_encoder_hip(torch::Library& m) {
+  m.impl("add_layernorm", &add_layernorm_hip);
+  register_attention_hip(m);
+}
+
+}  // namespace svoc
+
+extern "C" int svoc_attention_short_bf16(const void* qkv, const void* kmask, void* out, int64_t B, int S, int H,
+                                         int DH, hipStream_t stream);
+
+namespace svoc {
+namespace {
+
+// qkv [B, S, 3*H*DH] -> [B, S, H*DH]; key_mask [B, S] (nonzero = attend)
+at::Tensor attention_ref(const at::Tensor& qkv, const c10::optional<at::Tensor>& key_mask, int64_t heads) {
+  const int64_t B = qkv.size(0), S = qkv.size(1), HD = qkv.size(2) / 3, DH = HD / heads;
+  auto t = qkv.view({B, S, 3, heads, DH}).permute({2, 0, 3, 1, 4});
+  auto q = t[0].to(at::kFloat), k = t[1].to(at::kFloat), v = t[2].to(at::kFloat);
+  auto s = at::matmul(q, k.transpose(-1, -2)) / std::sqrt((double)DH);
+  if (key_mask.has_value()) {
+    auto m = key_mask->to(at::kBool).view({B, 1, 1, S});
+    s = s.masked_fill(m.logical_not(), -std::numeric_limits<float>::infinity());
+  }
+  auto o = at::matmul(at::softmax(s, -1), v);  // [B, H, S, DH]
+  return o.transpose(1, 2).reshape({B, S, HD}).to(qkv.scalar_type());
+}
+
+at::Tensor attention_cpu(const at::Tensor& qkv, const c10::optional<at::Tensor>& key_mask, int64_t heads) {
+  return attention_ref(qkv, key_mask, heads);
+}
+
+at::Tensor attention_hip(const at::Tensor& qkv, const c10::optional<at::Tensor>& key_mask, int64_t heads) {
+  TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) % (3 * heads) == 0, "qkv: [B, S, 3*H*DH]");
+  const int64_t B = qkv.size(0), S = qkv.size(1), HD = qkv.size(2) / 3, DH = HD / heads;
+  const bool ok = qkv.scalar_type() == at::kBFloat16 && DH == 64 && S % 32 == 0 && S >= 32 && S <= 128;
+  if (!ok) return attention_ref(qkv, key_mask, heads);  // other shapes: ATen (documented)
+  auto x = qkv.contiguous();
+  at::Tensor m;
+  if (key_mask.has_value()) {
+    TORCH_CHECK(key_mask->numel() == B * S, "key_mask: [B, S]");
+    m = key_mask->to(at::kByte).contiguous();
+  }
+  auto out = at::empty({B, S, HD}, x.options());
+  const int rc = svoc_attention_short_bf16(x.data_ptr(), key_mask.has_value() ? m.data_ptr() : nullptr,
+                                           out.data_ptr(), B, (int)S, (int)heads, (int)DH,
+                                           c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  TORCH_CHECK(rc == 0, "svoc_attention_short_bf16 failed: ", rc);
+  return out;
+}
+
+}  // namespace
+
+void register_attention_defs(torch::Library& m) {
+  m.def("attention_qkv(Tensor qkv, Tensor? key_mask, int heads) -> Tensor");
+}
+void register_attention_cpu(torch::Library& m) { m.impl("attention_qkv", &attention_cpu); }
+void register_attention_hip(torch::Library& m) { m.impl("attention_qkv", &attention_hip); }
+
+}  // namespace svoc

@@ -117,6 +117,7 @@ void register_extra_defs(torch::Library& m) {
   register_generator_defs(m);
   register_io_defs(m);
   register_bookkeeping_defs(m);
+  register_encoder_defs(m);
 }
 
 void register_extra_cpu(torch::Library& m) {
@@ -124,6 +125,7 @@ void register_extra_cpu(torch::Library& m) {
   register_governance_cpu(m);
   register_generator_cpu(m);
   register_bookkeeping_cpu(m);
+  register_encoder_cpu(m);
 }
 
 void register_extra_hip(torch::Library& m) {
@@ -131,6 +133,7 @@ void register_extra_hip(torch::Library& m) {
   register_governance_hip(m);
   register_generator_hip(m);
   register_bookkeeping_hip(m);
+  register_encoder_hip(m);
 }
 
 }  // namespace svoc

@@ -21,4 +21,7 @@ void register_io_cpu(torch::Library& m);
 void register_bookkeeping_defs(torch::Library& m);
 void register_bookkeeping_cpu(torch::Library& m);
 void register_bookkeeping_hip(torch::Library& m);
+void register_encoder_defs(torch::Library& m);
+void register_encoder_cpu(torch::Library& m);
+void register_encoder_hip(torch::Library& m);
 }  // namespace svoc

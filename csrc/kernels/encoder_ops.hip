@@ -1,0 +1,253 @@
+// Fused encoder epilogues for the sentiment path (svoc/models/encoder.py, post-LN BERT/RoBERTa).
+//
+// add_layernorm: out = LayerNorm(x + y) * w + b over the hidden dim, bf16 in/out, fp32 math.
+// One wave per row; each lane holds H/64 elements (H = 768: 12 per lane, three 8-byte loads per
+// operand) so the row never leaves registers: mean and variance (two-pass, on registers) by wave
+// butterflies.  Replaces an elementwise add + a separate LayerNorm (two extra HBM round trips of the
+// [tokens, H] activation) -- the post-LN residual is consumed only through the LayerNorm output.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace svoc {
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __builtin_bit_cast(float, (uint32_t)h << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even (finite inputs)
+  const uint32_t u = __builtin_bit_cast(uint32_t, f);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// EPL elements per lane (multiple of 4), H = 64 * EPL
+template <int EPL>
+__global__ __launch_bounds__(256) void add_layernorm_kernel(const uint16_t* __restrict__ x,
+                                                            const uint16_t* __restrict__ y,
+                                                            const uint16_t* __restrict__ w,
+                                                            const uint16_t* __restrict__ bias,
+                                                            uint16_t* __restrict__ out, int64_t rows, float eps) {
+  constexpr int H = 64 * EPL;
+  constexpr int V = EPL / 4;  // 8-byte vectors per lane
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const uint2* xr = (const uint2*)(x + row * H);
+  const uint2* yr = (const uint2*)(y + row * H);
+  float v[EPL];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int c = k * 64 + lane;  // coalesced: consecutive lanes read consecutive 8-byte pieces
+    const uint2 a = xr[c], b = yr[c];
+    const uint32_t aw[2] = {a.x, a.y}, bw[2] = {b.x, b.y};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float lo = bf2f(aw[j] & 0xffffu) + bf2f(bw[j] & 0xffffu);
+      const float hi = bf2f(aw[j] >> 16) + bf2f(bw[j] >> 16);
+      v[4 * k + 2 * j] = lo;
+      v[4 * k + 2 * j + 1] = hi;
+      s += lo + hi;
+    }
+  }
+  const float mean = wave_sum(s) * (1.f / H);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const float d = v[i] - mean;
+    q += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(q) * (1.f / H) + eps);
+  uint2* orow = (uint2*)(out + row * H);
+  const uint2* wr = (const uint2*)w;
+  const uint2* br = (const uint2*)bias;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int c = k * 64 + lane;
+    const uint2 gw = wr[c], gb = br[c];
+    const uint32_t ww[2] = {gw.x, gw.y}, bb[2] = {gb.x, gb.y};
+    uint32_t o[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float lo = (v[4 * k + 2 * j] - mean) * rstd * bf2f(ww[j] & 0xffffu) + bf2f(bb[j] & 0xffffu);
+      const float hi = (v[4 * k + 2 * j + 1] - mean) * rstd * bf2f(ww[j] >> 16) + bf2f(bb[j] >> 16);
+      o[j] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    }
+    orow[c] = make_uint2(o[0], o[1]);
+  }
+}
+
+}  // namespace svoc
+
+using namespace svoc;
+
+// Returns 0 on success, -1 if the hidden size is not supported (caller falls back to ATen).
+extern "C" int svoc_add_layernorm_bf16(const void* x, const void* y, const void* w, const void* b, void* out,
+                                       int64_t rows, int H, float eps, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  const auto* X = (const uint16_t*)x;
+  const auto* Y = (const uint16_t*)y;
+  const auto* W = (const uint16_t*)w;
+  const auto* B = (const uint16_t*)b;
+  auto* O = (uint16_t*)out;
+  switch (H) {
+    case 256: hipLaunchKernelGGL(add_layernorm_kernel<4>, grid, block, 0, stream, X, Y, W, B, O, rows, eps); break;
+    case 512: hipLaunchKernelGGL(add_layernorm_kernel<8>, grid, block, 0, stream, X, Y, W, B, O, rows, eps); break;
+    case 768: hipLaunchKernelGGL(add_layernorm_kernel<12>, grid, block, 0, stream, X, Y, W, B, O, rows, eps); break;
+    case 1024: hipLaunchKernelGGL(add_layernorm_kernel<16>, grid, block, 0, stream, X, Y, W, B, O, rows, eps); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// attention_qkv: softmax(Q Kᵀ / sqrt(64) + key-padding mask) V for short sequences (S <= 128,
+// S % 32 == 0, head dim 64), reading the fused QKV projection [B, S, 3, H, 64] directly and
+// writing [B, S, H, 64] (the out-projection's input layout: no transpose copies).
+//
+// One workgroup per (sequence, head), one wave per 32 queries.  MFMA orientation "key on the
+// register, query on the lane": X = K·Qᵀ (mfma_f32_32x32x16_bf16, A = K rows, B = Q rows, both 16-B
+// contiguous global loads) leaves each lane with one query's scores for 64 keys (its partner
+// lane ^ 32 holds the other 64), so the softmax is lane-local plus one xor-32 exchange, and the
+// accumulator registers ARE the A operand of Z = P·V (pairs of registers -> bf16, k order
+// 16s + 8(j>>2) + 4h + (j&3)).  V is staged transposed in LDS (row pitch S/2+2 dwords: conflict-free
+// 8-byte reads by 32 lanes) so each B fragment is two ds_read_b64.  P is normalised before the PV
+// product (bf16 P, as flash attention).  At S = 128 the whole problem is 32 MFMAs per wave.
+// ---------------------------------------------------------------------------------------------
+namespace svoc {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int NQB>  // S / 32: query blocks = waves = key blocks
+__global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __restrict__ qkv,
+                                                             const uint8_t* __restrict__ kmask,
+                                                             uint16_t* __restrict__ out, int H,
+                                                             float scale_log2) {
+  constexpr int S = 32 * NQB, DH = 64, PITCH = S + 4;  // bf16 elements per Vt row
+  __shared__ uint16_t Vt[DH * PITCH];
+  __shared__ uint8_t km[S];
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int64_t ts = (int64_t)3 * H * DH;  // token stride in qkv (elements)
+  const uint16_t* Qb = qkv + (int64_t)b * S * ts + h * DH;
+  const uint16_t* Kb = Qb + H * DH;
+  const uint16_t* Vb = Qb + 2 * H * DH;
+
+  // stage Vᵀ and the key mask
+  for (int c = tid; c < S * (DH / 8); c += 64 * NQB) {
+    const int key = c >> 3, e0 = (c & 7) * 8;
+    const uint4 v = *(const uint4*)(Vb + key * ts + e0);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      Vt[(e0 + 2 * i) * PITCH + key] = (uint16_t)(w[i] & 0xffffu);
+      Vt[(e0 + 2 * i + 1) * PITCH + key] = (uint16_t)(w[i] >> 16);
+    }
+  }
+  for (int k = tid; k < S; k += 64 * NQB) km[k] = kmask ? kmask[(int64_t)b * S + k] : (uint8_t)1;
+
+  // X = K·Qᵀ for this wave's 32 queries: rows = keys (registers), column = query (lane)
+  const int q0 = wave * 32;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(Qb + (q0 + r) * ts + ds * 16 + 8 * hh);
+  f32x16 x[NQB];
+#pragma unroll
+  for (int kb = 0; kb < NQB; ++kb) {
+    x[kb] = f32x16{};
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) {
+      const bf16x8 kf = *(const bf16x8*)(Kb + (kb * 32 + r) * ts + ds * 16 + 8 * hh);
+      x[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], x[kb], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // Vt and km staged
+
+  // softmax over the keys of query q0 + r (this lane: key rows (i&3) + 8(i>>2) + 4hh of each block)
+  float m = -__builtin_inff();
+#pragma unroll
+  for (int kb = 0; kb < NQB; ++kb)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const uint32_t mk4 = *(const uint32_t*)(km + kb * 32 + 8 * g + 4 * hh);  // 4 consecutive keys
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int i = 4 * g + t;
+        const bool on = (mk4 >> (8 * t)) & 0xffu;
+        const float v = on ? x[kb][i] * scale_log2 : -__builtin_inff();
+        x[kb][i] = v;
+        m = fmaxf(m, v);
+      }
+    }
+  m = fmaxf(m, __shfl_xor(m, 32));
+  float sum = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < NQB; ++kb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = exp2f(x[kb][i] - m);
+      x[kb][i] = p;
+      sum += p;
+    }
+  sum += __shfl_xor(sum, 32);
+  const float inv = 1.f / sum;
+
+  // Z = P·V: A = P (accumulator registers, rows = keys), B = V from Vᵀ in LDS
+  f32x16 z[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+  for (int kb = 0; kb < NQB; ++kb)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 pa;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pa[j] = (__bf16)(x[kb][8 * s + j] * inv);
+      const int key0 = kb * 32 + 16 * s + 4 * hh;
+#pragma unroll
+      for (int eb = 0; eb < 2; ++eb) {
+        const uint16_t* vr = Vt + (eb * 32 + r) * PITCH + key0;
+        const uint2 lo = *(const uint2*)vr, hi = *(const uint2*)(vr + 8);
+        bf16x8 vf;
+        const uint32_t w[4] = {lo.x, lo.y, hi.x, hi.y};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          vf[2 * j] = __builtin_bit_cast(__bf16, (uint16_t)(w[j] & 0xffffu));
+          vf[2 * j + 1] = __builtin_bit_cast(__bf16, (uint16_t)(w[j] >> 16));
+        }
+        z[eb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, vf, z[eb], 0, 0, 0);
+      }
+    }
+  // store: z[eb][i] = Z[query (i&3)+8(i>>2)+4hh][e = eb*32 + r]
+  uint16_t* Ob = out + ((int64_t)b * S + q0) * H * DH + h * DH;
+#pragma unroll
+  for (int eb = 0; eb < 2; ++eb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int q = (i & 3) + 8 * (i >> 2) + 4 * hh;
+      Ob[(int64_t)q * H * DH + eb * 32 + r] = f2bf(z[eb][i]);
+    }
+}
+
+}  // namespace svoc
+
+// qkv: [B, S, 3, H, 64] bf16 contiguous; kmask: [B, S] uint8 (1 = attend) or null; out: [B, S, H, 64].
+extern "C" int svoc_attention_short_bf16(const void* qkv, const void* kmask, void* out, int64_t B, int S, int H,
+                                         int DH, hipStream_t stream) {
+  if (DH != 64 || S % 32 != 0 || S < 32 || S > 128 || B * H > 0x7fffffffll) return -1;
+  if (B == 0) return 0;
+  const float scale_log2 = 1.4426950408889634f / 8.f;  // log2(e) / sqrt(64)
+  const auto* Q = (const uint16_t*)qkv;
+  const auto* M = (const uint8_t*)kmask;
+  auto* O = (uint16_t*)out;
+  const dim3 grid((unsigned)(B * H));
+  switch (S / 32) {
+    case 1: hipLaunchKernelGGL(attn_short_kernel<1>, grid, dim3(64), 0, stream, Q, M, O, H, scale_log2); break;
+    case 2: hipLaunchKernelGGL(attn_short_kernel<2>, grid, dim3(128), 0, stream, Q, M, O, H, scale_log2); break;
+    case 3: hipLaunchKernelGGL(attn_short_kernel<3>, grid, dim3(192), 0, stream, Q, M, O, H, scale_log2); break;
+    default: hipLaunchKernelGGL(attn_short_kernel<4>, grid, dim3(256), 0, stream, Q, M, O, H, scale_log2); break;
+  }
+  return (int)hipGetLastError();
+}

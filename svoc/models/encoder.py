@@ -8,8 +8,9 @@ head, sigmoid scores for all 28 go_emotions labels; the client keeps 6 labels
 There is no network on the GPU boxes, so the weights are random-initialised with a fixed seed and
 the architecture is BERT-base sized (12 layers, hidden 768, 12 heads, FFN 3072, vocab 50265,
 512 positions).  The implementation is plain PyTorch-ROCm: bf16 weights, fused QKV projection
-(one hipBLASLt GEMM), ``scaled_dot_product_attention`` (flash attention kernels on ROCm), pre-sized
-buffers so the forward can be captured in a HIP graph.
+(one hipBLASLt GEMM), a hand-written MFMA attention kernel for the short windows (S <= 128) that
+reads the QKV projection in place, GELU in the FC1 GEMM epilogue, fused residual-add + LayerNorm;
+pre-sized buffers so the forward can be captured in a HIP graph.
 """
 from __future__ import annotations
 
@@ -64,12 +65,29 @@ class Layer(nn.Module):
         self.fc2 = nn.Linear(c.ffn, c.hidden)
         self.ln2 = nn.LayerNorm(c.hidden, eps=c.layer_norm_eps)
 
-    def forward(self, x: torch.Tensor, mask: Optional[torch.Tensor]) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, key_mask: Optional[torch.Tensor]) -> torch.Tensor:
         B, S, H = x.shape
-        q, k, v = self.qkv(x).view(B, S, 3, self.heads, H // self.heads).permute(2, 0, 3, 1, 4)
-        a = F.scaled_dot_product_attention(q, k, v, attn_mask=mask)
-        x = self.ln1(x + self.out(a.transpose(1, 2).reshape(B, S, H)))   # post-LN (BERT/RoBERTa)
-        return self.ln2(x + self.fc2(F.gelu(self.fc1(x))))
+        from .. import ops as svops
+        # attention straight from the fused QKV projection [B, S, 3, heads, 64] into [B, S, H]
+        # (MFMA kernel for S <= 128 on the GPU, encoder_ops.hip; ATen otherwise)
+        a = svops.ops().attention_qkv(self.qkv(x), key_mask, self.heads)
+        # post-LN (BERT/RoBERTa): residual add + LayerNorm fused in one HIP kernel (encoder_ops.hip)
+        x = _add_ln(x, self.out(a), self.ln1)
+        return _add_ln(x, self.fc2(_linear_gelu(x, self.fc1)), self.ln2)
+
+
+def _linear_gelu(x: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
+    """fc1 + GELU; on the GPU the GELU runs in the hipBLASLt GEMM epilogue (one pass over the
+    [tokens, 3072] activation instead of two)."""
+    if x.is_cuda:
+        y = torch._addmm_activation(fc.bias, x.reshape(-1, x.shape[-1]), fc.weight.t(), use_gelu=True)
+        return y.view(*x.shape[:-1], -1)
+    return F.gelu(fc(x))
+
+
+def _add_ln(x: torch.Tensor, y: torch.Tensor, ln: nn.LayerNorm) -> torch.Tensor:
+    from .. import ops as svops
+    return svops.ops().add_layernorm(x, y, ln.weight, ln.bias, ln.eps)
 
 
 class SentimentEncoder(nn.Module):
@@ -102,12 +120,9 @@ class SentimentEncoder(nn.Module):
         B, S = ids.shape
         pos = torch.arange(2, S + 2, device=ids.device)           # RoBERTa positions start at pad+1
         x = self.ln(self.tok(ids) + self.pos(pos)[None] + self.typ.weight[0])
-        mask = None
-        if attention_mask is not None:
-            mask = torch.zeros(B, 1, 1, S, dtype=x.dtype, device=x.device)
-            mask.masked_fill_(attention_mask[:, None, None, :] == 0, float("-inf"))
+        kmask = attention_mask.to(torch.uint8) if attention_mask is not None else None
         for layer in self.layers:
-            x = layer(x, mask)
+            x = layer(x, kmask)
         if self.cfg.pool == "cls" or attention_mask is None:
             pooled = x[:, 0] if self.cfg.pool == "cls" else x.mean(1)
         else:

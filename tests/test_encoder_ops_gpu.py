@@ -1,0 +1,73 @@
+"""Fused encoder kernels (csrc/kernels/encoder_ops.hip) vs plain PyTorch fp32."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from svoc import ops as svops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("rows,H", [(1, 768), (1023, 768), (257, 256), (64, 1024), (5, 512)])
+def test_add_layernorm_bf16(rows, H):
+    g = torch.Generator(device="cuda").manual_seed(rows + H)
+    x = torch.randn(rows, H, device="cuda", generator=g).to(torch.bfloat16)
+    y = (0.5 * torch.randn(rows, H, device="cuda", generator=g) + 0.1).to(torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, device="cuda", generator=g)).to(torch.bfloat16)
+    b = (0.1 * torch.randn(H, device="cuda", generator=g)).to(torch.bfloat16)
+    out = svops.ops().add_layernorm(x, y, w, b, 1e-5)
+    ref = F.layer_norm(x.float() + y.float(), (H,), w.float(), b.float(), 1e-5)
+    assert out.dtype == torch.bfloat16 and out.shape == x.shape
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=2e-2)
+    # bf16 rounding of the output is the only error source: compare against the rounded reference
+    assert (out.float() - ref.to(torch.bfloat16).float()).abs().max().item() <= 0.0625
+
+
+def test_add_layernorm_3d_and_fallback_width():
+    x = torch.randn(2, 7, 64, device="cuda", dtype=torch.bfloat16)
+    y = torch.randn(2, 7, 64, device="cuda", dtype=torch.bfloat16)
+    w = torch.ones(64, device="cuda", dtype=torch.bfloat16)
+    b = torch.zeros(64, device="cuda", dtype=torch.bfloat16)
+    out = svops.ops().add_layernorm(x, y, w, b, 1e-5)   # H = 64: ATen path
+    torch.testing.assert_close(out.float(), F.layer_norm((x + y).float(), (64,), w.float(), b.float(), 1e-5),
+                               rtol=2e-2, atol=3e-2)
+
+
+def _attn_ref(qkv, mask, heads):
+    B, S, H3 = qkv.shape
+    HD = H3 // 3
+    DH = HD // heads
+    t = qkv.float().view(B, S, 3, heads, DH).permute(2, 0, 3, 1, 4)
+    s = t[0] @ t[1].transpose(-1, -2) / DH ** 0.5
+    if mask is not None:
+        s = s.masked_fill(~mask.bool()[:, None, None, :], float("-inf"))
+    return (torch.softmax(s, -1) @ t[2]).transpose(1, 2).reshape(B, S, HD)
+
+
+@pytest.mark.parametrize("S", [32, 64, 96, 128])
+def test_attention_qkv_mfma(S):
+    B, heads = 5, 12
+    g = torch.Generator(device="cuda").manual_seed(S)
+    qkv = torch.randn(B, S, 3 * heads * 64, device="cuda", generator=g).to(torch.bfloat16)
+    lens = torch.randint(1, S + 1, (B,), device="cuda", generator=g)
+    mask = (torch.arange(S, device="cuda")[None] < lens[:, None]).to(torch.uint8)
+    out = svops.ops().attention_qkv(qkv, mask, heads)
+    ref = _attn_ref(qkv, mask, heads)
+    assert out.shape == (B, S, heads * 64) and out.dtype == torch.bfloat16
+    torch.testing.assert_close(out.float(), ref, rtol=3e-2, atol=3e-2)
+    out2 = svops.ops().attention_qkv(qkv, None, heads)
+    torch.testing.assert_close(out2.float(), _attn_ref(qkv, None, heads), rtol=3e-2, atol=3e-2)
+
+
+def test_encoder_fused_matches_cpu_fp32():
+    from svoc.models.encoder import EncoderConfig, build
+    cfg = EncoderConfig(vocab_size=500, hidden=768, layers=2, heads=12, ffn=3072, max_positions=130)
+    enc_g = build("cuda", torch.bfloat16, seed=3, cfg=cfg)
+    enc_c = build("cpu", torch.float32, seed=3, cfg=cfg)
+    g = torch.Generator().manual_seed(0)
+    ids = torch.randint(3, 500, (6, 128), generator=g)
+    mask = (torch.arange(128)[None] < torch.tensor([128, 40, 77, 128, 9, 100])[:, None]).to(torch.int64)
+    with torch.no_grad():
+        sg = enc_g(ids.cuda(), mask.cuda()).float().cpu()
+        sc = enc_c(ids, mask)
+    torch.testing.assert_close(sg, sc, rtol=0, atol=0.05)
