@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="instances per GPU (default per config)")
     ap.add_argument("--wave-hint", type=int, default=0)
     ap.add_argument("--graph", type=int, default=1, help="capture the step in a HIP graph")
+    ap.add_argument("--mode", default=None, choices=["fast", "exact"],
+                    help="override the config's engine mode (exact = bit-exact wsad int64 path)")
     ap.add_argument("--log", default=None, help="append the result record to this JSON-lines file")
     ap.add_argument("--kernel-table", type=int, default=0, help="profile N extra steps (torch.profiler) "
                     "after the timed region and add the per-kernel table to the log record")
@@ -77,7 +79,8 @@ def main():
 
     B = args.batch or c["batch"]
     cfg = ConsensusConfig(n_oracles=c["N"], dimension=c["D"], n_failing_oracles=c["f"], constrained=True)
-    eng = ConsensusEngine(cfg, batch=B, device=dev, mode=c.get("mode", "fast"))
+    mode = args.mode or c.get("mode", "fast")
+    eng = ConsensusEngine(cfg, batch=B, device=dev, mode=mode)
     eng.wave_hint = args.wave_hint
     dp = DataParallelConsensus(eng, rank=rank, world=world)
     eng.randomize(seed=1000 + rank)
@@ -97,7 +100,8 @@ def main():
         extra["encoder_gflop_per_step"] = B * 30 * flops_per_sequence(pipe.encoder.cfg, c["seq_len"]) / 1e9
     elif U_per_inst:
         from svoc.stream import SyntheticUpdateStream
-        stream = SyntheticUpdateStream(B, c["N"], c["D"], U_per_inst, c["f"], pool=2, device=dev, seed=rank)
+        stream = SyntheticUpdateStream(B, c["N"], c["D"], U_per_inst, c["f"], pool=2, device=dev, seed=rank,
+                                       dtype=torch.int64 if mode == "exact" else torch.bfloat16)
     if args.config == "c5":
         from svoc.codec import address_to_limbs
         from svoc.governance import Governance
@@ -195,9 +199,10 @@ def main():
         out = {
             "metric": METRIC, "value": value, "unit": "consensus rounds/s", "n_gpus": world,
             "steps": steps_done, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": c.get("dtype", "bf16"), "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "int64-wsad" if mode == "exact" else c.get("dtype", "bf16"), "data": "synthetic",
             "config": {"model": c["model"], "global_batch": B * world, "seq_len": c["D"],
-                       "parallelism": f"dp{world}", "n_oracles": c["N"], "dimension": c["D"],
+                       "parallelism": f"dp{world}", "engine_mode": mode, "n_oracles": c["N"], "dimension": c["D"],
                        "n_failing": c["f"], "updates_per_instance_per_step": U_per_inst,
                        "oracle_updates_per_s": (U_per_inst * rounds / el) if U_per_inst else 0.0,
                        "hip_graph": graph is not None, "ok_fraction": ok, **extra},

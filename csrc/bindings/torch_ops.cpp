@@ -204,6 +204,11 @@ void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& 
   p.qr = qr.data_ptr<int64_t>();
   p.reliable = reliable.data_ptr<uint8_t>();
   p.status = status.data_ptr<int32_t>();
+  at::Tensor work;
+  if ((int64_t)p.D * 6 * 8 > 64 * 1024) {  // wide instances: per-column intermediates in HBM
+    work = at::empty({(int64_t)p.B, 6, (int64_t)p.D}, values.options());
+    p.work = work.data_ptr<int64_t>();
+  }
   auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
   const int rc = svoc_exact_round(&p, stream);
   TORCH_CHECK(rc == 0, "svoc_exact_round launch failed: ", rc);

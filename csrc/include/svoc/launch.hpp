@@ -44,6 +44,7 @@ struct ExactParams {
   uint8_t* reliable;        // [B, N]
   int32_t* status;          // [B]
   int legacy;               // obsolete-contract variant (see FastParams)
+  int64_t* work;            // [B, 6, D] workspace for wide instances (null: per-column data in LDS)
 };
 
 }  // namespace svoc

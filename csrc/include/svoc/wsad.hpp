@@ -54,7 +54,9 @@ SVOC_HD i128 idiv(i128 a, i128 b, int& st) {
   if (a == i128_min() || b == i128_min()) { fail(st, ST_OVERFLOW); return 0; }
   u128 ua = a < 0 ? (u128)(-a) : (u128)a;
   u128 ub = b < 0 ? (u128)(-b) : (u128)b;
-  i128 q = (i128)(ua / ub);
+  // 64-bit operands (the common case: wsad values and their products below 2^64) take the much
+  // cheaper 64-bit division; same truncated quotient
+  const i128 q = ((ua | ub) >> 64) == 0 ? (i128)((uint64_t)ua / (uint64_t)ub) : (i128)(ua / ub);
   return ((a >= 0) == (b >= 0)) ? q : -q;
 }
 

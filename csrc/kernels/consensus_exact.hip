@@ -26,8 +26,17 @@ __device__ __forceinline__ i128 shfl128(i128 v, int src) {
   return (i128)(((u128)hi << 64) | lo);
 }
 
-// wave-wide checked i128 sum in a fixed lane order (0..63) so overflow detection is deterministic.
+// wave-wide checked i128 sum.  The contract adds in row order and reverts on any i128 overflow of
+// a partial sum; when every term is below 2^118 in magnitude no partial sum of <= 256 terms can
+// overflow in ANY order, so a butterfly (6 exchanges) gives the identical integer.  Otherwise the
+// sum runs sequentially in lane order (0..63), as the CPU engine, for exact overflow detection.
 __device__ __forceinline__ i128 wave_sum(i128 v, int& st) {
+  const i128 lim = (i128)1 << 118;
+  if (__all(v < lim && v > -lim)) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += shfl128(v, threadIdx.x ^ o);
+    return v;
+  }
   i128 acc = 0;
   for (int l = 0; l < 64; ++l) acc = add(acc, shfl128(v, l), st);
   return acc;
@@ -44,58 +53,73 @@ struct Rows {
   bool on[RPL];  // row exists and takes part
 };
 
-// value of the element of stable rank `k` among the rows with on[] set (k is wave-uniform)
+// Column scratch in LDS: the wave's rows are published once, then every lane ranks its own rows
+// against them with broadcast LDS reads (one ds_read_b64 per row instead of three cross-lane
+// shuffles), both middle ranks in the same pass.
+struct ColScratch {
+  int64_t x[256];
+  uint8_t on[256];
+  int64_t pick[2];
+};
+
+// stable ranks mid-1 and mid among the rows with on[] set (math.cairo:113-126 via MergeSort)
 template <int RPL>
-__device__ i128 rank_value(const Rows<RPL>& r, int lane, int k) {
-  i128 found = 0;
-  int hit = 0;
+__device__ void middle_values(const Rows<RPL>& r, int lane, int n_rows, int mid, ColScratch& cs, i128& a,
+                              i128& b) {
 #pragma unroll
   for (int j = 0; j < RPL; ++j) {
-    int rank = 0;
-#pragma unroll
-    for (int jj = 0; jj < RPL; ++jj) {
-      for (int l = 0; l < 64; ++l) {
-        const int64_t xk = shfl64(r.x[jj], l);
-        const int onk = __shfl((int)r.on[jj], l);
-        const int idx_k = jj * 64 + l, idx_m = j * 64 + lane;
-        rank += (onk && (xk < r.x[j] || (xk == r.x[j] && idx_k < idx_m))) ? 1 : 0;
-      }
+    const int row = j * 64 + lane;
+    if (row < n_rows) {
+      cs.x[row] = r.x[j];
+      cs.on[row] = r.on[j] ? 1 : 0;
     }
-    if (r.on[j] && rank == k) { found = r.x[j]; hit = 1; }
   }
-  int dummy = ST_OK;
-  // exactly one lane holds it
-  i128 v = hit ? found : 0;
-  for (int l = 0; l < 64; ++l) {
-    const int h = __shfl(hit, l);
-    if (h) return shfl128(v, l);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < RPL; ++j) {
+    const int me = j * 64 + lane;
+    if (me < n_rows && r.on[j]) {
+      const int64_t xm = r.x[j];
+      int rank = 0;
+      for (int k = 0; k < n_rows; ++k) {
+        const int64_t xk = cs.x[k];
+        rank += (cs.on[k] && (xk < xm || (xk == xm && k < me))) ? 1 : 0;
+      }
+      if (rank == mid - 1) cs.pick[0] = xm;
+      if (rank == mid) cs.pick[1] = xm;
+    }
   }
-  (void)dummy;
-  return 0;
+  __syncthreads();
+  a = cs.pick[0];
+  b = cs.pick[1];
+  __syncthreads();  // the scratch is reused by the next column
 }
 
 template <int RPL>
-__device__ i128 smooth_median_w(const Rows<RPL>& r, int lane, int count, int& st) {
+__device__ i128 smooth_median_w(const Rows<RPL>& r, int lane, int n_rows, int count, ColScratch& cs, int& st) {
   if (count == 0) { fail(st, ST_USIZE_UNDERFLOW); return 0; }
   if (count == 1) { fail(st, ST_INDEX_OOB); return 0; }
-  const int mid = count / 2;
-  const i128 a = rank_value<RPL>(r, lane, mid - 1), b = rank_value<RPL>(r, lane, mid);
+  i128 a, b;
+  middle_values<RPL>(r, lane, n_rows, count / 2, cs, a, b);
   return idiv_pos64(add(a, b, st), 2, st);
 }
 
 template <int RPL>
 __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
   extern __shared__ __attribute__((aligned(16))) int64_t lds[];
+  __shared__ ColScratch cs;
   const int b = blockIdx.x;
   if (p.active && !p.active[b]) return;
   const int lane = threadIdx.x;
   const int N = p.N, D = p.D;
-  int64_t* c1 = lds;
-  int64_t* cons = lds + D;
-  int64_t* means = lds + 2 * D;
-  int64_t* vars = lds + 3 * D;
-  int64_t* sk = lds + 4 * D;
-  int64_t* ku = lds + 5 * D;
+  // per-column intermediates: LDS, or a [B, 6, D] global workspace when 6*D int64 exceed the LDS
+  int64_t* const ws = p.work ? p.work + (int64_t)b * 6 * D : lds;
+  int64_t* c1 = ws;
+  int64_t* cons = ws + D;
+  int64_t* means = ws + 2 * D;
+  int64_t* vars = ws + 3 * D;
+  int64_t* sk = ws + 4 * D;
+  int64_t* ku = ws + 5 * D;
   const int64_t* X = p.values + (int64_t)b * N * D;
   int st = ST_OK;  // wave-uniform by construction (every lane runs the same checked reductions)
 
@@ -108,7 +132,7 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
       rows.on[j] = row < N;
       rows.x[j] = row < N ? X[(int64_t)row * D + d] : 0;
     }
-    const i128 c = smooth_median_w<RPL>(rows, lane, N, st);
+    const i128 c = smooth_median_w<RPL>(rows, lane, N, N, cs, st);
     if (lane == 0) c1[d] = (int64_t)c;
   }
   __syncthreads();
@@ -166,7 +190,7 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
     }
     i128 c;
     if (p.constrained) {
-      c = smooth_median_w<RPL>(rows, lane, R, st);
+      c = smooth_median_w<RPL>(rows, lane, N, R, cs, st);
     } else {
       i128 s = 0;
 #pragma unroll
@@ -269,8 +293,8 @@ using namespace svoc;
 extern "C" int svoc_exact_round(const ExactParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
   if (p->N < 1 || p->N > 256 || p->D < 1) return -1;
-  const size_t lds = (size_t)p->D * 6 * sizeof(int64_t);
-  if (lds > 150 * 1024) return -2;
+  const size_t lds = p->work ? 0 : (size_t)p->D * 6 * sizeof(int64_t);
+  if (lds > 64 * 1024) return -2;  // the binding passes a global workspace for wide instances
   auto k = p->N <= 64 ? consensus_exact_kernel<1> : consensus_exact_kernel<4>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;

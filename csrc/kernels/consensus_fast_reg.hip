@@ -45,7 +45,7 @@ SVOC_DEV uint32_t from_key(u16x2 k) {
   else return key_to_bf16x2(k);
 }
 
-template <int NSEG, int WAVES, bool CONS, int MODE>
+template <int NSEG, int WAVES, bool CONS, int MODE, bool RAW = false>
 __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // column pairs per wave
   constexpr int NPAD = 64 * NSEG;       // padded oracle rows
@@ -96,9 +96,19 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
     int nvl = nv, nll = nl;
     asm volatile("" : "+v"(nvl), "+v"(nll));
     float cA, cB;
+    // columns past D contribute 0 to qr: their bf16 halves are masked to +0 and their centre is +0
+    const uint32_t mW = vA ? (vB ? 0xffffffffu : 0x0000ffffu) : 0u;
+    uint32_t wraw[RAW ? 64 : 1];  // RAW: keep the raw words for the qr pass (no re-read)
     {
       u16x2 r[64];
-      if (N == NPAD) {  // uniform: no padding rows
+      if (RAW) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          wraw[i] = bload(rs, vo, i * rowb) & mW;
+          const uint32_t hi_m = ~lt_mask(i, nll);
+          r[i] = as_k((as_u32(to_key<CONS>(wraw[i])) & (lt_mask(i, nvl) | hi_m)) | hi_m);
+        }
+      } else if (N == NPAD) {  // uniform: no padding rows
 #pragma unroll
         for (int i = 0; i < 64; ++i) r[i] = to_key<CONS>(bload(rs, vo, i * rowb));
       } else {
@@ -122,12 +132,10 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
     }
     __builtin_amdgcn_sched_barrier(0);
     float part[64];
-    // columns past D contribute 0: their bf16 halves are masked to +0 and their centre is +0
-    const uint32_t mW = vA ? (vB ? 0xffffffffu : 0x0000ffffu) : 0u;
     const f32x2 c2 = {vA ? cA : 0.f, vB ? cB : 0.f};
 #pragma unroll
     for (int i = 0; i < 64; ++i) {
-      const uint32_t w = bload(rs, vo, i * rowb) & mW;  // L2/MALL-hot re-read
+      const uint32_t w = RAW ? wraw[i] : bload(rs, vo, i * rowb) & mW;  // else: L2/MALL-hot re-read
       const f32x2 y = bf16x2_to_f32x2(w) - c2;          // v_pk_add_f32
       const f32x2 q = y * y;                              // v_pk_mul_f32
       part[i] = q.x + q.y;
@@ -351,10 +359,10 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
   }
 }
 
-template <int NSEG, int WAVES, int MODE>
+template <int NSEG, int WAVES, int MODE, bool RAW = false>
 static void launch_reg_mode(const FastParams& p, hipStream_t stream) {
-  auto k = p.constrained ? consensus_fast_reg_kernel<NSEG, WAVES, true, MODE>
-                         : consensus_fast_reg_kernel<NSEG, WAVES, false, MODE>;
+  auto k = p.constrained ? consensus_fast_reg_kernel<NSEG, WAVES, true, MODE, RAW>
+                         : consensus_fast_reg_kernel<NSEG, WAVES, false, MODE, RAW>;
   hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
 }
 
@@ -364,6 +372,8 @@ static int launch_reg(const FastParams& p, hipStream_t stream) {
     launch_reg_mode<NSEG, WAVES, 1>(p, stream);
   } else if (p.mode == 2) {
     launch_reg_mode<NSEG, WAVES, 2>(p, stream);
+  } else if (p.wave_hint == -6) {
+    launch_reg_mode<NSEG, WAVES, 0, true>(p, stream);  // fused, raw words kept in VGPRs (no re-read)
   } else if (p.wave_hint != -1) {
     launch_reg_mode<NSEG, WAVES, 0>(p, stream);  // fused single launch (default)
   } else {

@@ -37,7 +37,8 @@ class SyntheticUpdateStream:
                 gb = torch._standard_gamma(torch.full((e - s, D), a, device=dev), generator=g)
                 hon = ga / (ga + gb)
                 uni = torch.rand(e - s, D, generator=g, device=dev)
-                vals[s:e] = torch.where(fail[s:e, None], uni, hon).to(dtype)
+                x = torch.where(fail[s:e, None], uni, hon)
+                vals[s:e] = (x.double() * 1_000_000).to(torch.int64) if dtype == torch.int64 else x.to(dtype)
             self.batches.append((inst.contiguous(), orc.contiguous(), vals))
 
     def batch(self, i: int):

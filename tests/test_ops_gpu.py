@@ -97,6 +97,17 @@ def test_exact_hip_goldens(name):
     assert o["qr"][0].tolist() == g["qr"]
 
 
+def test_exact_hip_wide_instances_workspace():
+    """6*D int64 intermediates beyond 64 KiB of LDS: the kernel switches to an HBM workspace."""
+    rng = random.Random(4)
+    B, N, D = 3, 9, 1500
+    vals = torch.tensor([[[rng.randint(400000, 600000) for _ in range(D)] for _ in range(N)] for _ in range(B)])
+    oc = run_exact(vals, 2, True)
+    og = run_exact(vals.to(DEV), 2, True)
+    for k in ("status", "consensus", "rel", "qr", "skew", "kurt", "reliable", "c1"):
+        assert torch.equal(oc[k], og[k].cpu()), k
+
+
 @pytest.mark.parametrize("constrained", [True, False])
 def test_exact_hip_matches_cpu_random(constrained):
     rng = random.Random(99)
@@ -173,3 +184,19 @@ def test_fast_hip_split_modes_match_full(N, D, f, constrained):
         assert torch.equal(os_["reliable"][ok], full["reliable"][ok])
         torch.testing.assert_close(os_["consensus"][ok], full["consensus"][ok][:, lo:hi], rtol=0, atol=1e-6)
         torch.testing.assert_close(os_["rel"][ok], full["rel"][ok], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("N,D,hint", [(7, 6, 0), (64, 1024, 0), (256, 700, 0), (64, 1024, -6), (200, 96, -6),
+                                      (128, 512, 1)])
+def test_fast_kernels_deterministic(N, D, hint):
+    """Same inputs -> bitwise identical outputs (no float atomics; fixed reduction orders)."""
+    x, _ = beta_oracles(9, N, D, max(1, N // 8), seed=N + D)
+    xg = x.to(DEV)
+    a = run_fast(xg, D, max(1, N // 8), True, 1.0, wave_hint=hint)
+    b = run_fast(xg.clone(), D, max(1, N // 8), True, 1.0, wave_hint=hint)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+    r = torch_ref.fast_round(xg[:, :, :D], max(1, N // 8), True, 1.0)
+    ok = a["status"] == 0
+    assert ok.any()
+    _cmp_fast(a, r, ok)
