@@ -3,6 +3,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <cmath>
 #include <cstring>
 
 #include "svoc/launch.hpp"
@@ -83,6 +84,16 @@ void apply_updates_cpu(at::Tensor values, at::Tensor enabled, at::Tensor n_activ
     if (st == ST_OK && p.constrained)
       for (int d = 0; d < p.D; ++d)
         if (!in_range_cpu(p, u, d)) { st = ST_INTERVAL_INPUT; break; }
+    if (st == ST_OK && !p.constrained && p.dtype != 2)
+      for (int d = 0; d < p.D; ++d) {
+        const float f = p.dtype == 1 ? ((const float*)p.upd)[u * p.D + d] : [&] {
+          uint32_t w = (uint32_t)((const uint16_t*)p.upd)[u * p.D + d] << 16;
+          float x;
+          std::memcpy(&x, &w, 4);
+          return x;
+        }();
+        if (!std::isfinite(f)) { st = ST_NON_FINITE; break; }
+      }
     p.upd_status[u] = st;
     if (st != ST_OK) continue;
     std::memcpy((unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes,

@@ -24,6 +24,7 @@ enum Status : int {
   ST_WRONG_ADMIN_INDEX = 21,
   ST_ZERO_VARIANCE = 32,
   ST_TOO_FEW_RELIABLE = 33,
+  ST_NON_FINITE = 34,  // unconstrained float update with NaN / inf
 };
 
 }  // namespace svoc

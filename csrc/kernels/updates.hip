@@ -29,6 +29,13 @@ __device__ __forceinline__ bool bf16_unit(uint32_t raw16) {  // 0 <= x <= 1 (and
   return raw16 <= 0x3f80u || raw16 == 0x8000u;
 }
 
+// unconstrained float values must be finite (the wsad domain has no NaN / inf)
+__device__ __forceinline__ bool finite_at(const UpdateParams& p, int64_t u, int d) {
+  if (p.dtype == 0) return (((const uint16_t*)p.upd)[u * p.D + d] & 0x7f80u) != 0x7f80u;
+  if (p.dtype == 1) return (__builtin_bit_cast(uint32_t, ((const float*)p.upd)[u * p.D + d]) & 0x7f800000u) != 0x7f800000u;
+  return true;
+}
+
 // L lanes per update (L = power of two covering the row in 16-B chunks, capped at 64): a wave
 // serves 64/L updates, so the deployed 7 x 6 config (12-B rows) runs 64 updates per wave instead of
 // one, and wide rows (c3: 8 KiB) get a whole wave each.  True iff all L lanes of the group agree.
@@ -68,9 +75,14 @@ __global__ __launch_bounds__(256) void upd_validate_kernel(UpdateParams p) {
       for (int d = sub; d < p.D; d += L) ok = ok && in_range(p, u, d);
     }
   }
-  ok = group_all<L>(ok);  // all lanes reach the ballot (no early return above)
+  bool fin = true;
+  if (in && st == ST_OK && !p.constrained && p.dtype != 2)
+    for (int d = sub; d < p.D; d += L) fin = fin && finite_at(p, u, d);
+  ok = group_all<L>(ok);  // all lanes reach the ballots (no early return above)
+  fin = group_all<L>(fin);
   if (in && sub == 0) {
     if (st == ST_OK && !ok) st = ST_INTERVAL_INPUT;
+    if (st == ST_OK && !fin) st = ST_NON_FINITE;
     p.upd_status[u] = st;
     if (st == ST_OK) atomicMax(&p.winner[b * p.N + o], (int)u);
   }

@@ -33,6 +33,7 @@ class Status(enum.IntEnum):
     # fast-mode only (float path): non-fatal diagnostics are never produced, these revert outputs
     ZERO_VARIANCE = 32        # a reliable column has sigma == 0 (exact mode reports DIV_BY_ZERO)
     TOO_FEW_RELIABLE = 33     # R < 4: kurtosis denominator (n-2)(n-3) == 0 (exact: DIV_BY_ZERO)
+    NON_FINITE = 34           # unconstrained float update holding NaN / inf (no wsad counterpart)
 
     @property
     def is_revert(self) -> bool:

@@ -94,3 +94,17 @@ def test_fast_cpu_tracks_exact_on_fixtures():
         assert o["reliable"][0].bool().tolist() == g["reliable"]
         assert torch.allclose(o["consensus"][0].double(), torch.tensor(g["consensus"], dtype=torch.float64) / 1e6, atol=2e-6)
         assert torch.allclose(o["rel"][0].double(), torch.tensor([g["rel1"], g["rel2"]], dtype=torch.float64) / 1e6, atol=2e-5)
+
+
+def test_unconstrained_updates_reject_non_finite():
+    """Fast-mode unconstrained updates holding NaN / inf are rejected (NON_FINITE), others applied."""
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    from svoc.status import Status
+    e = ConsensusEngine(ConsensusConfig(n_oracles=4, dimension=3, n_failing_oracles=0, constrained=False,
+                                        unconstrained_max_spread=10.0), 2, device="cpu", mode="fast",
+                        storage="fp32")
+    vals = torch.tensor([[1.0, 2.0, 3.0], [float("nan"), 0.0, 0.0], [0.0, float("inf"), 0.0], [5.0, -5.0, 1e30]])
+    st = e.apply_updates(torch.tensor([0, 0, 1, 1]), torch.tensor([0, 1, 2, 3]), vals)
+    assert st.tolist() == [Status.OK, Status.NON_FINITE, Status.NON_FINITE, Status.OK]
+    assert e.values[0, 0, :3].tolist() == [1.0, 2.0, 3.0] and int(e.enabled[0, 1]) == 0

@@ -200,3 +200,18 @@ def test_fast_kernels_deterministic(N, D, hint):
     ok = a["status"] == 0
     assert ok.any()
     _cmp_fast(a, r, ok)
+
+
+def test_unconstrained_updates_reject_non_finite_gpu():
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    from svoc.status import Status
+    for D in (3, 64):   # 1 lane and 8 lanes per update
+        e = ConsensusEngine(ConsensusConfig(n_oracles=4, dimension=D, n_failing_oracles=0, constrained=False,
+                                            unconstrained_max_spread=10.0), 2, device=DEV, mode="fast")
+        vals = torch.zeros(4, D)
+        vals[1, D - 1] = float("nan")
+        vals[2, 0] = float("-inf")
+        st = e.apply_updates(torch.tensor([0, 0, 1, 1], device=DEV), torch.tensor([0, 1, 2, 3], device=DEV),
+                             vals.to(DEV))
+        assert st.cpu().tolist() == [Status.OK, Status.NON_FINITE, Status.NON_FINITE, Status.OK]
