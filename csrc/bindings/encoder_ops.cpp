@@ -65,8 +65,9 @@ void register_encoder_hip(torch::Library& m) {
 
 }  // namespace svoc
 
-extern "C" int svoc_attention_short_bf16(const void* qkv, const void* kmask, void* out, int64_t B, int S, int H,
-                                         int DH, hipStream_t stream);
+extern "C" int svoc_attention_short_bf16(const void* qkv, const void* kmask, const int* cu_seqlens,
+                                         int64_t rows_total, void* out, int64_t B, int S, int H, int DH,
+                                         hipStream_t stream);
 
 namespace svoc {
 namespace {
@@ -101,10 +102,49 @@ at::Tensor attention_hip(const at::Tensor& qkv, const c10::optional<at::Tensor>&
     m = key_mask->to(at::kByte).contiguous();
   }
   auto out = at::empty({B, S, HD}, x.options());
-  const int rc = svoc_attention_short_bf16(x.data_ptr(), key_mask.has_value() ? m.data_ptr() : nullptr,
+  const int rc = svoc_attention_short_bf16(x.data_ptr(), key_mask.has_value() ? m.data_ptr() : nullptr, nullptr, 0,
                                            out.data_ptr(), B, (int)S, (int)heads, (int)DH,
                                            c10::hip::getCurrentHIPStream(x.device().index()).stream());
   TORCH_CHECK(rc == 0, "svoc_attention_short_bf16 failed: ", rc);
+  return out;
+}
+
+// packed (unpadded) tokens: qkv [T, 3*H*DH], sequence b = rows [cu[b], cu[b+1])
+at::Tensor attention_varlen_ref(const at::Tensor& qkv, const at::Tensor& cu, int64_t max_len, int64_t heads) {
+  (void)max_len;
+  const int64_t T = qkv.size(0), HD = qkv.size(1) / 3, DH = HD / heads;
+  auto cuh = cu.to(at::kCPU, at::kLong);
+  auto out = at::empty({T, HD}, qkv.options());
+  for (int64_t b = 0; b + 1 < cuh.numel(); ++b) {
+    const int64_t lo = cuh[b].item<int64_t>(), hi = cuh[b + 1].item<int64_t>();
+    if (hi <= lo) continue;
+    auto t = qkv.slice(0, lo, hi).view({hi - lo, 3, heads, DH}).permute({1, 2, 0, 3}).to(at::kFloat);
+    auto s = at::matmul(t[0], t[1].transpose(-1, -2)) / std::sqrt((double)DH);
+    auto o = at::matmul(at::softmax(s, -1), t[2]);  // [heads, L, DH]
+    out.slice(0, lo, hi).copy_(o.transpose(0, 1).reshape({hi - lo, HD}));
+  }
+  return out;
+}
+
+at::Tensor attention_varlen_cpu(const at::Tensor& qkv, const at::Tensor& cu, int64_t max_len, int64_t heads) {
+  return attention_varlen_ref(qkv, cu, max_len, heads);
+}
+
+at::Tensor attention_varlen_hip(const at::Tensor& qkv, const at::Tensor& cu, int64_t max_len, int64_t heads) {
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) % (3 * heads) == 0, "qkv: [T, 3*H*DH]");
+  TORCH_CHECK(cu.scalar_type() == at::kInt && cu.dim() == 1 && cu.is_contiguous() && cu.device() == qkv.device(),
+              "cu_seqlens: int32 [B+1] on the device");
+  const int64_t T = qkv.size(0), HD = qkv.size(1) / 3, DH = HD / heads, B = cu.numel() - 1;
+  const int64_t S = (max_len + 31) / 32 * 32;
+  const bool ok = qkv.scalar_type() == at::kBFloat16 && DH == 64 && S >= 32 && S <= 128;
+  if (!ok) return attention_varlen_ref(qkv, cu, max_len, heads);
+  auto x = qkv.contiguous();
+  auto out = at::empty({T, HD}, x.options());
+  if (T == 0) return out;
+  const int rc = svoc_attention_short_bf16(x.data_ptr(), nullptr, cu.data_ptr<int>(), T, out.data_ptr(), B, (int)S,
+                                           (int)heads, (int)DH,
+                                           c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  TORCH_CHECK(rc == 0, "svoc_attention_short_bf16 (varlen) failed: ", rc);
   return out;
 }
 
@@ -112,8 +152,15 @@ at::Tensor attention_hip(const at::Tensor& qkv, const c10::optional<at::Tensor>&
 
 void register_attention_defs(torch::Library& m) {
   m.def("attention_qkv(Tensor qkv, Tensor? key_mask, int heads) -> Tensor");
+  m.def("attention_varlen(Tensor qkv, Tensor cu_seqlens, int max_len, int heads) -> Tensor");
 }
-void register_attention_cpu(torch::Library& m) { m.impl("attention_qkv", &attention_cpu); }
-void register_attention_hip(torch::Library& m) { m.impl("attention_qkv", &attention_hip); }
+void register_attention_cpu(torch::Library& m) {
+  m.impl("attention_qkv", &attention_cpu);
+  m.impl("attention_varlen", &attention_varlen_cpu);
+}
+void register_attention_hip(torch::Library& m) {
+  m.impl("attention_qkv", &attention_hip);
+  m.impl("attention_varlen", &attention_varlen_hip);
+}
 
 }  // namespace svoc

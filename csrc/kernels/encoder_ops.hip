@@ -122,25 +122,36 @@ namespace svoc {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-template <int NQB>  // S / 32: query blocks = waves = key blocks
+template <int NQB>  // S_max / 32: query blocks = waves = key blocks
 __global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __restrict__ qkv,
                                                              const uint8_t* __restrict__ kmask,
-                                                             uint16_t* __restrict__ out, int H,
-                                                             float scale_log2) {
+                                                             const int* __restrict__ cu_seqlens,
+                                                             int64_t rows_total, uint16_t* __restrict__ out,
+                                                             int H, float scale_log2) {
   constexpr int S = 32 * NQB, DH = 64, PITCH = S + 4;  // bf16 elements per Vt row
   __shared__ uint16_t Vt[DH * PITCH];
   __shared__ uint8_t km[S];
   const int bh = blockIdx.x, b = bh / H, h = bh % H;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int64_t ts = (int64_t)3 * H * DH;  // token stride in qkv (elements)
-  const uint16_t* Qb = qkv + (int64_t)b * S * ts + h * DH;
+  // padded batch: sequence b = rows [b*S, b*S + S), keys masked by kmask.
+  // packed (varlen): sequence b = rows [cu[b], cu[b+1]), keys past its length masked; rows read past
+  // the end of the buffer are clamped (their scores are masked, their V rows get P = 0).
+  const int64_t base = cu_seqlens ? cu_seqlens[b] : (int64_t)b * S;
+  const int L = cu_seqlens ? cu_seqlens[b + 1] - cu_seqlens[b] : S;
+  const int nkb = (L + 31) >> 5;  // key / query blocks holding real tokens
+  auto row = [&](int k) -> int64_t {
+    const int64_t t = base + k;
+    return t < rows_total ? t : rows_total - 1;
+  };
+  const uint16_t* Qb = qkv + h * DH;
   const uint16_t* Kb = Qb + H * DH;
   const uint16_t* Vb = Qb + 2 * H * DH;
 
   // stage Vᵀ and the key mask
-  for (int c = tid; c < S * (DH / 8); c += 64 * NQB) {
+  for (int c = tid; c < nkb * 32 * (DH / 8); c += 64 * NQB) {
     const int key = c >> 3, e0 = (c & 7) * 8;
-    const uint4 v = *(const uint4*)(Vb + key * ts + e0);
+    const uint4 v = *(const uint4*)(Vb + row(key) * ts + e0);
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -148,24 +159,32 @@ __global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __
       Vt[(e0 + 2 * i + 1) * PITCH + key] = (uint16_t)(w[i] >> 16);
     }
   }
-  for (int k = tid; k < S; k += 64 * NQB) km[k] = kmask ? kmask[(int64_t)b * S + k] : (uint8_t)1;
+  for (int k = tid; k < S; k += 64 * NQB)
+    km[k] = cu_seqlens ? (uint8_t)(k < L) : (kmask ? kmask[(int64_t)b * S + k] : (uint8_t)1);
 
   // X = K·Qᵀ for this wave's 32 queries: rows = keys (registers), column = query (lane)
   const int q0 = wave * 32;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(Qb + (q0 + r) * ts + ds * 16 + 8 * hh);
+  const bool active = q0 < L;
   f32x16 x[NQB];
 #pragma unroll
-  for (int kb = 0; kb < NQB; ++kb) {
-    x[kb] = f32x16{};
+  for (int kb = 0; kb < NQB; ++kb) x[kb] = f32x16{};
+  if (active) {
+    bf16x8 qf[4];
 #pragma unroll
-    for (int ds = 0; ds < 4; ++ds) {
-      const bf16x8 kf = *(const bf16x8*)(Kb + (kb * 32 + r) * ts + ds * 16 + 8 * hh);
-      x[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], x[kb], 0, 0, 0);
+    for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(Qb + row(q0 + r) * ts + ds * 16 + 8 * hh);
+#pragma unroll
+    for (int kb = 0; kb < NQB; ++kb) {
+      if (kb < nkb) {
+#pragma unroll
+        for (int ds = 0; ds < 4; ++ds) {
+          const bf16x8 kf = *(const bf16x8*)(Kb + row(kb * 32 + r) * ts + ds * 16 + 8 * hh);
+          x[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], x[kb], 0, 0, 0);
+        }
+      }
     }
   }
   __syncthreads();  // Vt and km staged
+  if (!active) return;
 
   // softmax over the keys of query q0 + r (this lane: key rows (i&3) + 8(i>>2) + 4hh of each block)
   float m = -__builtin_inff();
@@ -173,7 +192,7 @@ __global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __
   for (int kb = 0; kb < NQB; ++kb)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const uint32_t mk4 = *(const uint32_t*)(km + kb * 32 + 8 * g + 4 * hh);  // 4 consecutive keys
+      const uint32_t mk4 = kb < nkb ? *(const uint32_t*)(km + kb * 32 + 8 * g + 4 * hh) : 0u;  // 4 keys
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int i = 4 * g + t;
@@ -199,7 +218,8 @@ __global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __
   // Z = P·V: A = P (accumulator registers, rows = keys), B = V from Vᵀ in LDS
   f32x16 z[2] = {f32x16{}, f32x16{}};
 #pragma unroll
-  for (int kb = 0; kb < NQB; ++kb)
+  for (int kb = 0; kb < NQB; ++kb) {
+    if (kb >= nkb) continue;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 pa;
@@ -220,34 +240,37 @@ __global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __
         z[eb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, vf, z[eb], 0, 0, 0);
       }
     }
-  // store: z[eb][i] = Z[query (i&3)+8(i>>2)+4hh][e = eb*32 + r]
-  uint16_t* Ob = out + ((int64_t)b * S + q0) * H * DH + h * DH;
+  }
+  // store: z[eb][i] = Z[query (i&3)+8(i>>2)+4hh][e = eb*32 + r]; queries past the length skipped
 #pragma unroll
   for (int eb = 0; eb < 2; ++eb)
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const int q = (i & 3) + 8 * (i >> 2) + 4 * hh;
-      Ob[(int64_t)q * H * DH + eb * 32 + r] = f2bf(z[eb][i]);
+      const int q = q0 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+      if (q < L) out[(base + q) * H * DH + h * DH + eb * 32 + r] = f2bf(z[eb][i]);
     }
 }
 
 }  // namespace svoc
 
 // qkv: [B, S, 3, H, 64] bf16 contiguous; kmask: [B, S] uint8 (1 = attend) or null; out: [B, S, H, 64].
-extern "C" int svoc_attention_short_bf16(const void* qkv, const void* kmask, void* out, int64_t B, int S, int H,
-                                         int DH, hipStream_t stream) {
+// Packed variant: cu_seqlens [B + 1] (device) with sequence b at rows [cu[b], cu[b+1]), lengths <= S;
+// qkv: [rows_total, 3, H, 64], out: [rows_total, H, 64].
+extern "C" int svoc_attention_short_bf16(const void* qkv, const void* kmask, const int* cu_seqlens, int64_t rows_total,
+                                         void* out, int64_t B, int S, int H, int DH, hipStream_t stream) {
   if (DH != 64 || S % 32 != 0 || S < 32 || S > 128 || B * H > 0x7fffffffll) return -1;
   if (B == 0) return 0;
   const float scale_log2 = 1.4426950408889634f / 8.f;  // log2(e) / sqrt(64)
   const auto* Q = (const uint16_t*)qkv;
   const auto* M = (const uint8_t*)kmask;
   auto* O = (uint16_t*)out;
+  const int64_t R = cu_seqlens ? rows_total : B * S;
   const dim3 grid((unsigned)(B * H));
   switch (S / 32) {
-    case 1: hipLaunchKernelGGL(attn_short_kernel<1>, grid, dim3(64), 0, stream, Q, M, O, H, scale_log2); break;
-    case 2: hipLaunchKernelGGL(attn_short_kernel<2>, grid, dim3(128), 0, stream, Q, M, O, H, scale_log2); break;
-    case 3: hipLaunchKernelGGL(attn_short_kernel<3>, grid, dim3(192), 0, stream, Q, M, O, H, scale_log2); break;
-    default: hipLaunchKernelGGL(attn_short_kernel<4>, grid, dim3(256), 0, stream, Q, M, O, H, scale_log2); break;
+    case 1: hipLaunchKernelGGL(attn_short_kernel<1>, grid, dim3(64), 0, stream, Q, M, cu_seqlens, R, O, H, scale_log2); break;
+    case 2: hipLaunchKernelGGL(attn_short_kernel<2>, grid, dim3(128), 0, stream, Q, M, cu_seqlens, R, O, H, scale_log2); break;
+    case 3: hipLaunchKernelGGL(attn_short_kernel<3>, grid, dim3(192), 0, stream, Q, M, cu_seqlens, R, O, H, scale_log2); break;
+    default: hipLaunchKernelGGL(attn_short_kernel<4>, grid, dim3(256), 0, stream, Q, M, cu_seqlens, R, O, H, scale_log2); break;
   }
   return (int)hipGetLastError();
 }

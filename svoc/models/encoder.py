@@ -75,6 +75,27 @@ class Layer(nn.Module):
         x = _add_ln(x, self.out(a), self.ln1)
         return _add_ln(x, self.fc2(_linear_gelu(x, self.fc1)), self.ln2)
 
+    def forward_packed(self, x: torch.Tensor, plan: "PackPlan") -> torch.Tensor:
+        """x: [T, H] real tokens only (sequence b = rows [cu[b], cu[b+1]))."""
+        from .. import ops as svops
+        a = svops.ops().attention_varlen(self.qkv(x), plan.cu, plan.max_len, self.heads)
+        x = _add_ln(x, self.out(a), self.ln1)
+        return _add_ln(x, self.fc2(_linear_gelu(x, self.fc1)), self.ln2)
+
+
+@dataclasses.dataclass
+class PackPlan:
+    """Unpadded token layout of a right-padded batch (the reference pipeline classifies each comment
+    on its own, i.e. never computes padding tokens)."""
+    idx: torch.Tensor      # [T] flat positions b * S + s of the real tokens, in order
+    pos: torch.Tensor      # [T] position ids
+    cu: torch.Tensor       # [B + 1] int32 sequence offsets
+    lens: torch.Tensor     # [B] float lengths
+    T: int
+    B: int
+    S: int
+    max_len: int
+
 
 def _linear_gelu(x: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
     """fc1 + GELU; on the GPU the GELU runs in the hipBLASLt GEMM epilogue (one pass over the
@@ -102,6 +123,8 @@ class SentimentEncoder(nn.Module):
         self.dense = nn.Linear(c.hidden, c.hidden)      # RobertaClassificationHead: dense-tanh-out
         self.head = nn.Linear(c.hidden, c.n_labels)
         self.apply(self._init)
+        self.packed = True                 # unpadded token path on the GPU (see plan())
+        self._plan_cache = None
         # random-init head scaled so the synthetic scores spread like a trained multi-label head's
         # (larger logits than the default init): keeps honest bootstrap oracles distinguishable at wsad
         # resolution, otherwise every column has ~zero variance and the contract reverts (§2.8-5)
@@ -115,9 +138,46 @@ class SentimentEncoder(nn.Module):
         if isinstance(m, nn.Linear) and m.bias is not None:
             nn.init.zeros_(m.bias)
 
+    def plan(self, attention_mask: torch.Tensor) -> Optional[PackPlan]:
+        """Packing plan of a right-padded mask (None if some row is not of the form 1..1 0..0).
+        Cached per mask tensor (data pointer + version), so a captured HIP graph replays without
+        the host synchronisation this needs the first time."""
+        key = (attention_mask.data_ptr(), attention_mask._version, tuple(attention_mask.shape))
+        if self._plan_cache is not None and self._plan_cache[0] == key:
+            return self._plan_cache[1]
+        B, S = attention_mask.shape
+        m = attention_mask.bool()
+        lens = m.sum(1)
+        plan = None
+        if torch.equal(m, torch.arange(S, device=m.device)[None] < lens[:, None]):
+            idx = m.flatten().nonzero().squeeze(1)
+            cu = torch.zeros(B + 1, dtype=torch.int32, device=m.device)
+            cu[1:] = lens.cumsum(0).to(torch.int32)
+            plan = PackPlan(idx=idx, pos=idx % S + 2, cu=cu, lens=lens.to(torch.float32).clamp(min=1), T=int(idx.numel()),
+                            B=B, S=S, max_len=int(lens.max()) if B else 0)
+        self._plan_cache = (key, plan)
+        return plan
+
+    def _forward_packed(self, ids: torch.Tensor, p: PackPlan) -> torch.Tensor:
+        x = self.ln(self.tok(ids.reshape(-1)[p.idx]) + self.pos(p.pos) + self.typ.weight[0])   # [T, H]
+        for layer in self.layers:
+            x = layer.forward_packed(x, p)
+        if self.cfg.pool == "cls":
+            pooled = x[p.cu[:-1].long()]
+        else:   # masked mean: scatter back to the padded grid (unique indices: deterministic) and sum
+            xp = torch.zeros(p.B * p.S, x.shape[1], dtype=torch.float32, device=x.device)
+            xp[p.idx] = x.float()
+            pooled = (xp.view(p.B, p.S, -1).sum(1) / p.lens[:, None]).to(x.dtype)
+        h = torch.tanh(self.dense(pooled))
+        return torch.sigmoid(self.head(h).float())
+
     def forward(self, ids: torch.Tensor, attention_mask: Optional[torch.Tensor] = None) -> torch.Tensor:
         """ids [B, S] -> 28 sigmoid scores [B, 28] (float32)."""
         B, S = ids.shape
+        if self.packed and attention_mask is not None and ids.is_cuda and S <= 128:
+            p = self.plan(attention_mask)
+            if p is not None and p.T > 0:
+                return self._forward_packed(ids, p)
         pos = torch.arange(2, S + 2, device=ids.device)           # RoBERTa positions start at pad+1
         x = self.ln(self.tok(ids) + self.pos(pos)[None] + self.typ.weight[0])
         kmask = attention_mask.to(torch.uint8) if attention_mask is not None else None

@@ -71,3 +71,30 @@ def test_encoder_fused_matches_cpu_fp32():
         sg = enc_g(ids.cuda(), mask.cuda()).float().cpu()
         sc = enc_c(ids, mask)
     torch.testing.assert_close(sg, sc, rtol=0, atol=0.05)
+
+
+def test_attention_varlen_mfma():
+    heads = 12
+    lens = [128, 1, 33, 64, 95, 7, 128, 32]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device="cuda")
+    T = int(cu[-1])
+    g = torch.Generator(device="cuda").manual_seed(1)
+    qkv = torch.randn(T, 3 * heads * 64, device="cuda", generator=g).to(torch.bfloat16)
+    out = svops.ops().attention_varlen(qkv, cu, max(lens), heads)
+    ref = svops.ops().attention_varlen(qkv.cpu().float(), cu.cpu(), max(lens), heads)   # CPU reference path
+    torch.testing.assert_close(out.float().cpu(), ref.float(), rtol=3e-2, atol=3e-2)
+
+
+def test_encoder_packed_equals_padded():
+    from svoc.models.encoder import EncoderConfig, build
+    cfg = EncoderConfig(vocab_size=500, hidden=768, layers=2, heads=12, ffn=3072, max_positions=130)
+    enc = build("cuda", torch.bfloat16, seed=4, cfg=cfg)
+    g = torch.Generator().manual_seed(2)
+    ids = torch.randint(3, 500, (7, 128), generator=g).cuda()
+    mask = (torch.arange(128)[None] < torch.tensor([128, 40, 77, 1, 9, 100, 64])[:, None]).to(torch.int64).cuda()
+    with torch.no_grad():
+        a = enc(ids, mask)
+        assert enc.plan(mask) is not None and enc.plan(mask).T == 419
+        enc.packed = False
+        b = enc(ids, mask)
+    torch.testing.assert_close(a, b, rtol=0, atol=0.03)
