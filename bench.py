@@ -91,13 +91,17 @@ def main():
     extra = {}
     if args.config == "c4":
         from svoc.models import corpus
-        from svoc.models.encoder import flops_per_sequence
         from svoc.models.sentiment_oracle import SentimentOraclePipeline
         pipe = SentimentOraclePipeline(eng, seed=0)
         g = torch.Generator(device=dev).manual_seed(rank)
         toks = [corpus.synthetic_token_batch(B * 30, c["seq_len"], 50265, g, dev) for _ in range(2)]
+        from svoc.models.encoder import flops_for_lengths
         extra["comments_per_step"] = B * 30
-        extra["encoder_gflop_per_step"] = B * 30 * flops_per_sequence(pipe.encoder.cfg, c["seq_len"]) / 1e9
+        lens = toks[0][1].sum(1).tolist()
+        extra["real_tokens_per_step"] = int(sum(lens))
+        extra["padded_tokens_per_step"] = B * 30 * c["seq_len"]
+        # the packed path computes real tokens only (as the reference pipeline, one comment at a time)
+        extra["encoder_gflop_per_step"] = flops_for_lengths(pipe.encoder.cfg, lens) / 1e9
     elif U_per_inst:
         from svoc.stream import SyntheticUpdateStream
         stream = SyntheticUpdateStream(B, c["N"], c["D"], U_per_inst, c["f"], pool=2, device=dev, seed=rank,

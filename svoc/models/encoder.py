@@ -206,6 +206,11 @@ def build(device="cuda", dtype=torch.bfloat16, seed: int = 0, cfg: EncoderConfig
     return m.to(device=device, dtype=dtype).eval()
 
 
+def flops_for_lengths(c: EncoderConfig, lens) -> float:
+    """Forward FLOPs of a batch of unpadded sequences (lengths ``lens``)."""
+    return float(sum(flops_per_sequence(c, int(n)) for n in lens))
+
+
 def flops_per_sequence(c: EncoderConfig, S: int) -> float:
     """Forward FLOPs for one sequence (GEMMs + attention), for throughput reporting."""
     per_layer = 2 * S * c.hidden * (3 * c.hidden + c.hidden + 2 * c.ffn) + 4 * S * S * c.hidden
