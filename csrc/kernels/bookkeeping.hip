@@ -11,19 +11,22 @@ __global__ __launch_bounds__(256) void round_prologue_kernel(RoundBook r) {
   if (b < r.B) r.active[b] = book_active(r, b);
 }
 
+// grid-stride over the instances with at most EPI_BLOCKS workgroups: the four counter atomics per
+// workgroup then number a few thousand instead of B/64 (1M instances: 16k same-address atomics)
+constexpr int EPI_BLOCKS = 512;
+
 __global__ __launch_bounds__(256) void round_epilogue_kernel(RoundBook r) {
-  const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
   unsigned long long v[4] = {0, 0, 0, 0};
-  if (b < r.B) {
+  for (int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x; b < r.B; b += (int64_t)gridDim.x * 256) {
     const bool act = r.active[b] != 0;
     const bool ok = book_ok(r, b);
     if (ok) {
       r.consensus_active[b] = 1;
-      v[0] = book_rel2_fx(r, b);
-      v[1] = 1;
+      v[0] += book_rel2_fx(r, b);
+      v[1] += 1;
     }
-    v[2] = act ? 1 : 0;
-    v[3] = (act && !ok) ? 1 : 0;
+    v[2] += act ? 1 : 0;
+    v[3] += (act && !ok) ? 1 : 0;
     r.touched[b] = 0;
   }
   if (r.acc == nullptr) return;
@@ -56,6 +59,8 @@ extern "C" int svoc_round_prologue(const RoundBook* r, hipStream_t stream) {
 
 extern "C" int svoc_round_epilogue(const RoundBook* r, hipStream_t stream) {
   if (r->B <= 0) return 0;
-  hipLaunchKernelGGL(round_epilogue_kernel, dim3((unsigned)((r->B + 255) / 256)), dim3(256), 0, stream, *r);
+  const int64_t blocks = (r->B + 255) / 256;
+  hipLaunchKernelGGL(round_epilogue_kernel, dim3((unsigned)(blocks < EPI_BLOCKS ? blocks : EPI_BLOCKS)), dim3(256), 0,
+                     stream, *r);
   return (int)hipGetLastError();
 }

@@ -25,17 +25,39 @@
 
 namespace svoc {
 
+// Butterfly all-reduce over the G lanes of a group on DPP (no LDS crossbar): quad_perm [1,0,3,2]
+// and [2,3,0,1] (xor 1, xor 2), row_half_mirror (pairs each quad with the other quad of its 8-lane
+// half), row_ror:8 (xor 8 in a 16-lane row); xor 16 / 32 by ds_bpermute.  Every step adds two
+// partner values in both lanes, so all G lanes end with the bit-identical sum (fp add commutes).
+template <int CTRL>
+SVOC_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+SVOC_DEV int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, false);
+}
+constexpr int DPP_XOR1 = 0xB1, DPP_XOR2 = 0x4E, DPP_HALF_MIRROR = 0x141, DPP_ROR8 = 0x128;
+
 template <int G>
 SVOC_DEV float group_sum(float v) {
-#pragma unroll
-  for (int m = 1; m < G; m <<= 1) v += __shfl_xor(v, m);
+  if constexpr (G >= 2) v += dpp_f<DPP_XOR1>(v);
+  if constexpr (G >= 4) v += dpp_f<DPP_XOR2>(v);
+  if constexpr (G >= 8) v += dpp_f<DPP_HALF_MIRROR>(v);
+  if constexpr (G >= 16) v += dpp_f<DPP_ROR8>(v);
+  if constexpr (G >= 32) v += __shfl_xor(v, 16);
+  if constexpr (G >= 64) v += __shfl_xor(v, 32);
   return v;
 }
 
 template <int G>
 SVOC_DEV int group_or(int v) {
-#pragma unroll
-  for (int m = 1; m < G; m <<= 1) v |= __shfl_xor(v, m);
+  if constexpr (G >= 2) v |= dpp_i<DPP_XOR1>(v);
+  if constexpr (G >= 4) v |= dpp_i<DPP_XOR2>(v);
+  if constexpr (G >= 8) v |= dpp_i<DPP_HALF_MIRROR>(v);
+  if constexpr (G >= 16) v |= dpp_i<DPP_ROR8>(v);
+  if constexpr (G >= 32) v |= __shfl_xor(v, 16);
+  if constexpr (G >= 64) v |= __shfl_xor(v, 32);
   return v;
 }
 
