@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--config-file", default=None, help="YAML config (configs/*.yaml); overrides --config")
     ap.add_argument("--batch", type=int, default=0, help="instances per GPU (default per config)")
     ap.add_argument("--wave-hint", type=int, default=0)
     ap.add_argument("--graph", type=int, default=1, help="capture the step in a HIP graph")
@@ -66,6 +67,13 @@ def main():
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.config_file:
+        import yaml
+        with open(args.config_file, encoding="utf-8") as f:
+            doc = yaml.safe_load(f)
+        args.config = doc.pop("name")
+        doc.pop("baseline_config", None)
+        CONFIGS[args.config] = {**CONFIGS.get(args.config, {}), **doc}
     c = CONFIGS[args.config]
     dev = torch.device("cuda", local) if c.get("device", "cuda") == "cuda" else torch.device("cpu")
 
