@@ -56,6 +56,10 @@ def main():
     ap.add_argument("--graph", type=int, default=1, help="capture the step in a HIP graph")
     ap.add_argument("--mode", default=None, choices=["fast", "exact"],
                     help="override the config's engine mode (exact = bit-exact wsad int64 path)")
+    ap.add_argument("--dshard", action="store_true",
+                    help="strong scaling: every rank holds a column slice of ALL instances (D-sharding, one "
+                         "[B, N] qr all-reduce per round) instead of its own instances (DP, default)")
+    ap.add_argument("--backend", default=None, help="torch.distributed backend (default: nccl = RCCL on GPU)")
     ap.add_argument("--log", default=None, help="append the result record to this JSON-lines file")
     ap.add_argument("--kernel-table", type=int, default=0, help="profile N extra steps (torch.profiler) "
                     "after the timed region and add the per-kernel table to the log record")
@@ -64,9 +68,6 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if args.config_file:
         import yaml
         with open(args.config_file, encoding="utf-8") as f:
@@ -76,6 +77,13 @@ def main():
         CONFIGS[args.config] = {**CONFIGS.get(args.config, {}), **doc}
     c = CONFIGS[args.config]
     dev = torch.device("cuda", local) if c.get("device", "cuda") == "cuda" else torch.device("cpu")
+    if world > 1:
+        if dev.type == "cuda":
+            torch.cuda.set_device(local)
+            dist.init_process_group(args.backend or "nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend or "gloo")
+    dshard = args.dshard and world > 1
 
     from svoc.config import ConsensusConfig
     from svoc.engine import ConsensusEngine
@@ -86,12 +94,19 @@ def main():
             torch.cuda.synchronize(dev)
 
     B = args.batch or c["batch"]
-    cfg = ConsensusConfig(n_oracles=c["N"], dimension=c["D"], n_failing_oracles=c["f"], constrained=True)
+    D_local, lo = c["D"], 0
+    if dshard:
+        from svoc.parallel.dshard import run_round_sharded, shard_bounds
+        lo, hi = shard_bounds(c["D"], rank, world)
+        D_local = hi - lo
+    cfg = ConsensusConfig(n_oracles=c["N"], dimension=D_local, n_failing_oracles=c["f"], constrained=True)
     mode = args.mode or c.get("mode", "fast")
+    if dshard and (mode != "fast" or args.config in ("c4", "c5")):
+        raise SystemExit("--dshard is for the fast column-sharded configs (c2, c3)")
     eng = ConsensusEngine(cfg, batch=B, device=dev, mode=mode)
     eng.wave_hint = args.wave_hint
     dp = DataParallelConsensus(eng, rank=rank, world=world)
-    eng.randomize(seed=1000 + rank)
+    eng.randomize(seed=1000 + (0 if dshard else rank))
 
     # synthetic update stream resident in HBM: `pool` steps of updates, cycled
     U_per_inst = int(round(c["update_frac"] * c["N"]))
@@ -112,7 +127,9 @@ def main():
         extra["encoder_gflop_per_step"] = flops_for_lengths(pipe.encoder.cfg, lens) / 1e9
     elif U_per_inst:
         from svoc.stream import SyntheticUpdateStream
-        stream = SyntheticUpdateStream(B, c["N"], c["D"], U_per_inst, c["f"], pool=2, device=dev, seed=rank,
+        # D-sharding: every rank streams the same updates (same seed), its own column slice of them
+        stream = SyntheticUpdateStream(B, c["N"], D_local, U_per_inst, c["f"], pool=2, device=dev,
+                                       seed=(0 if dshard else rank),
                                        dtype=torch.int64 if mode == "exact" else torch.bfloat16)
     if args.config == "c5":
         from svoc.codec import address_to_limbs
@@ -136,16 +153,22 @@ def main():
         extra["state_bytes_per_instance"] = eng.bytes_per_instance(c["N"], c["D"], "fast") + 3 * 4 * 8 + 3 * 8 + 3 * (1 + 4 + 32) + c["N"] * 32
         extra["instances_per_288GB"] = int(288e9 // extra["state_bytes_per_instance"])
 
+    def run_round():
+        if dshard:
+            run_round_sharded(eng, c["D"], world=world)   # includes the qr all-reduce
+        else:
+            eng.run_round(only_touched=True)
+
     def step(i):  # device-only work (capturable)
         if pipe is not None:
             pipe.fetch(*toks[i % 2])
         elif stream is not None:
             inst, orc, vals = stream.batch(i)
             eng.apply_updates(inst, orc, vals)
-            eng.run_round(only_touched=True)
+            run_round()
         else:
             eng.touched.fill_(1)
-            eng.run_round(only_touched=True)
+            run_round()
         if gov is not None:
             gov.submit_tensors(*gov_batches[i % 2])
         dp.accumulate()
@@ -156,7 +179,7 @@ def main():
     sync()
 
     graph = None
-    if args.graph and dev.type == "cuda":
+    if args.graph and dev.type == "cuda" and not dshard:   # (no collectives inside a captured graph)
         # the stream cycles with period `pool`: capture one period and replay it
         period = stream.pool if stream is not None else (2 if (pipe is not None or gov is not None) else 1)
         s = torch.cuda.Stream(device=dev)
@@ -204,17 +227,17 @@ def main():
         dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     el = float(elapsed.item())
     ms_per_step = 1e3 * el / steps_done
-    rounds = B * world * steps_done
+    rounds = B * (1 if dshard else world) * steps_done   # D-sharding: all ranks share the same B instances
     value = rounds / el
     ok = dp.global_ok_fraction()
     if rank == 0:
         out = {
             "metric": METRIC, "value": value, "unit": "consensus rounds/s", "n_gpus": world,
             "steps": steps_done, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None,
+            "scaling": "strong" if dshard else "weak", "vs_baseline": None,
             "dtype": "int64-wsad" if mode == "exact" else c.get("dtype", "bf16"), "data": "synthetic",
-            "config": {"model": c["model"], "global_batch": B * world, "seq_len": c["D"],
-                       "parallelism": f"dp{world}", "engine_mode": mode, "n_oracles": c["N"], "dimension": c["D"],
+            "config": {"model": c["model"], "global_batch": B * (1 if dshard else world), "seq_len": c["D"],
+                       "parallelism": f"dshard{world}" if dshard else f"dp{world}", "engine_mode": mode, "n_oracles": c["N"], "dimension": c["D"],
                        "n_failing": c["f"], "updates_per_instance_per_step": U_per_inst,
                        "oracle_updates_per_s": (U_per_inst * rounds / el) if U_per_inst else 0.0,
                        "hip_graph": graph is not None, "ok_fraction": ok, **extra},

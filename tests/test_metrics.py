@@ -51,3 +51,38 @@ def test_bench_c1_record(tmp_path):
     assert out["steps"] == 20 and out["value"] > 0 and out["config"]["ok_fraction"] == 1.0
     rec = metrics.read_jsonl(str(log))[-1]
     assert rec["kind"] == "bench" and rec["health"]["consensus_active"] == 1
+
+
+def _cpu_cfg(tmp_path):
+    p = tmp_path / "cpu_small.yaml"
+    p.write_text("name: cpu_small\nmodel: test N=16 D=64 streaming\nN: 16\nD: 64\nf: 2\nbatch: 8\n"
+                 "update_frac: 0.25\ndevice: cpu\nmode: fast\n")
+    return str(p)
+
+
+def _run_dist(args, timeout=600):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py")] + args
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-4000:]
+    return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+
+
+def _port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_bench_two_ranks_dp_and_dshard_gloo(tmp_path):
+    """The driver's multi-rank contract (torch.distributed.run, max over ranks, rank-0 JSON) on gloo."""
+    cfg = _cpu_cfg(tmp_path)
+    dp = _run_dist(["--config-file", cfg, "--gpus", "2", "--steps", "4", "--warmup", "1"])
+    assert dp["n_gpus"] == 2 and dp["scaling"] == "weak" and dp["config"]["global_batch"] == 16
+    assert dp["config"]["ok_fraction"] == 1.0
+    ds = _run_dist(["--config-file", cfg, "--gpus", "2", "--steps", "4", "--warmup", "1", "--dshard"])
+    assert ds["scaling"] == "strong" and ds["config"]["parallelism"] == "dshard2"
+    assert ds["config"]["global_batch"] == 8 and ds["config"]["ok_fraction"] == 1.0
