@@ -164,7 +164,7 @@ def main():
             pipe.fetch(*toks[i % 2])
         elif stream is not None:
             inst, orc, vals = stream.batch(i)
-            eng.apply_updates(inst, orc, vals)
+            eng.apply_updates(inst, orc, vals, unique=True)   # the stream has distinct (instance, oracle)
             run_round()
         else:
             eng.touched.fill_(1)

@@ -73,8 +73,9 @@ bool in_range_cpu(const UpdateParams& p, int64_t u, int d) {
 
 void apply_updates_cpu(at::Tensor values, at::Tensor enabled, at::Tensor n_active, at::Tensor touched,
                        at::Tensor winner, const at::Tensor& inst, const at::Tensor& oracle, const at::Tensor& upd,
-                       bool constrained, at::Tensor upd_status) {
+                       bool constrained, at::Tensor upd_status, bool unique) {
   (void)winner;
+  (void)unique;  // sequential CPU loop: last writer wins either way
   UpdateParams p = make_update_params(values, enabled, n_active, touched, inst, oracle, upd, constrained, upd_status);
   const int64_t row_bytes = (int64_t)p.D * p.elem_bytes;
   for (int64_t u = 0; u < p.U; ++u) {  // sequential = last writer wins
@@ -108,8 +109,9 @@ void apply_updates_cpu(at::Tensor values, at::Tensor enabled, at::Tensor n_activ
 
 void apply_updates_hip(at::Tensor values, at::Tensor enabled, at::Tensor n_active, at::Tensor touched,
                        at::Tensor winner, const at::Tensor& inst, const at::Tensor& oracle, const at::Tensor& upd,
-                       bool constrained, at::Tensor upd_status) {
+                       bool constrained, at::Tensor upd_status, bool unique) {
   UpdateParams p = make_update_params(values, enabled, n_active, touched, inst, oracle, upd, constrained, upd_status);
+  p.unique = unique ? 1 : 0;
   TORCH_CHECK(winner.scalar_type() == at::kInt && winner.numel() == (int64_t)p.B * p.N && winner.is_contiguous(),
               "winner workspace: int32 [B, N] filled with -1");
   p.winner = winner.data_ptr<int32_t>();
@@ -123,7 +125,7 @@ void apply_updates_hip(at::Tensor values, at::Tensor enabled, at::Tensor n_activ
 void register_extra_defs(torch::Library& m) {
   m.def(
       "apply_updates(Tensor(a!) values, Tensor(b!) enabled, Tensor(c!) n_active, Tensor(d!) touched, "
-      "Tensor(e!) winner, Tensor inst, Tensor oracle, Tensor upd, bool constrained, Tensor(f!) upd_status) -> ()");
+      "Tensor(e!) winner, Tensor inst, Tensor oracle, Tensor upd, bool constrained, Tensor(f!) upd_status, bool unique=False) -> ()");
   register_governance_defs(m);
   register_generator_defs(m);
   register_io_defs(m);

@@ -74,6 +74,7 @@ struct UpdateParams {
   int elem_bytes;           // 2 (bf16), 4 (fp32) or 8 (int64 wsad)
   int dtype;                // 0 bf16, 1 fp32, 2 int64
   int constrained;
+  int unique;               // caller guarantees distinct (instance, oracle) pairs: one fused pass
 };
 
 }  // namespace svoc

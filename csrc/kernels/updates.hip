@@ -116,6 +116,67 @@ __global__ __launch_bounds__(256) void upd_apply_kernel(UpdateParams p) {
   }
 }
 
+// unique (instance, oracle) pairs (e.g. a synthetic stream, one bootstrap batch per window): no
+// last-writer resolution needed, so validation and the row copy run in one pass over the updates
+// (one read of the update rows instead of two)
+template <int L>
+__global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
+  const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
+  const int sub = threadIdx.x & (L - 1);
+  const bool in = u < p.U;
+  int st = ST_OK;
+  int64_t b = 0, o = 0;
+  if (in) {
+    b = p.inst[u];
+    o = p.oracle[u];
+    if (b < 0 || b >= p.B || o < 0 || o >= p.N) st = ST_NOT_ORACLE;
+  }
+  const int64_t row_bytes = (int64_t)p.D * p.elem_bytes;
+  const unsigned char* src = (const unsigned char*)p.upd + u * row_bytes;
+  bool ok = true, fin = true;
+  if (in && st == ST_OK) {
+    if (p.dtype == 0 && (row_bytes & 15) == 0 && (((uintptr_t)src) & 15) == 0) {
+      for (int64_t i = sub; i < row_bytes / 16; i += L) {
+        const uint4 v = ((const uint4*)src)[i];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (p.constrained) ok = ok && bf16_unit(w[k] & 0xffffu) && bf16_unit(w[k] >> 16);
+          else fin = fin && ((w[k] & 0x7f80u) != 0x7f80u) && ((w[k] & 0x7f800000u) != 0x7f800000u);
+        }
+      }
+    } else {
+      for (int d = sub; d < p.D; d += L) {
+        if (p.constrained) ok = ok && in_range(p, u, d);
+        else if (p.dtype != 2) fin = fin && finite_at(p, u, d);
+      }
+    }
+  }
+  ok = group_all<L>(ok);   // every lane reaches the ballots
+  fin = group_all<L>(fin);
+  if (!in) return;
+  if (st == ST_OK && !ok) st = ST_INTERVAL_INPUT;
+  if (st == ST_OK && !fin) st = ST_NON_FINITE;
+  if (sub == 0) p.upd_status[u] = st;
+  if (st != ST_OK) return;
+  // the row was just read by these lanes: the copy re-reads it from L2
+  unsigned char* dst = (unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes;
+  if (((uintptr_t)dst & 15) == 0 && ((uintptr_t)src & 15) == 0 && (row_bytes & 15) == 0) {
+    for (int64_t i = sub; i < row_bytes / 16; i += L) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+  } else if (((uintptr_t)dst & 3) == 0 && ((uintptr_t)src & 3) == 0 && (row_bytes & 3) == 0) {
+    for (int64_t i = sub; i < row_bytes / 4; i += L) ((uint32_t*)dst)[i] = ((const uint32_t*)src)[i];
+  } else {
+    for (int64_t i = sub; i < row_bytes; i += L) dst[i] = src[i];
+  }
+  if (sub == 0) {
+    if (!p.enabled[b * p.N + o]) {
+      p.enabled[b * p.N + o] = 1;
+      atomicAdd(&p.n_active[b], 1);
+    }
+    p.touched[b] = 1;
+  }
+}
+
 __global__ __launch_bounds__(256) void upd_reset_kernel(UpdateParams p) {
   const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= p.U || p.upd_status[u] != ST_OK) return;
@@ -125,6 +186,10 @@ __global__ __launch_bounds__(256) void upd_reset_kernel(UpdateParams p) {
 template <int L>
 static int launch_updates(const UpdateParams& p, hipStream_t stream) {
   const int64_t blocks = ((int64_t)p.U * L + 255) / 256;
+  if (p.unique) {
+    hipLaunchKernelGGL(upd_fused_unique_kernel<L>, dim3((unsigned)blocks), dim3(256), 0, stream, p);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(upd_validate_kernel<L>, dim3((unsigned)blocks), dim3(256), 0, stream, p);
   hipLaunchKernelGGL(upd_apply_kernel<L>, dim3((unsigned)blocks), dim3(256), 0, stream, p);
   hipLaunchKernelGGL(upd_reset_kernel, dim3((unsigned)((p.U + 255) / 256)), dim3(256), 0, stream, p);

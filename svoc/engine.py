@@ -100,8 +100,12 @@ class ConsensusEngine:
             return vals.to(self.device, torch.int64).contiguous()
         return vals.to(self.device, self.vdtype).contiguous()
 
-    def apply_updates(self, inst: torch.Tensor, oracle: torch.Tensor, vals: torch.Tensor) -> torch.Tensor:
-        """Store a batch of predictions (no consensus). Returns the per-update status [U] (device)."""
+    def apply_updates(self, inst: torch.Tensor, oracle: torch.Tensor, vals: torch.Tensor,
+                      unique: bool = False) -> torch.Tensor:
+        """Store a batch of predictions (no consensus). Returns the per-update status [U] (device).
+
+        ``unique=True``: the caller guarantees distinct (instance, oracle) pairs in the batch, so the GPU
+        validates and stores in one pass (no last-writer resolution)."""
         inst = torch.as_tensor(inst, dtype=torch.int64, device=self.device).contiguous()
         oracle = torch.as_tensor(oracle, dtype=torch.int64, device=self.device).contiguous()
         vals = self._as_storage(torch.as_tensor(vals))
@@ -109,7 +113,7 @@ class ConsensusEngine:
             raise ValueError(f"predictions must be [U, {self.D}]")
         st = torch.empty(inst.numel(), dtype=torch.int32, device=self.device)
         self._ops.apply_updates(self.values, self.enabled, self.n_active, self.touched, self._winner,
-                                inst, oracle, vals, self.cfg.constrained, st)
+                                inst, oracle, vals, self.cfg.constrained, st, bool(unique))
         return st
 
     # ------------------------------------------------------------------ rounds

@@ -54,6 +54,6 @@ class SentimentOraclePipeline:
         """One simulation fetch for every window + one consensus round per instance."""
         pred = self.oracles(self.classify(ids, mask))
         self.fetches += 1
-        st = self.engine.apply_updates(self._inst, self._orc, pred.view(-1, pred.shape[-1]))
+        st = self.engine.apply_updates(self._inst, self._orc, pred.view(-1, pred.shape[-1]), unique=True)
         self.engine.run_round()
         return st

@@ -215,3 +215,26 @@ def test_unconstrained_updates_reject_non_finite_gpu():
         st = e.apply_updates(torch.tensor([0, 0, 1, 1], device=DEV), torch.tensor([0, 1, 2, 3], device=DEV),
                              vals.to(DEV))
         assert st.cpu().tolist() == [Status.OK, Status.NON_FINITE, Status.NON_FINITE, Status.OK]
+
+
+@pytest.mark.parametrize("D,constrained", [(6, True), (4096, True), (100, False)])
+def test_unique_update_path_matches_general(D, constrained):
+    """apply_updates(unique=True) (one fused pass) == the last-writer path on distinct pairs."""
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    cfg = ConsensusConfig(n_oracles=16, dimension=D, n_failing_oracles=2, constrained=constrained,
+                          unconstrained_max_spread=5.0)
+    g = torch.Generator().manual_seed(D)
+    B, U = 40, 300
+    flat = torch.randperm(B * 16, generator=g)[:U]
+    inst, orc = flat // 16, flat % 16
+    vals = torch.rand(U, D, generator=g)
+    vals[3, 0] = 1.5                 # interval error (constrained) / fine (unconstrained)
+    vals[7, D - 1] = float("nan")    # rejected either way
+    outs = []
+    for unique in (False, True):
+        e = ConsensusEngine(cfg, B, device=DEV, mode="fast")
+        st = e.apply_updates(inst.to(DEV), orc.to(DEV), vals.to(DEV), unique=unique)
+        outs.append((st.cpu(), e.values.cpu(), e.enabled.cpu(), e.n_active.cpu(), e.touched.cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
