@@ -46,7 +46,7 @@ SVOC_DEV uint32_t from_key(u16x2 k) {
 }
 
 template <int NSEG, int WAVES, bool CONS, int MODE, bool RAW = false>
-__global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastParams p) {
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW ? 2 : 4))) void consensus_fast_reg_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // column pairs per wave
   constexpr int NPAD = 64 * NSEG;       // padded oracle rows
   constexpr int W = WAVES * P * 2;      // columns per workgroup step
@@ -109,8 +109,14 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
           r[i] = as_k((as_u32(to_key<CONS>(wraw[i])) & (lt_mask(i, nvl) | hi_m)) | hi_m);
         }
       } else if (N == NPAD) {  // uniform: no padding rows
+        if (CONS) {  // key and run polarity in one XOR: raw ^ (0x80008000 ^ pol)
+          const uint32_t kp = 0x80008000u ^ pol;
 #pragma unroll
-        for (int i = 0; i < 64; ++i) r[i] = to_key<CONS>(bload(rs, vo, i * rowb));
+          for (int i = 0; i < 64; ++i) r[i] = as_k(bload(rs, vo, i * rowb) ^ kp);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 64; ++i) r[i] = as_k(as_u32(to_key<CONS>(bload(rs, vo, i * rowb))) ^ pol);
+        }
       } else {
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
@@ -118,8 +124,10 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
           r[i] = as_k((as_u32(to_key<CONS>(bload(rs, vo, i * rowb))) & (lt_mask(i, nvl) | hi_m)) | hi_m);
         }
       }
+      if (RAW || N != NPAD) {
 #pragma unroll
-      for (int i = 0; i < 64; ++i) r[i] = as_k(as_u32(r[i]) ^ pol);
+        for (int i = 0; i < 64; ++i) r[i] = as_k(as_u32(r[i]) ^ pol);
+      }
       u16x2 klo, khi;
       median_group<NSEG>(r, klo, khi);
       const uint32_t lo = from_key<CONS>(klo), hi = from_key<CONS>(khi);
@@ -133,12 +141,21 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
     __builtin_amdgcn_sched_barrier(0);
     float part[64];
     const f32x2 c2 = {vA ? cA : 0.f, vB ? cB : 0.f};
+    if (RAW || (s + 1) * W > D) {  // slab with columns past D (uniform): masked words
 #pragma unroll
-    for (int i = 0; i < 64; ++i) {
-      const uint32_t w = RAW ? wraw[i] : bload(rs, vo, i * rowb) & mW;  // else: L2/MALL-hot re-read
-      const f32x2 y = bf16x2_to_f32x2(w) - c2;          // v_pk_add_f32
-      const f32x2 q = y * y;                              // v_pk_mul_f32
-      part[i] = q.x + q.y;
+      for (int i = 0; i < 64; ++i) {
+        const uint32_t w = RAW ? wraw[i] : bload(rs, vo, i * rowb) & mW;  // else: L2/MALL-hot re-read
+        const f32x2 y = bf16x2_to_f32x2(w) - c2;          // v_pk_add_f32
+        const f32x2 q = y * y;                              // v_pk_mul_f32
+        part[i] = q.x + q.y;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const f32x2 y = bf16x2_to_f32x2(bload(rs, vo, i * rowb)) - c2;
+        const f32x2 q = y * y;
+        part[i] = q.x + q.y;
+      }
     }
 #pragma unroll
     for (int h = 32, msk = P / 2; msk >= 1; h >>= 1, msk >>= 1) {
@@ -274,8 +291,11 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
     const int colA = s * W + 2 * cp;
     const bool vA = colA < D, vB = colA + 1 < D;
     const int vo = seg_off + (vA ? colA * 2 : 0);
-    uint64_t mm = mymask, ml = mylow;
-    asm volatile("" : "+v"(mm), "+v"(ml));
+    // sentinel bits with the run polarity folded in: row bit set -> key 0xFFFF (after ^pol), i.e.
+    // mlp = ~(lowmask ^ polarity): a low (-inf) row gives 0 ^ pol, a high (+inf) row ~0 ^ pol
+    uint64_t mm = mymask, mlp = ~(mylow ^ (pol ? ~0ull : 0ull));
+    asm volatile("" : "+v"(mm), "+v"(mlp));
+    const uint32_t kp2 = 0x80008000u ^ pol;
     // shifted power sums (shift = the first reliable row: no cancellation for clustered columns)
     const uint32_t w0 = bload(rs, vA ? colA * 2 : 0, first_rel * rowb);
     const f32x2 sh = {bf16_lo(w0), bf16_hi(w0)};
@@ -288,7 +308,9 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
       uint32_t w = wv[i];
       uint32_t mk = bit_mask(mm, i);
       // reliable rows keep their key; non-reliable rows become -inf (lowmask) / +inf sentinels
-      uint32_t key = CONS ? (as_u32(pos_to_key(w)) & mk) | ~(mk | bit_mask(ml, i)) : 0u;
+      // reliable rows: key ^ polarity; others: the -inf / +inf sentinel ^ polarity, read straight
+      // from the pre-combined mask mlp (v_bfi: 4 ops per row for key + sentinel + polarity)
+      uint32_t key = CONS ? ((w ^ kp2) & mk) | (bit_mask(mlp, i) & ~mk) : 0u;
       // row-ordered accumulation: keeps LLVM from front-loading all 64 rows (VGPRs)
       asm volatile("" : "+v"(w), "+v"(mk), "+v"(key), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
       if (CONS) wv[i] = key;
@@ -306,7 +328,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_reg_kernel(FastPara
     if (CONS) {
       u16x2 r[64];
 #pragma unroll
-      for (int i = 0; i < 64; ++i) r[i] = as_k(wv[i] ^ pol);
+      for (int i = 0; i < 64; ++i) r[i] = as_k(wv[i]);
       u16x2 klo, khi;
       median_group<NSEG>(r, klo, khi);
       const uint32_t lo = key_to_pos(klo), hi = key_to_pos(khi);
