@@ -1,5 +1,6 @@
-// Bit-exact (wsad, i128 arithmetic) consensus round on the GPU: one wave per instance, lane = oracle
-// row (RPL rows per lane for N > 64), loops over columns.  Every integer operation is the same
+// Bit-exact (wsad, i128 arithmetic) consensus round on the GPU: one group of GS lanes per instance
+// (a whole wave, or 8/16/32 lanes so small instances share a wave), lane = oracle row (RPL rows per
+// lane for N > 64), loops over columns.  Every integer operation is the same
 // csrc/include/svoc/wsad.hpp routine the CPU golden engine uses, evaluated in the same stage order
 // (all c1, qr, rel1, rank mask, all consensus, rel2, all means, all variances, all skewness, all
 // kurtosis -- contract/src/contract.cairo:451-500), so the outputs and the first-error status match
@@ -26,26 +27,42 @@ __device__ __forceinline__ i128 shfl128(i128 v, int src) {
   return (i128)(((u128)hi << 64) | lo);
 }
 
-// wave-wide checked i128 sum.  The contract adds in row order and reverts on any i128 overflow of
-// a partial sum; when every term is below 2^118 in magnitude no partial sum of <= 256 terms can
-// overflow in ANY order, so a butterfly (6 exchanges) gives the identical integer.  Otherwise the
-// sum runs sequentially in lane order (0..63), as the CPU engine, for exact overflow detection.
-__device__ __forceinline__ i128 wave_sum(i128 v, int& st) {
-  const i128 lim = (i128)1 << 118;
-  if (__all(v < lim && v > -lim)) {
+// A group of GS lanes = one instance (GS = 64: one instance per wave; GS = 8/16/32: 64/GS instances
+// share a wave).  One wave per workgroup, so __syncthreads never waits on another wave and groups
+// may leave the column loops at different iterations.
+template <int GS>
+struct Grp {
+  int lane, gl, base;
+  uint64_t mask;
+  __device__ Grp() {
+    lane = threadIdx.x;
+    gl = lane % GS;
+    base = lane - gl;
+    mask = GS == 64 ? ~0ull : (((1ull << GS) - 1ull) << base);
+  }
+  __device__ bool all(bool v) const { return (__ballot(!v) & mask) == 0; }
+  __device__ int count(bool v) const { return __popcll(__ballot(v) & mask); }
+  __device__ int any_or(int v) const {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += shfl128(v, threadIdx.x ^ o);
+    for (int o = GS / 2; o >= 1; o >>= 1) v |= __shfl_xor(v, o);
     return v;
   }
-  i128 acc = 0;
-  for (int l = 0; l < 64; ++l) acc = add(acc, shfl128(v, l), st);
-  return acc;
-}
-
-__device__ __forceinline__ int wave_or(int v) {
-  for (int o = 32; o >= 1; o >>= 1) v |= __shfl_xor(v, o);
-  return v;
-}
+  // checked i128 sum over the group.  The contract adds in row order and reverts on any i128
+  // overflow of a partial sum; when every term is below 2^118 in magnitude no partial sum of <= 256
+  // terms can overflow in ANY order, so a butterfly gives the identical integer.  Otherwise the sum
+  // runs sequentially in lane order, as the CPU engine, for exact overflow detection.
+  __device__ i128 sum(i128 v, int& st) const {
+    const i128 lim = (i128)1 << 118;
+    if (all(v < lim && v > -lim)) {
+#pragma unroll
+      for (int o = GS / 2; o >= 1; o >>= 1) v += shfl128(v, lane ^ o);
+      return v;
+    }
+    i128 acc = 0;
+    for (int l = 0; l < GS; ++l) acc = add(acc, shfl128(v, base + l), st);
+    return acc;
+  }
+};
 
 template <int RPL>
 struct Rows {
@@ -53,22 +70,22 @@ struct Rows {
   bool on[RPL];  // row exists and takes part
 };
 
-// Column scratch in LDS: the wave's rows are published once, then every lane ranks its own rows
-// against them with broadcast LDS reads (one ds_read_b64 per row instead of three cross-lane
-// shuffles), both middle ranks in the same pass.
+// Column scratch in LDS (one per group): the group's rows are published once, then every lane ranks
+// its own rows against them with broadcast LDS reads, both middle ranks in the same pass.
+template <int NR>
 struct ColScratch {
-  int64_t x[256];
-  uint8_t on[256];
+  int64_t x[NR];
+  uint8_t on[NR];
   int64_t pick[2];
 };
 
 // stable ranks mid-1 and mid among the rows with on[] set (math.cairo:113-126 via MergeSort)
-template <int RPL>
-__device__ void middle_values(const Rows<RPL>& r, int lane, int n_rows, int mid, ColScratch& cs, i128& a,
-                              i128& b) {
+template <int RPL, int GS>
+__device__ void middle_values(const Rows<RPL>& r, const Grp<GS>& g, int n_rows, int mid, ColScratch<RPL * GS>& cs,
+                              i128& a, i128& b) {
 #pragma unroll
   for (int j = 0; j < RPL; ++j) {
-    const int row = j * 64 + lane;
+    const int row = j * GS + g.gl;
     if (row < n_rows) {
       cs.x[row] = r.x[j];
       cs.on[row] = r.on[j] ? 1 : 0;
@@ -77,7 +94,7 @@ __device__ void middle_values(const Rows<RPL>& r, int lane, int n_rows, int mid,
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < RPL; ++j) {
-    const int me = j * 64 + lane;
+    const int me = j * GS + g.gl;
     if (me < n_rows && r.on[j]) {
       const int64_t xm = r.x[j];
       int rank = 0;
@@ -95,25 +112,30 @@ __device__ void middle_values(const Rows<RPL>& r, int lane, int n_rows, int mid,
   __syncthreads();  // the scratch is reused by the next column
 }
 
-template <int RPL>
-__device__ i128 smooth_median_w(const Rows<RPL>& r, int lane, int n_rows, int count, ColScratch& cs, int& st) {
+template <int RPL, int GS>
+__device__ i128 smooth_median_w(const Rows<RPL>& r, const Grp<GS>& g, int n_rows, int count,
+                                ColScratch<RPL * GS>& cs, int& st) {
   if (count == 0) { fail(st, ST_USIZE_UNDERFLOW); return 0; }
   if (count == 1) { fail(st, ST_INDEX_OOB); return 0; }
   i128 a, b;
-  middle_values<RPL>(r, lane, n_rows, count / 2, cs, a, b);
+  middle_values<RPL, GS>(r, g, n_rows, count / 2, cs, a, b);
   return idiv_pos64(add(a, b, st), 2, st);
 }
 
-template <int RPL>
+template <int RPL, int GS>
 __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
+  constexpr int IPW = 64 / GS;  // instances per wave (= per workgroup)
   extern __shared__ __attribute__((aligned(16))) int64_t lds[];
-  __shared__ ColScratch cs;
-  const int b = blockIdx.x;
-  if (p.active && !p.active[b]) return;
-  const int lane = threadIdx.x;
+  __shared__ ColScratch<RPL * GS> css[IPW];
+  const Grp<GS> g;
+  const int gi = threadIdx.x / GS;
+  const int b = blockIdx.x * IPW + gi;
+  if (b >= p.B || (p.active && !p.active[b])) return;
+  const int gl = g.gl;
+  ColScratch<RPL * GS>& cs = css[gi];
   const int N = p.N, D = p.D;
   // per-column intermediates: LDS, or a [B, 6, D] global workspace when 6*D int64 exceed the LDS
-  int64_t* const ws = p.work ? p.work + (int64_t)b * 6 * D : lds;
+  int64_t* const ws = p.work ? p.work + (int64_t)b * 6 * D : lds + (int64_t)gi * 6 * D;
   int64_t* c1 = ws;
   int64_t* cons = ws + D;
   int64_t* means = ws + 2 * D;
@@ -121,104 +143,103 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
   int64_t* sk = ws + 4 * D;
   int64_t* ku = ws + 5 * D;
   const int64_t* X = p.values + (int64_t)b * N * D;
-  int st = ST_OK;  // wave-uniform by construction (every lane runs the same checked reductions)
+  int st = ST_OK;  // group-uniform by construction (every lane runs the same checked reductions)
 
   Rows<RPL> rows;
   // ---- pass 1: c1 per column
   for (int d = 0; d < D && st == ST_OK; ++d) {
 #pragma unroll
     for (int j = 0; j < RPL; ++j) {
-      const int row = j * 64 + lane;
+      const int row = j * GS + gl;
       rows.on[j] = row < N;
       rows.x[j] = row < N ? X[(int64_t)row * D + d] : 0;
     }
-    const i128 c = smooth_median_w<RPL>(rows, lane, N, N, cs, st);
-    if (lane == 0) c1[d] = (int64_t)c;
+    const i128 c = smooth_median_w<RPL, GS>(rows, g, N, N, cs, st);
+    if (gl == 0) c1[d] = (int64_t)c;
   }
   __syncthreads();
-  if (st != ST_OK) { if (lane == 0) p.status[b] = st; return; }
+  if (st != ST_OK) { if (gl == 0) p.status[b] = st; return; }
   // quadratic risk per row (lane-local), then the checked mean
   i128 qr[RPL];
   int lst = ST_OK;
 #pragma unroll
   for (int j = 0; j < RPL; ++j) {
-    const int row = j * 64 + lane;
+    const int row = j * GS + gl;
     i128 acc = 0;
     if (row < N)
       for (int d = 0; d < D; ++d) acc = add(acc, qdev(X[(int64_t)row * D + d], c1[d], lst), lst);
     qr[j] = acc;
   }
-  // any lane's overflow reverts (first error in row order = the smallest failing code is not
-  // needed: qr can only fail with OVERFLOW)
-  if (wave_or(lst != ST_OK)) st = ST_OVERFLOW;
+  // any lane's overflow reverts (qr can only fail with OVERFLOW)
+  if (g.any_or(lst != ST_OK)) st = ST_OVERFLOW;
   i128 sum_qr = 0;
 #pragma unroll
-  for (int j = 0; j < RPL; ++j) sum_qr = add(sum_qr, wave_sum(qr[j], st), st);
+  for (int j = 0; j < RPL; ++j) sum_qr = add(sum_qr, g.sum(qr[j], st), st);
   const i128 mean_qr = idiv(sum_qr, (i128)N, st);
   const int64_t rdim = p.legacy ? 1 : D;  // obsolete contracts: no /D (contract_nd.cairo:418)
   const i128 rel1 = p.constrained ? constrained_reliability(mean_qr, rdim, st)
                                   : unconstrained_reliability(wsqrt(mean_qr, st), p.max_spread, st);
   if (st == ST_OK && !in_unit_interval(rel1)) st = ST_RELIABILITY_INTERVAL;
   if (st == ST_OK && p.n_failing > N) st = ST_USIZE_UNDERFLOW;
-  if (st != ST_OK) { if (lane == 0) p.status[b] = st; return; }
+  if (st != ST_OK) { if (gl == 0) p.status[b] = st; return; }
   // rank mask: (qr asc, idx desc) (sort.cairo:96-101)
   const int threshold = N - p.n_failing;
   bool rel[RPL];
 #pragma unroll
   for (int j = 0; j < RPL; ++j) {
-    const int me = j * 64 + lane;
+    const int me = j * GS + gl;
     int rank = 0;
 #pragma unroll
     for (int jj = 0; jj < RPL; ++jj)
-      for (int l = 0; l < 64; ++l) {
-        const int k = jj * 64 + l;
-        const i128 qk = shfl128(qr[jj], l);
+      for (int l = 0; l < GS; ++l) {
+        const int k = jj * GS + l;
+        const i128 qk = shfl128(qr[jj], g.base + l);
         if (k < N) rank += (qk < qr[j] || (qk == qr[j] && k > me)) ? 1 : 0;
       }
     rel[j] = me < N && rank < threshold;
   }
   int R = 0;
 #pragma unroll
-  for (int j = 0; j < RPL; ++j) R += __popcll(__ballot(rel[j]));
+  for (int j = 0; j < RPL; ++j) R += g.count(rel[j]);
   // ---- pass 2: consensus per column over the reliable rows
   for (int d = 0; d < D && st == ST_OK; ++d) {
 #pragma unroll
     for (int j = 0; j < RPL; ++j) {
-      const int row = j * 64 + lane;
+      const int row = j * GS + gl;
       rows.on[j] = rel[j];
       rows.x[j] = row < N ? X[(int64_t)row * D + d] : 0;
     }
     i128 c;
     if (p.constrained) {
-      c = smooth_median_w<RPL>(rows, lane, N, R, cs, st);
+      c = smooth_median_w<RPL, GS>(rows, g, N, R, cs, st);
     } else {
       i128 s = 0;
 #pragma unroll
-      for (int j = 0; j < RPL; ++j) s = add(s, wave_sum(rows.on[j] ? (i128)rows.x[j] : 0, st), st);
+      for (int j = 0; j < RPL; ++j) s = add(s, g.sum(rows.on[j] ? (i128)rows.x[j] : 0, st), st);
       c = idiv(s, (i128)R, st);
     }
-    if (lane == 0) cons[d] = (int64_t)c;
+    if (gl == 0) cons[d] = (int64_t)c;
   }
   i128 s2 = 0;
 #pragma unroll
-  for (int j = 0; j < RPL; ++j) s2 = add(s2, wave_sum(rel[j] ? qr[j] : 0, st), st);
+  for (int j = 0; j < RPL; ++j) s2 = add(s2, g.sum(rel[j] ? qr[j] : 0, st), st);
   const i128 mean_qr2 = idiv(s2, (i128)R, st);
   const i128 rel2 = p.constrained ? constrained_reliability(mean_qr2, rdim, st)
                                   : unconstrained_reliability(wsqrt(mean_qr2, st), p.max_spread, st);
   if (st == ST_OK && !in_unit_interval(rel2)) st = ST_RELIABILITY_INTERVAL;
   if (p.legacy) {  // obsolete contracts store no moments
-    for (int d = lane; d < D; d += 64) sk[d] = ku[d] = 0;
+    for (int d = gl; d < D; d += GS) sk[d] = ku[d] = 0;
   }
   // ---- moments (math.cairo:208-222, 320-398), stage by stage like the CPU engine
   for (int d = 0; d < D && st == ST_OK && !p.legacy; ++d) {
     i128 s = 0;
 #pragma unroll
     for (int j = 0; j < RPL; ++j) {
-      const int row = j * 64 + lane;
-      s = add(s, wave_sum(rel[j] ? (i128)X[(int64_t)row * D + d] : 0, st), st);
+      const int row = j * GS + gl;
+      s = add(s, g.sum(rel[j] ? (i128)X[(int64_t)row * D + d] : 0, st), st);
     }
     const i128 mu = idiv(s, (i128)R, st);
-    if (lane == 0) means[d] = (int64_t)mu;
+    if (gl == 0) means[d] = (int64_t)mu;
   }
   __syncthreads();
   for (int d = 0; d < D && st == ST_OK && !p.legacy; ++d) {
@@ -226,13 +247,13 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
     int l2 = ST_OK;
 #pragma unroll
     for (int j = 0; j < RPL; ++j) {
-      const int row = j * 64 + lane;
+      const int row = j * GS + gl;
       const i128 q = rel[j] ? qdev(X[(int64_t)row * D + d], means[d], l2) : 0;
-      if (wave_or(l2 != ST_OK)) fail(st, ST_OVERFLOW);
-      s = add(s, wave_sum(q, st), st);
+      if (g.any_or(l2 != ST_OK)) fail(st, ST_OVERFLOW);
+      s = add(s, g.sum(q, st), st);
     }
     const i128 v = idiv(s, (i128)R, st);
-    if (lane == 0) vars[d] = (int64_t)v;
+    if (gl == 0) vars[d] = (int64_t)v;
   }
   __syncthreads();
   for (int pass = 0; pass < 2 && !p.legacy; ++pass) {  // 0: skewness for all d, 1: kurtosis for all d
@@ -242,7 +263,7 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
       int l2 = ST_OK;
 #pragma unroll
       for (int j = 0; j < RPL; ++j) {
-        const int row = j * 64 + lane;
+        const int row = j * GS + gl;
         i128 t = 0;
         if (rel[j] && st == ST_OK) {
           const i128 z = wdiv(sub(X[(int64_t)row * D + d], means[d], l2), sd, l2);
@@ -250,21 +271,20 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
           t = pass == 0 ? wmul(z2, z, l2) : wmul(z2, z2, l2);
         }
         // first error in row order, as the CPU loop: smallest failing row's code wins
-        int code = l2;
-        for (int l = 0; l < 64; ++l) {
-          const int c = __shfl(code, l);
+        for (int l = 0; l < GS; ++l) {
+          const int c = __shfl(l2, g.base + l);
           if (c != ST_OK) { fail(st, c); break; }
         }
-        s = add(s, wave_sum(t, st), st);
+        s = add(s, g.sum(t, st), st);
       }
       const i128 out = pass == 0 ? skew_from_sum(s, R, st) : kurt_from_sum(s, R, st);
-      if (lane == 0) (pass == 0 ? sk : ku)[d] = (int64_t)out;
+      if (gl == 0) (pass == 0 ? sk : ku)[d] = (int64_t)out;
     }
   }
   __syncthreads();
-  if (st != ST_OK) { if (lane == 0) p.status[b] = st; return; }
+  if (st != ST_OK) { if (gl == 0) p.status[b] = st; return; }
   // ---- commit
-  for (int d = lane; d < D; d += 64) {
+  for (int d = gl; d < D; d += GS) {
     const int64_t o = (int64_t)b * D + d;
     p.consensus[o] = cons[d];
     p.skew[o] = sk[d];
@@ -273,31 +293,46 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
   }
 #pragma unroll
   for (int j = 0; j < RPL; ++j) {
-    const int row = j * 64 + lane;
+    const int row = j * GS + gl;
     if (row < N) {
       p.reliable[(int64_t)b * N + row] = rel[j] ? 1 : 0;
       p.qr[(int64_t)b * N + row] = (int64_t)qr[j];
     }
   }
-  if (lane == 0) {
+  if (gl == 0) {
     p.rel[2 * (int64_t)b] = (int64_t)rel1;
     p.rel[2 * (int64_t)b + 1] = (int64_t)rel2;
     p.status[b] = ST_OK;
   }
 }
 
+template <int RPL, int GS>
+static int launch_exact(const ExactParams& p, hipStream_t stream) {
+  constexpr int IPW = 64 / GS;
+  const size_t lds = p.work ? 0 : (size_t)IPW * p.D * 6 * sizeof(int64_t);
+  if (lds > 64 * 1024) return -2;  // the binding passes a global workspace for wide instances
+  auto k = consensus_exact_kernel<RPL, GS>;
+  hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(k, dim3((unsigned)((p.B + IPW - 1) / IPW)), dim3(64), lds, stream, p);
+  return (int)hipGetLastError();
+}
+
 }  // namespace svoc
 
 using namespace svoc;
 
+// Lane group per instance: the smallest of 8 / 16 / 32 lanes holding one row each (several
+// instances per wave, e.g. the deployed 7 x 6 config runs 8 per wave), else a full wave with 1 or 4
+// rows per lane.  Wide instances (6*D int64 > LDS budget) use the HBM workspace and a full wave.
 extern "C" int svoc_exact_round(const ExactParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
   if (p->N < 1 || p->N > 256 || p->D < 1) return -1;
-  const size_t lds = p->work ? 0 : (size_t)p->D * 6 * sizeof(int64_t);
-  if (lds > 64 * 1024) return -2;  // the binding passes a global workspace for wide instances
-  auto k = p->N <= 64 ? consensus_exact_kernel<1> : consensus_exact_kernel<4>;
-  hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(k, dim3(p->B), dim3(64), lds, stream, *p);
-  return (int)hipGetLastError();
+  const size_t per_inst = (size_t)p->D * 6 * sizeof(int64_t);
+  if (!p->work) {
+    if (p->N <= 8 && 8 * per_inst <= 64 * 1024) return launch_exact<1, 8>(*p, stream);
+    if (p->N <= 16 && 4 * per_inst <= 64 * 1024) return launch_exact<1, 16>(*p, stream);
+    if (p->N <= 32 && 2 * per_inst <= 64 * 1024) return launch_exact<1, 32>(*p, stream);
+  }
+  return p->N <= 64 ? launch_exact<1, 64>(*p, stream) : launch_exact<4, 64>(*p, stream);
 }
