@@ -12,6 +12,8 @@
 
 namespace svoc {
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ bool in_range(const UpdateParams& p, int64_t u, int d) {
   if (p.dtype == 0) {
     const uint16_t raw = ((const uint16_t*)p.upd)[u * p.D + d];
@@ -43,7 +45,7 @@ template <int L>
 __device__ __forceinline__ bool group_all(bool ok) {
   const uint64_t bad = __ballot(!ok);
   const int lane = threadIdx.x & 63;
-  const uint64_t gm = (L == 64) ? ~0ull : (((1ull << L) - 1ull) << (lane & ~(L - 1)));
+  const uint64_t gm = (L == 64) ? ~0ull : (((1ull << (L & 63)) - 1ull) << (lane & ~(L - 1)));
   return (bad & gm) == 0;
 }
 
@@ -133,40 +135,80 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
   }
   const int64_t row_bytes = (int64_t)p.D * p.elem_bytes;
   const unsigned char* src = (const unsigned char*)p.upd + u * row_bytes;
-  bool ok = true, fin = true;
-  if (in && st == ST_OK) {
-    if (p.dtype == 0 && (row_bytes & 15) == 0 && (((uintptr_t)src) & 15) == 0) {
-      for (int64_t i = sub; i < row_bytes / 16; i += L) {
-        const uint4 v = ((const uint4*)src)[i];
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  unsigned char* dst = (unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes;
+  const bool vec = (row_bytes & 15) == 0 && (((uintptr_t)src) & 15) == 0 && (((uintptr_t)dst) & 15) == 0;
+  // bf16 rows of <= RB*L 16-B chunks (c3: 8 KiB rows, 8 chunks per lane): every chunk is loaded
+  // once into registers (all loads in flight together, non-temporal: the update batch is read
+  // once), validated there and stored from there, so the row is never re-read
+  constexpr int RB = 8;
+  const int64_t nch = row_bytes / 16;
+  if (p.dtype == 0 && vec && nch <= (int64_t)RB * L) {  // uniform over the launch
+    uint4 v[RB];
+    bool ok = true, fin = true;
+    const bool live = in && st == ST_OK;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (p.constrained) ok = ok && bf16_unit(w[k] & 0xffffu) && bf16_unit(w[k] >> 16);
-          else fin = fin && ((w[k] & 0x7f80u) != 0x7f80u) && ((w[k] & 0x7f800000u) != 0x7f800000u);
-        }
-      }
-    } else {
-      for (int d = sub; d < p.D; d += L) {
-        if (p.constrained) ok = ok && in_range(p, u, d);
-        else if (p.dtype != 2) fin = fin && finite_at(p, u, d);
+    for (int k = 0; k < RB; ++k) {
+      const int64_t i = sub + (int64_t)k * L;
+      u32x4 t = {0u, 0u, 0u, 0u};
+      if (live && i < nch) t = __builtin_nontemporal_load((const u32x4*)src + i);
+      v[k] = uint4{t.x, t.y, t.z, t.w};
+    }
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (p.constrained) ok = ok && bf16_unit(w[j] & 0xffffu) && bf16_unit(w[j] >> 16);
+        else fin = fin && ((w[j] & 0x7f80u) != 0x7f80u) && ((w[j] & 0x7f800000u) != 0x7f800000u);
       }
     }
-  }
-  ok = group_all<L>(ok);   // every lane reaches the ballots
-  fin = group_all<L>(fin);
-  if (!in) return;
-  if (st == ST_OK && !ok) st = ST_INTERVAL_INPUT;
-  if (st == ST_OK && !fin) st = ST_NON_FINITE;
-  if (sub == 0) p.upd_status[u] = st;
-  if (st != ST_OK) return;
-  // the row was just read by these lanes: the copy re-reads it from L2
-  unsigned char* dst = (unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes;
-  if (((uintptr_t)dst & 15) == 0 && ((uintptr_t)src & 15) == 0 && (row_bytes & 15) == 0) {
-    for (int64_t i = sub; i < row_bytes / 16; i += L) ((uint4*)dst)[i] = ((const uint4*)src)[i];
-  } else if (((uintptr_t)dst & 3) == 0 && ((uintptr_t)src & 3) == 0 && (row_bytes & 3) == 0) {
-    for (int64_t i = sub; i < row_bytes / 4; i += L) ((uint32_t*)dst)[i] = ((const uint32_t*)src)[i];
+    ok = group_all<L>(ok);
+    fin = group_all<L>(fin);
+    if (!in) return;
+    if (st == ST_OK && !ok) st = ST_INTERVAL_INPUT;
+    if (st == ST_OK && !fin) st = ST_NON_FINITE;
+    if (sub == 0) p.upd_status[u] = st;
+    if (st != ST_OK) return;
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const int64_t i = sub + (int64_t)k * L;
+      if (i < nch) ((uint4*)dst)[i] = v[k];
+    }
   } else {
-    for (int64_t i = sub; i < row_bytes; i += L) dst[i] = src[i];
+    bool ok = true, fin = true;
+    if (in && st == ST_OK) {
+      if (p.dtype == 0 && vec) {
+        for (int64_t i = sub; i < nch; i += L) {
+          const uint4 v = ((const uint4*)src)[i];
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (p.constrained) ok = ok && bf16_unit(w[k] & 0xffffu) && bf16_unit(w[k] >> 16);
+            else fin = fin && ((w[k] & 0x7f80u) != 0x7f80u) && ((w[k] & 0x7f800000u) != 0x7f800000u);
+          }
+        }
+      } else {
+        for (int d = sub; d < p.D; d += L) {
+          if (p.constrained) ok = ok && in_range(p, u, d);
+          else if (p.dtype != 2) fin = fin && finite_at(p, u, d);
+        }
+      }
+    }
+    ok = group_all<L>(ok);   // every lane reaches the ballots
+    fin = group_all<L>(fin);
+    if (!in) return;
+    if (st == ST_OK && !ok) st = ST_INTERVAL_INPUT;
+    if (st == ST_OK && !fin) st = ST_NON_FINITE;
+    if (sub == 0) p.upd_status[u] = st;
+    if (st != ST_OK) return;
+    // the row was just read by these lanes: the copy re-reads it from L2
+    if (vec) {
+      for (int64_t i = sub; i < nch; i += L) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    } else if (((uintptr_t)dst & 3) == 0 && ((uintptr_t)src & 3) == 0 && (row_bytes & 3) == 0) {
+      for (int64_t i = sub; i < row_bytes / 4; i += L) ((uint32_t*)dst)[i] = ((const uint32_t*)src)[i];
+    } else {
+      for (int64_t i = sub; i < row_bytes; i += L) dst[i] = src[i];
+    }
   }
   if (sub == 0) {
     if (!p.enabled[b * p.N + o]) {
