@@ -2,6 +2,7 @@
 // CUDA (= HIP on ROCm) kernels = the hand-written gfx950 kernels in csrc/kernels/*.hip.
 // All ops write into caller-provided outputs ("out" semantics) so the Python engine owns the state
 // tensors and can capture steady-state steps in HIP graphs.
+#include <cstdlib>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
@@ -61,8 +62,10 @@ void fast_round_checks(const at::Tensor& values, int64_t D, const at::Tensor& c1
 void fast_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t D,
                     int64_t n_failing, bool constrained, double max_spread, at::Tensor c1, at::Tensor cons,
                     at::Tensor skew, at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable,
-                    at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim, bool legacy) {
+                    at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim, bool legacy,
+                    const c10::optional<at::Tensor>& work) {
   (void)wave_hint;
+  (void)work;
   fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
   const int64_t B = values.size(0), N = values.size(1), ld = values.size(2), is = values.stride(0);
   TORCH_CHECK(values.scalar_type() == at::kBFloat16 || values.scalar_type() == at::kFloat,
@@ -106,7 +109,8 @@ void fast_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& a
 void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t D,
                     int64_t n_failing, bool constrained, double max_spread, at::Tensor c1, at::Tensor cons,
                     at::Tensor skew, at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable,
-                    at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim, bool legacy) {
+                    at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim, bool legacy,
+                    const c10::optional<at::Tensor>& work) {
   fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
   TORCH_CHECK(values.scalar_type() == at::kBFloat16, "GPU fast path stores values in bf16");
   const int64_t B = values.size(0), N = values.size(1), ld = values.size(2);
@@ -135,6 +139,26 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
   p.qr = qr.data_ptr<float>();
   p.reliable = reliable.data_ptr<uint8_t>();
   p.status = status.data_ptr<int32_t>();
+  // window-kernel workspace: the caller's (it must persist between mode 1 and mode 2 of a
+  // D-sharded round), else a temporary one for a full round
+  at::Tensor wtmp;
+  const int64_t words = fast_work_words(D);
+  if (work.has_value() && work->defined()) {
+    TORCH_CHECK(work->is_contiguous() && work->element_size() == 4 && work->device() == values.device(),
+                "work: contiguous 4-byte elements on the values' device");
+    TORCH_CHECK(work->numel() >= fast_work_numel(B, D), "work: needs ", fast_work_numel(B, D),
+                " elements (svoc.ops.fast_work_numel)");
+    p.work = (uint32_t*)work->data_ptr();
+  } else if (mode == 0 && (N > 16 || D > 128) && n_failing <= 32) {
+    wtmp = at::empty({fast_work_numel(B, D)}, values.options().dtype(at::kInt));
+    p.work = (uint32_t*)wtmp.data_ptr();
+  }
+  {
+    const char* wc = std::getenv("SVOC_WIN_CANCEL");   // tests / experiments: force or avoid the cleanup
+    p.win_cancel = wc ? (float)std::atof(wc) : 64.f;
+  }
+  p.work_pairs = (int)fast_work_pairs(D);
+  p.work_stride = words;
   auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
   const int rc = svoc_fast_round_bf16(&p, stream);
   TORCH_CHECK(rc == 0, "svoc_fast_round_bf16 launch failed: ", rc);
@@ -221,7 +245,8 @@ TORCH_LIBRARY(svoc, m) {
   m.def(
       "fast_round(Tensor values, Tensor? active, int D, int n_failing, bool constrained, float max_spread, "
       "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "
-      "Tensor(g!) reliable, Tensor(h!) status, int wave_hint=0, int mode=0, int rel_dim=0, bool legacy=False) -> ()");
+      "Tensor(g!) reliable, Tensor(h!) status, int wave_hint=0, int mode=0, int rel_dim=0, bool legacy=False, "
+      "Tensor? work=None) -> ()");
   m.def(
       "exact_round(Tensor values, Tensor? active, int n_failing, bool constrained, int max_spread, "
       "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "

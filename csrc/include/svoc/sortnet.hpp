@@ -69,6 +69,23 @@ SVOC_DEV uint32_t bit_mask(uint64_t m, int i) {  // bit i set
 }
 
 SVOC_DEV u16x2 shfl_xor_k(u16x2 v, int m) { return as_k((uint32_t)__shfl_xor((int)as_u32(v), m)); }
+
+// Value of lane ^ M (compile-time M) without __shfl_xor's per-call lane-index arithmetic:
+// DPP quad_perm for M = 1, 2 (VALU, foldable into the consumer), ds_swizzle xor-mode for 4..16,
+// v_permlane32_swap for 32.
+template <int M>
+SVOC_DEV uint32_t xor_lane_u32(uint32_t v) {
+  static_assert(M == 1 || M == 2 || M == 4 || M == 8 || M == 16 || M == 32, "xor distance");
+  if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);
+  else if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);
+  else if constexpr (M <= 16) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (M << 10));
+  else {
+    const auto t = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return (__lane_id() & 32) ? t[0] : t[1];
+  }
+}
+template <int M>
+SVOC_DEV float xor_lane(float v) { return __builtin_bit_cast(float, xor_lane_u32<M>(__builtin_bit_cast(uint32_t, v))); }
 SVOC_DEV u16x2 shfl_k(u16x2 v, int src) { return as_k((uint32_t)__shfl((int)as_u32(v), src)); }
 
 // Full ascending bitonic sort of the 64 registers of one lane (each half independently).
@@ -339,6 +356,108 @@ SVOC_DEV void median_group(u16x2 (&r)[64], u16x2& lo, u16x2& hi) {
     }
     lo = mx;
     hi = mn;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Order-statistic windows (consensus_fast_win.hip).  Pass 2's smooth median over the reliable rows
+// is an order statistic of the FULL column shifted by at most f ranks, so pass 1 keeps the H keys on
+// either side of the median instead of just the middle pair, and pass 2 only ranks the f removed
+// keys against that window (no second sorting network over N rows).
+
+// Half-cleaner between lanes l and l ^ XM with XOR hooks: `iy` is XORed into the upper lane's keys
+// on the way in (~0 when the upper lane is in the opposite polarity), `ox` / `oy` into the minima /
+// maxima on the way out (the output polarity of the lower / upper lane).  xhc_swap<XM> is
+// xhc_pol<XM>(r, ~0u, 0, 0).
+template <int XM>
+SVOC_DEV void xhc_pol(u16x2 (&r)[64], uint32_t iy, uint32_t ox, uint32_t oy) {
+#pragma unroll
+  for (int k = 0; k < 32; ++k) {
+    uint32_t x = as_u32(r[2 * k]), y = as_u32(r[2 * k + 1]);
+    xswap<XM>(x, y);
+    y ^= iy;
+    const u16x2 lo = kmin(as_k(x), as_k(y)), hi = kmax(as_k(x), as_k(y));
+    x = as_u32(lo) ^ ox;
+    y = as_u32(hi) ^ oy;
+    xswap<XM>(x, y);
+    r[2 * k] = as_k(x);
+    r[2 * k + 1] = as_k(y);
+  }
+}
+
+// The top H = 2^k + 1 keys of a bitonic in-lane sequence of 64, ascending: out[0] is the H-th
+// largest, out[H-1] the maximum.  Max-only half-cleaners down to 2K = 2(H-1) keys, one split into
+// the top K (sorted by a half-cleaner cascade) and the rest (whose maximum is the H-th largest).
+template <int H>
+SVOC_DEV void bitonic_top(const u16x2 (&r)[64], u16x2 (&out)[H]) {
+  constexpr int K = H - 1;
+  static_assert(K >= 2 && K <= 32 && (K & (K - 1)) == 0, "H = 2^k + 1, at most 33");
+  u16x2 t[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) t[i] = r[i];
+#pragma unroll
+  for (int n = 64; n > 2 * K; n >>= 1) {
+#pragma unroll
+    for (int i = 0; i < n / 2; ++i) t[i] = kmax(t[i], t[i + n / 2]);
+  }
+  u16x2 mx = kmin(t[0], t[K]);
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const u16x2 a = t[i], b = t[i + K];
+    if (i) mx = kmax(mx, kmin(a, b));
+    t[i] = kmax(a, b);
+  }
+#pragma unroll
+  for (int j = K / 2; j > 0; j >>= 1) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+      const int l = i ^ j;
+      if (l > i) {
+        const u16x2 a = t[i], b = t[l];
+        t[i] = kmin(a, b);
+        t[l] = kmax(a, b);
+      }
+    }
+  }
+  out[0] = mx;
+#pragma unroll
+  for (int i = 0; i < K; ++i) out[i + 1] = t[i];
+}
+
+// Sorted-position window around the middle of the group's 64*NSEG keys (r holds keys XOR
+// group_polarity<NSEG>(seg), sentinel-split as for median_group).  With c = NPAD/2:
+//   part 0 ("lower"): w0[m] = key at sorted position c - H + m      (ascending, true keys)
+//   part 1 ("upper"): w1[m] = ~(key at sorted position c + H - 1 - m) (ascending complemented keys)
+// NSEG 1: both parts in the lane (w holds w0 then w1, 2H keys).  NSEG 2: part 0 in seg 0, part 1 in
+// seg 1.  NSEG 4: part 0 in seg 1, part 1 in seg 2 (segs 0 and 3 compute discarded keys).  lo / hi
+// (the middle pair, positions c - 1 and c, true keys) are returned in every lane of the group.
+template <int NSEG, int P, int H>
+SVOC_DEV void window_group(u16x2 (&r)[64], int seg, int lane, u16x2 (&w)[NSEG == 1 ? 2 * H : H], u16x2& lo,
+                           u16x2& hi) {
+  sort64_oem(r);
+  if constexpr (NSEG == 1) {
+#pragma unroll
+    for (int m = 0; m < H; ++m) {
+      w[m] = r[32 - H + m];
+      w[H + m] = ~r[32 + H - 1 - m];
+    }
+    lo = r[31];
+    hi = r[32];
+  } else {
+    if constexpr (NSEG == 2) {
+      xhc_pol<32>(r, ~0u, 0u, ~0u);         // seg 0: lower half (true), seg 1: upper half complemented
+    } else {
+      xhc_swap<16>(r);
+      merge64(r);
+      xhc_pol<32>(r, ~0u, 0u, 0u);          // segs 0-1: lower 128, segs 2-3: upper 128 (true keys)
+      const uint32_t xm = seg >= 2 ? ~0u : 0u;
+      xhc_pol<16>(r, 0u, xm, xm);           // seg 1: top of the lower half, seg 2: bottom of upper (~)
+    }
+    bitonic_top<H>(r, w);
+    constexpr int slo = NSEG == 2 ? 0 : 1;
+    const int pw = lane % P;
+    lo = shfl_k(w[H - 1], slo * P + pw);
+    hi = ~shfl_k(w[H - 1], (slo + 1) * P + pw);
   }
 }
 

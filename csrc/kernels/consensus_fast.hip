@@ -416,6 +416,7 @@ using namespace svoc;
 //   N <= 128 -> 2 lanes; N <= 256 -> 4 lanes (4 waves, 64-KiB slabs, 2 workgroups per CU).
 extern "C" int svoc_fast_round_bf16_reg(const FastParams* p, hipStream_t stream);
 extern "C" int svoc_fast_round_bf16_small(const FastParams* p, hipStream_t stream);
+extern "C" int svoc_fast_round_bf16_win(const FastParams* p, hipStream_t stream);
 
 extern "C" int svoc_fast_round_bf16(const FastParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
@@ -423,6 +424,17 @@ extern "C" int svoc_fast_round_bf16(const FastParams* p, hipStream_t stream) {
   // into two launches).  Positive hints select this LDS-tiled kernel (1 = its default geometry).
   // small instances (N <= 16, D <= 128, full round): several instances per wave, registers only
   if (p->wave_hint == 0 && p->mode == 0 && p->N <= 16 && p->D <= 128) return svoc_fast_round_bf16_small(p, stream);
+  // default: one-network window kernel (consensus_fast_win.hip) when it applies (workspace given,
+  // f <= 32); -7 forces the two-network register kernel
+  if (p->wave_hint == 0) {
+    const int rc = svoc_fast_round_bf16_win(p, stream);
+    if (rc != -2) return rc;
+  }
+  if (p->wave_hint == -7) {
+    FastParams q = *p;
+    q.wave_hint = 0;
+    return svoc_fast_round_bf16_reg(&q, stream);
+  }
   if (p->wave_hint <= 0) return svoc_fast_round_bf16_reg(p, stream);
   if (p->N < 2 || p->N > 256 || p->ld % 8 != 0 || p->D > p->ld) return -1;
   if (p->N <= 64) {

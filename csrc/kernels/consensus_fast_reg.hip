@@ -11,40 +11,16 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "svoc/bufload.hpp"
 #include "svoc/launch.hpp"
 #include "svoc/sortnet.hpp"
 #include "svoc/status.hpp"
 
 namespace svoc {
 
-// Buffer resource over one instance: row offsets ride in SGPRs (soffset), the lane's column-pair
-// offset in one VGPR (voffset); rows past N fall outside num_records and read as 0 (no clamping).
-SVOC_DEV __amdgpu_buffer_rsrc_t instance_rsrc(const void* base, uint32_t bytes) {
-  const uint64_t pa = (uint64_t)base;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pa);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
-                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-
-SVOC_DEV uint32_t bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
-}
-
 // MODE 0: fused round; 1: pass 1 only (c1 + qr -> global); 2: rank + pass 2 from the global qr.
 // The default launch runs MODE 1 then MODE 2: each half gets its own register allocation (~110
 // VGPRs instead of ~230 for the fused body), i.e. twice the resident waves per SIMD.
-template <bool CONS>
-SVOC_DEV u16x2 to_key(uint32_t raw) {
-  if constexpr (CONS) return pos_to_key(raw);
-  else return bf16x2_to_key(raw);
-}
-template <bool CONS>
-SVOC_DEV uint32_t from_key(u16x2 k) {
-  if constexpr (CONS) return key_to_pos(k);
-  else return key_to_bf16x2(k);
-}
-
 template <int NSEG, int WAVES, bool CONS, int MODE, bool RAW = false>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW ? 2 : 4))) void consensus_fast_reg_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // column pairs per wave

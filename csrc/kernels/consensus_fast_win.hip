@@ -1,0 +1,568 @@
+// Fused two-pass robust consensus, fast mode, "window" variant: ONE sorting network and ONE read of
+// the instance per round.
+//
+// Semantics: contract/src/contract.cairo:442-503 (constrained) / :370-434 (unconstrained), as in
+// consensus_fast_reg.hip.  The pass-2 smooth median (over the R = N - f reliable rows, ranks
+// R/2 - 1 and R/2, math.cairo:113-126) is an order statistic of the FULL column shifted by at most
+// f ranks: with a = N/2 - R/2 it lies at sorted position R/2 - 1 + j of the full column for the
+// smallest j with  #{removed keys <= w_j} <= j  (w = the full column's sorted keys from position
+// R/2 - 1 on).  So:
+//   pass 1 (phase A): the register-streaming median network of consensus_fast_reg.hip, extended to
+//     keep H keys on either side of the median (window_group, sortnet.hpp), written to a workspace;
+//     the qr loop (the reg kernel's) also accumulates the all-row power sums of d = x - c1;
+//   rank mask: unchanged (sort by (qr asc, idx desc), the first R are reliable);
+//   pass 2 (phase B, two lanes per column pair): only the f removed rows are read.  Their keys
+//     (f + 2 <= 2H slots with -inf / +inf sentinels around them) are sorted by a small network and
+//     compared slot by slot with the window:
+//       med_lo = min{ w_j : w_j < u'_j },  med_hi = min{ w_j : w_j < u'_(j-1) }
+//     (u' = the sorted removed keys shifted by the sentinel count, so slot j pairs with window
+//     position j).  The reliable rows' power sums are the all-row sums minus the removed rows'.
+//     When that difference would cancel (all-row second / fourth sums more than win_cancel x the
+//     reliable ones: far outliers around a tight cluster, or zero variance) the column goes on the
+//     instance's list, and the workgroup recomputes those columns exactly over the reliable rows
+//     (one wave per column) before it finishes.
+// Versus the reg kernel: no second 64*NSEG-key network, no second read of the instance (HBM: the
+// pass-1 read + the window round trip + the removed rows).  Valid for f <= 32 with a + 1 <= H and
+// f - a + 1 <= H (H = 5 or 17); the dispatcher falls back to consensus_fast_reg.hip otherwise.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "svoc/bufload.hpp"
+#include "svoc/launch.hpp"
+#include "svoc/sortnet.hpp"
+#include "svoc/status.hpp"
+
+namespace svoc {
+
+// The reliable sums are trusted when sum_all(d^2) <= C * sum_R(d^2) and likewise for d^4, C =
+// p.win_cancel (default 64, SVOC_WIN_CANCEL): the fp32 error of the difference is then <= C x the
+// all-row sums' own relative error (~1e-6 worst case, ~1e-7 typical).
+
+SVOC_DEV u16x2 win_cand(u16x2 wt, u16x2 zt) {  // wt < zt ? wt : 0xFFFF, per 16-bit half
+  const u16x2 d = __builtin_elementwise_sub_sat(zt, wt);
+  const u16x2 one = {1, 1};
+  const u16x2 m = __builtin_elementwise_min(d, one) - one;  // 0 where wt < zt, 0xFFFF otherwise
+  return wt | m;
+}
+
+// Skewness / sample-adjusted excess kurtosis (math.cairo:320-363) of n values from power sums of
+// d = x - shift; returns false for zero variance (the contract's sqrt(0) -> div-by-zero revert).
+SVOC_DEV bool moments_from_sums(float n, float t1, float t2, float t3, float t4, float& dl, float& sk, float& ku) {
+  dl = t1 / n;
+  const float e2 = t2 / n, e3 = t3 / n, e4 = t4 / n;
+  const float mu2 = e2 - dl * dl;
+  const float mu3 = e3 - 3.f * dl * e2 + 2.f * dl * dl * dl;
+  const float mu4 = e4 - 4.f * dl * e3 + 6.f * dl * dl * e2 - 3.f * dl * dl * dl * dl;
+  sk = 0.f;
+  ku = 0.f;
+  if (!(mu2 > 0.f)) return false;
+  const float k3 = n / ((n - 1.f) * (n - 2.f));
+  const float k4a = n * (n + 1.f) / (n - 1.f), k4b = 3.f * (n - 1.f) * (n - 1.f), k4c = (n - 2.f) * (n - 3.f);
+  const float sd = sqrtf(mu2);
+  sk = n * mu3 / (mu2 * sd) * k3;
+  ku = (n * mu4 / (mu2 * mu2) * k4a - k4b) / k4c;
+  return true;
+}
+
+// qr partials of the lane's 64 rows reduced across the wave's column pairs (the reg kernel's
+// transposing butterfly: stage L exchanges with lane ^ (P >> L) and halves the row set), evaluated
+// depth-first so only O(log) partials are live instead of 64; the leaves also accumulate the rows'
+// power sums of d = x - c1.  MASKW: slab with columns past D (their halves masked to +0, centre +0);
+// MASKROWS: rows >= N (read as 0 past the buffer end) are masked out of the power sums.
+struct QrCtx {
+  int nvl, lane;
+  f32x2 c2;
+};
+template <int L, int I, int P, bool MASKROWS>
+SVOC_DEV float qr_tree(const QrCtx& c, const uint32_t (&wv)[64], f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
+  if constexpr (L == 0) {
+    f32x2 y = bf16x2_to_f32x2(wv[I]) - c.c2;
+    f32x2 q = y * y;
+    const float part = q.x + q.y;
+    if (MASKROWS) {
+      const uint32_t rm = lt_mask(I, c.nvl);
+      y = fand2(y, rm);
+      q = fand2(q, rm);
+    }
+    s1 += y;
+    s2 += q;
+    s3 = __builtin_elementwise_fma(q, y, s3);
+    s4 = __builtin_elementwise_fma(q, q, s4);
+    return part;
+  } else {
+    constexpr int msk = P >> L;
+    const float lo_v = qr_tree<L - 1, I, P, MASKROWS>(c, wv, s1, s2, s3, s4);
+    const float hi_v = qr_tree<L - 1, I + (64 >> L), P, MASKROWS>(c, wv, s1, s2, s3, s4);
+    const bool up = (c.lane & msk) != 0;
+    const float send = up ? lo_v : hi_v;
+    const float keep = up ? hi_v : lo_v;
+    return keep + xor_lane<msk>(send);
+  }
+}
+// One butterfly tree (final slot I): its 64/KEEP rows I, I + KEEP, ... are loaded together (all in
+// flight at once), then reduced depth-first; an empty asm closes the tree so the next tree's loads
+// are not hoisted into this one (only one tree's words live: no spills at NSEG 4).
+template <int P, int I, bool MASKW, bool MASKROWS>
+SVOC_DEV void qr_tree_slot(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, const QrCtx& c, float* acc,
+                           f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
+  constexpr int KEEP = 64 / P;
+  uint32_t wv[64];
+#pragma unroll
+  for (int m = 0; m < 64 / KEEP; ++m) {
+    const int i = I + KEEP * m;
+    wv[i] = bload(rs, vo, i * rowb);
+    if (MASKW) wv[i] &= mW;
+  }
+  constexpr int S = __builtin_ctz(P);   // butterfly stages: log2(P)
+  acc[I] += qr_tree<S, I, P, MASKROWS>(c, wv, s1, s2, s3, s4);
+  asm volatile("" : "+v"(acc[I]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
+}
+template <int P, bool MASKW, bool MASKROWS, int... Is>
+SVOC_DEV void qr_moments_seq(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, const QrCtx& c, float* acc,
+                             f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4, std::integer_sequence<int, Is...>) {
+  (qr_tree_slot<P, Is, MASKW, MASKROWS>(rs, vo, rowb, mW, c, acc, s1, s2, s3, s4), ...);
+}
+template <int P, bool MASKW, bool MASKROWS>
+SVOC_DEV void qr_moments(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, const QrCtx& c, float* acc,
+                         f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
+  qr_moments_seq<P, MASKW, MASKROWS>(rs, vo, rowb, mW, c, acc, s1, s2, s3, s4,
+                                     std::make_integer_sequence<int, 64 / P>{});
+}
+
+template <int NSEG, int WAVES, int H, bool CONS, int MODE>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4))) void consensus_fast_win_kernel(FastParams p) {
+  constexpr int P = 64 / NSEG;          // column pairs per wave (phase A)
+  constexpr int NPAD = 64 * NSEG;
+  constexpr int W = WAVES * P * 2;      // columns per workgroup step (phase A)
+  constexpr int NT = WAVES * 64;
+  constexpr int KEEP = 64 / P;
+  __shared__ float qr_part[WAVES * NPAD];
+  __shared__ float qr_lds[NPAD];
+  __shared__ uint64_t relmask[4];
+  __shared__ int urow[32];      // removed rows, index order
+  __shared__ float misc_f[2];
+  __shared__ int misc_i[3];     // status, zero-variance flag, cleanup list length
+
+  const int b = blockIdx.x;
+  if (p.active && !p.active[b]) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 32) urow[tid] = 0;  // f < 32: unused slots still name a valid row
+  if (tid == 0) misc_i[2] = 0;
+  const int seg = lane / P, pair_w = lane % P;
+  const int cp = wave * P + pair_w;
+  const int N = p.N, D = p.D;
+  const int rowb = p.ld * 2;
+  const uint16_t* inst = (const uint16_t*)p.values + (int64_t)b * p.inst_stride;
+  const __amdgpu_buffer_rsrc_t rs = instance_rsrc(inst, (uint32_t)(N * rowb));
+  const int nslab = (D + W - 1) / W;
+  const int Dp = p.work_pairs;
+  // this instance's workspace (buffer ops, 32-bit offsets): [H][2][Dp] window keys, then at byte
+  // offset MOM the [4][Dp] float2 all-row power sums, then at LST the [2 Dp] cleanup column list
+  const __amdgpu_buffer_rsrc_t ws = instance_rsrc(p.work + (int64_t)b * p.work_stride, (uint32_t)(p.work_stride * 4));
+  const int MOM = 2 * H * Dp * 4;
+  const int LST = MOM + 4 * Dp * 8;
+  const int lo1 = (NPAD - N + 1) >> 1;
+  const int nv = N - seg * 64;
+  const int nl = N + lo1 - seg * 64;
+  const int seg_off = seg * 64 * rowb;
+  const uint32_t pol = group_polarity<NSEG>(seg);
+
+  float acc[KEEP];
+#pragma unroll
+  for (int i = 0; i < KEEP; ++i) acc[i] = 0.f;
+
+  // ------------------------------------------------------------ phase A: pass 1
+  const int pass1_slabs = MODE == 2 ? 0 : nslab;
+#pragma nounroll
+  for (int s = 0; s < pass1_slabs; ++s) {
+    const int colA = s * W + 2 * cp;
+    const int pg = s * (W / 2) + cp;    // workspace pair index
+    const bool vA = colA < D, vB = colA + 1 < D;
+    const int vo = seg_off + (vA ? colA * 2 : 0);
+    int nvl = nv, nll = nl;
+    asm volatile("" : "+v"(nvl), "+v"(nll));
+    float cA, cB;
+    const uint32_t mW = vA ? (vB ? 0xffffffffu : 0x0000ffffu) : 0u;
+    {
+      u16x2 r[64];
+      if (N == NPAD) {
+        if (CONS) {
+          const uint32_t kp = 0x80008000u ^ pol;
+#pragma unroll
+          for (int i = 0; i < 64; ++i) r[i] = as_k(bload(rs, vo, i * rowb) ^ kp);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 64; ++i) r[i] = as_k(as_u32(to_key<CONS>(bload(rs, vo, i * rowb))) ^ pol);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          const uint32_t hi_m = ~lt_mask(i, nll);
+          r[i] = as_k(((as_u32(to_key<CONS>(bload(rs, vo, i * rowb))) & (lt_mask(i, nvl) | hi_m)) | hi_m) ^ pol);
+        }
+      }
+      u16x2 klo, khi;
+      if constexpr (CONS) {
+        u16x2 wk[NSEG == 1 ? 2 * H : H];
+        window_group<NSEG, P, H>(r, seg, lane, wk, klo, khi);
+        if constexpr (NSEG == 1) {
+#pragma unroll
+          for (int m = 0; m < H; ++m) {
+            bstore(ws, as_u32(wk[m]), pg * 4, 2 * m * Dp * 4);
+            bstore(ws, as_u32(wk[H + m]), (Dp + pg) * 4, 2 * m * Dp * 4);
+          }
+        } else {
+          constexpr int slo = NSEG == 2 ? 0 : 1;
+          if (seg == slo || seg == slo + 1) {
+            const int part = seg - slo;
+#pragma unroll
+            for (int m = 0; m < H; ++m) bstore(ws, as_u32(wk[m]), (part * Dp + pg) * 4, 2 * m * Dp * 4);
+          }
+        }
+      } else {
+        median_group<NSEG>(r, klo, khi);
+      }
+      const uint32_t lo = from_key<CONS>(klo), hi = from_key<CONS>(khi);
+      cA = 0.5f * (bf16_lo(lo) + bf16_lo(hi));
+      cB = 0.5f * (bf16_hi(lo) + bf16_hi(hi));
+    }
+    if (seg == 0) {
+      if (vA) p.c1[(int64_t)b * D + colA] = cA;
+      if (vB) p.c1[(int64_t)b * D + colA + 1] = cB;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // the re-read's offset depends on the network's result (empty asm): otherwise the 64 loads are
+    // hoisted above the network and both 64-register arrays are live at once (spills)
+    int vo2 = vo;
+    asm volatile("" : "+v"(vo2) : "v"(cA), "v"(cB));
+    const QrCtx qc{nvl, lane, f32x2{vA ? cA : 0.f, vB ? cB : 0.f}};
+    f32x2 s1 = {0.f, 0.f}, s2 = s1, s3 = s1, s4 = s1;
+    if ((s + 1) * W <= D) {
+      if (N == NPAD) qr_moments<P, false, false>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
+      else qr_moments<P, false, true>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
+    } else {
+      if (N == NPAD) qr_moments<P, true, false>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
+      else qr_moments<P, true, true>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
+    }
+    if constexpr (NSEG == 4) {
+      s1.x += xor_lane<16>(s1.x); s1.y += xor_lane<16>(s1.y); s2.x += xor_lane<16>(s2.x); s2.y += xor_lane<16>(s2.y);
+      s3.x += xor_lane<16>(s3.x); s3.y += xor_lane<16>(s3.y); s4.x += xor_lane<16>(s4.x); s4.y += xor_lane<16>(s4.y);
+    }
+    if constexpr (NSEG >= 2) {
+      s1.x += xor_lane<32>(s1.x); s1.y += xor_lane<32>(s1.y); s2.x += xor_lane<32>(s2.x); s2.y += xor_lane<32>(s2.y);
+      s3.x += xor_lane<32>(s3.x); s3.y += xor_lane<32>(s3.y); s4.x += xor_lane<32>(s4.x); s4.y += xor_lane<32>(s4.y);
+    }
+    if (seg == 0) {
+      bstore2(ws, s1, pg * 8, MOM);
+      bstore2(ws, s2, pg * 8, MOM + Dp * 8);
+      bstore2(ws, s3, pg * 8, MOM + 2 * Dp * 8);
+      bstore2(ws, s4, pg * 8, MOM + 3 * Dp * 8);
+    }
+  }
+
+  // ------------------------------------------------------------ qr reduction
+  {
+    int base = 0;
+#pragma unroll
+    for (int h = 32, msk = P / 2; msk >= 1; h >>= 1, msk >>= 1) base += (lane & msk) ? h : 0;
+#pragma unroll
+    for (int i = 0; i < KEEP; ++i) qr_part[wave * NPAD + seg * 64 + base + i] = acc[i];
+  }
+  __syncthreads();
+  for (int t = tid; t < NPAD; t += NT) {
+    float q = 0.f;
+    if (MODE == 2) {
+      q = t < N ? p.qr[(int64_t)b * N + t] : 0.f;
+    } else {
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) q += qr_part[w * NPAD + t];
+    }
+    qr_lds[t] = q;
+  }
+  __syncthreads();
+  if (MODE == 1) {
+    for (int t = tid; t < N; t += NT) p.qr[(int64_t)b * N + t] = qr_lds[t];
+    if (tid == 0) p.status[b] = ST_OK;
+    return;
+  }
+
+  // ------------------------------------------------------------ rank mask (contract.cairo:345-363)
+  const int f = p.n_failing;
+  const int R = N - f;
+  for (int base = 0; base < NPAD; base += NT) {
+    const int t = base + tid;
+    bool rel = false;
+    if (t < N) {
+      const float myq = qr_lds[t];
+      int rank = 0;
+      const int n4 = N & ~3;
+      for (int j = 0; j < n4; j += 4) {
+        const float4 q4 = *(const float4*)(qr_lds + j);
+        rank += (q4.x < myq || (q4.x == myq && j > t)) ? 1 : 0;
+        rank += (q4.y < myq || (q4.y == myq && j + 1 > t)) ? 1 : 0;
+        rank += (q4.z < myq || (q4.z == myq && j + 2 > t)) ? 1 : 0;
+        rank += (q4.w < myq || (q4.w == myq && j + 3 > t)) ? 1 : 0;
+      }
+      for (int j = n4; j < N; ++j) {
+        const float qj = qr_lds[j];
+        rank += (qj < myq || (qj == myq && j > t)) ? 1 : 0;
+      }
+      rel = rank < R;
+    }
+    const uint64_t bal = __ballot(rel);
+    if (lane == 0 && (t >> 6) < 4) relmask[t >> 6] = bal;
+  }
+  __syncthreads();
+  // removed rows in index order (pass 2 reads only these)
+  for (int t = tid; t < N; t += NT) {
+    const int w = t >> 6;
+    const uint64_t nr = ~relmask[w];
+    if ((nr >> (t & 63)) & 1) {
+      int cnt = __popcll(nr & ((1ull << (t & 63)) - 1));
+      for (int v = 0; v < w; ++v) cnt += __popcll(~relmask[v]);
+      if (cnt < 32) urow[cnt] = t;
+    }
+  }
+  if (tid < 64) {
+    float s_all = 0.f, s_rel = 0.f;
+    for (int t = tid; t < N; t += 64) {
+      const float q = qr_lds[t];
+      s_all += q;
+      s_rel += ((relmask[t >> 6] >> (t & 63)) & 1) ? q : 0.f;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      s_all += __shfl_xor(s_all, o);
+      s_rel += __shfl_xor(s_rel, o);
+    }
+    if (tid == 0) {
+      int st = ST_OK;
+      const float rd = p.legacy ? 1.f : (float)(p.rel_dim > 0 ? p.rel_dim : D);
+      float rel1, rel2 = 0.f;
+      if (CONS) rel1 = 1.f - 2.f * sqrtf(s_all / (float)N / rd);
+      else rel1 = 1.f - fminf(p.max_spread, sqrtf(s_all / (float)N)) / p.max_spread;
+      if (!(rel1 >= 0.f && rel1 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
+      else if (R < 2) st = R <= 0 ? ST_USIZE_UNDERFLOW : ST_INDEX_OOB;
+      else {
+        if (CONS) rel2 = 1.f - 2.f * sqrtf(s_rel / (float)R / rd);
+        else rel2 = 1.f - fminf(p.max_spread, sqrtf(s_rel / (float)R)) / p.max_spread;
+        if (!(rel2 >= 0.f && rel2 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
+        else if (R < 4 && !p.legacy) st = ST_TOO_FEW_RELIABLE;
+      }
+      misc_f[0] = rel1;
+      misc_f[1] = rel2;
+      misc_i[0] = st;
+      misc_i[1] = 0;
+    }
+  }
+  __syncthreads();
+  if (misc_i[0] != ST_OK) {
+    if (tid == 0) p.status[b] = misc_i[0];
+    return;
+  }
+  for (int t = tid; t < N; t += NT) {
+    p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
+    p.qr[(int64_t)b * N + t] = qr_lds[t];
+  }
+
+  // ------------------------------------------------------------ phase B: pass 2 (contract.cairo:476-500)
+  // two lanes per column pair; lane parity = window part (0: lower, true keys; 1: upper, complemented
+  // keys) = the column whose moments / outputs the lane finalises
+  const float n = (float)R;
+  const int sh = H - 1 - (N / 2 - R / 2);   // -inf sentinels in front of the removed keys
+  const int npairs = (D + 1) >> 1;
+  const int64_t ob = (int64_t)b * D;
+  const int part = lane & 1;
+  const uint32_t ppol = part ? ~0u : 0u;
+  bool zv = false;
+#pragma nounroll
+  for (int base = wave * 32; base < npairs; base += WAVES * 32) {
+    const int pair = base + (lane >> 1);
+    const int pr = pair < npairs ? pair : npairs - 1;
+    const int col = 2 * pr + part;
+    const bool cv = pair < npairs && col < D;
+    const int vo = pr * 4;
+    const float c1A = p.c1[ob + 2 * pr];
+    const float c1B = 2 * pr + 1 < D ? p.c1[ob + 2 * pr + 1] : 0.f;
+    // opaque per-iteration copies: otherwise LICM hoists the 2H slot offsets / masks (uniform,
+    // loop-invariant) out of the pair loop and keeps them live in VGPRs (spills)
+    int shl = sh, fl = f;
+    asm volatile("" : "+s"(shl), "+s"(fl));
+    // the removed rows' words, all loads in flight at once (uniform row offsets).  Constrained: the
+    // 2H network slots (slot t = removed row t - sh; the others become sentinels below);
+    // unconstrained: the f <= 32 removed rows
+    constexpr int NS = CONS ? 2 * H : 32;
+    uint32_t uw[NS];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      const int row = CONS ? t - shl : t;
+      const bool real = row >= 0 && row < fl;
+      uw[t] = 0u;
+      if (CONS || real) uw[t] = bload(rs, vo, __builtin_amdgcn_readfirstlane(urow[real ? row : 0]) * rowb);
+    }
+    // removed rows' power sums of this lane's column (d = x - c1)
+    const float cc = part ? c1B : c1A;
+    const uint32_t hsh = part ? 0u : 16u;   // bf16 of the lane's column -> fp32 bits
+    float u1 = 0.f, u2 = 0.f, u3 = 0.f, u4 = 0.f;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      const int row = CONS ? t - shl : t;
+      if (row >= 0 && row < fl) {   // uniform
+        const float y = __builtin_bit_cast(float, (uw[t] << hsh) & 0xffff0000u) - cc;
+        const float q = y * y;
+        u1 += y;
+        u2 += q;
+        u3 = fmaf(q, y, u3);
+        u4 = fmaf(q, q, u4);
+      }
+    }
+
+    float med = 0.f;
+    if constexpr (CONS) {
+      // removed keys + sentinels (2H slots) in this lane's polarity, sorted: ranks 0..H are consumed
+      u16x2 z[64];
+#pragma unroll
+      for (int t = 0; t < 64; ++t) {
+        if (t < 2 * H) {
+          const int row = t - shl;
+          const bool real = row >= 0 && row < fl;
+          // scalar masks only: real slot -> key, else the -inf (0) / +inf (~0) sentinel
+          const uint32_t mreal = real ? ~0u : 0u;
+          const uint32_t kx = real ? 0x80008000u : (t < shl ? 0u : ~0u);
+          z[t] = as_k((uw[t] & mreal) ^ kx ^ ppol);
+        } else {
+          z[t] = as_k(~0u);
+        }
+      }
+      sort_oem<64>(z);
+      uint32_t clo = ~0u, chi = ~0u;
+#pragma unroll
+      for (int m = 0; m < H; ++m) {
+        const u16x2 wt = as_k(bload(ws, (part * Dp + pr) * 4, 2 * m * Dp * 4) ^ ppol);
+        const u16x2 zl = as_k(as_u32(z[m]) ^ ppol);
+        const uint32_t zprev = m == 0 ? 0u : as_u32(z[m - 1]);
+        const u16x2 zh = as_k(blend(zprev, as_u32(z[m + 1]), ppol) ^ ppol);
+        clo = as_u32(kmin(as_k(clo), win_cand(wt, zl)));
+        chi = as_u32(kmin(as_k(chi), win_cand(wt, zh)));
+      }
+      clo = as_u32(kmin(as_k(clo), as_k(xor_lane_u32<1>(clo))));
+      chi = as_u32(kmin(as_k(chi), as_k(xor_lane_u32<1>(chi))));
+      const uint32_t lo = key_to_pos(as_k(clo)), hi = key_to_pos(as_k(chi));
+      med = part ? 0.5f * (bf16_hi(lo) + bf16_hi(hi)) : 0.5f * (bf16_lo(lo) + bf16_lo(hi));
+    }
+
+    // reliable rows' power sums = all-row sums (phase A) - removed rows' sums
+    const int mo = pr * 8 + part * 4;
+    const float sa2 = bloadf(ws, mo, MOM + Dp * 8), sa4 = bloadf(ws, mo, MOM + 3 * Dp * 8);
+    const float t1 = bloadf(ws, mo, MOM) - u1;
+    const float t2 = sa2 - u2;
+    const float t3 = bloadf(ws, mo, MOM + 2 * Dp * 8) - u3;
+    const float t4 = sa4 - u4;
+    const bool good = t2 > 0.f && sa2 <= p.win_cancel * t2 && sa4 <= p.win_cancel * t4;
+    if (cv) {
+      float dl, sk, ku;
+      const bool nz = moments_from_sums(n, t1, t2, t3, t4, dl, sk, ku);
+      if (CONS) p.consensus[ob + col] = med;
+      if (good) {
+        if (!CONS) p.consensus[ob + col] = cc + dl;
+        p.skew[ob + col] = p.legacy ? 0.f : sk;
+        p.kurt[ob + col] = p.legacy ? 0.f : ku;
+        zv |= !nz;
+      } else {
+        // exact recomputation over the reliable rows below (each column listed once: <= D entries)
+        const int k = atomicAdd(&misc_i[2], 1);
+        bstore(ws, (uint32_t)col, k * 4, LST);
+      }
+    }
+  }
+  if (zv && !p.legacy) misc_i[1] = 1;
+  __syncthreads();
+  // cleanup: one wave per listed column, lanes stride the rows, wave reduction (math.cairo:320-363)
+  const int nredo = misc_i[2];
+  if (nredo) {
+    for (int k = wave; k < nredo; k += WAVES) {
+      // (sc0: read through the vL1D -- the entry was written by another wave of this workgroup)
+      const int col = (int)__builtin_amdgcn_readfirstlane(__builtin_amdgcn_raw_buffer_load_b32(ws, 0, LST + k * 4, 1));
+      const float cc = p.c1[ob + col];
+      const uint16_t* xc = inst + col;
+      float t1 = 0.f, t2 = 0.f, t3 = 0.f, t4 = 0.f;
+#pragma unroll
+      for (int g = 0; g < NSEG; ++g) {
+        const int i = g * 64 + lane;
+        const bool use = i < N && ((relmask[g] >> lane) & 1);
+        if (use) {
+          const float y = __builtin_bit_cast(float, (uint32_t)xc[(int64_t)i * p.ld] << 16) - cc;
+          const float q = y * y;
+          t1 += y;
+          t2 += q;
+          t3 = fmaf(q, y, t3);
+          t4 = fmaf(q, q, t4);
+        }
+      }
+      t1 += xor_lane<1>(t1); t2 += xor_lane<1>(t2); t3 += xor_lane<1>(t3); t4 += xor_lane<1>(t4);
+      t1 += xor_lane<2>(t1); t2 += xor_lane<2>(t2); t3 += xor_lane<2>(t3); t4 += xor_lane<2>(t4);
+      t1 += xor_lane<4>(t1); t2 += xor_lane<4>(t2); t3 += xor_lane<4>(t3); t4 += xor_lane<4>(t4);
+      t1 += xor_lane<8>(t1); t2 += xor_lane<8>(t2); t3 += xor_lane<8>(t3); t4 += xor_lane<8>(t4);
+      t1 += xor_lane<16>(t1); t2 += xor_lane<16>(t2); t3 += xor_lane<16>(t3); t4 += xor_lane<16>(t4);
+      t1 += xor_lane<32>(t1); t2 += xor_lane<32>(t2); t3 += xor_lane<32>(t3); t4 += xor_lane<32>(t4);
+      if (lane == 0) {
+        float dl, sk, ku;
+        const bool nz = moments_from_sums(n, t1, t2, t3, t4, dl, sk, ku);
+        if (!CONS) p.consensus[ob + col] = cc + dl;
+        p.skew[ob + col] = p.legacy ? 0.f : sk;
+        p.kurt[ob + col] = p.legacy ? 0.f : ku;
+        if (!nz && !p.legacy) misc_i[1] = 1;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    p.rel[2 * (int64_t)b] = misc_f[0];
+    p.rel[2 * (int64_t)b + 1] = misc_f[1];
+    p.status[b] = misc_i[1] ? ST_ZERO_VARIANCE : ST_OK;
+  }
+}
+
+template <int NSEG, int H, bool CONS>
+static void launch_win_c(const FastParams& p, hipStream_t stream) {
+  constexpr int WAVES = 4;
+  if (p.mode == 1) hipLaunchKernelGGL((consensus_fast_win_kernel<NSEG, WAVES, H, CONS, 1>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+  else if (p.mode == 2) hipLaunchKernelGGL((consensus_fast_win_kernel<NSEG, WAVES, H, CONS, 2>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+  else hipLaunchKernelGGL((consensus_fast_win_kernel<NSEG, WAVES, H, CONS, 0>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+}
+
+template <int NSEG>
+static void launch_win(const FastParams& p, int H, hipStream_t stream) {
+  if (!p.constrained) launch_win_c<NSEG, 5, false>(p, stream);   // no window: H = 5 keeps the layout
+  else if (H == 5) launch_win_c<NSEG, 5, true>(p, stream);
+  else launch_win_c<NSEG, 17, true>(p, stream);
+}
+
+// Window half-width for (N, f): the smallest H in {5, 17} with a + 1 <= H and f - a + 1 <= H.
+static int win_h(int N, int f) {
+  const int R = N - f, a = N / 2 - R / 2;
+  if (a + 1 <= 5 && f - a + 1 <= 5) return 5;
+  if (a + 1 <= 17 && f - a + 1 <= 17) return 17;
+  return 0;
+}
+
+}  // namespace svoc
+
+using namespace svoc;
+
+// Returns -2 when the window kernel does not apply (no workspace, f > 32, ...): the caller falls back.
+extern "C" int svoc_fast_round_bf16_win(const FastParams* p, hipStream_t stream) {
+  if (p->B <= 0) return 0;
+  if (!p->work || p->N < 2 || p->N > 256 || p->ld % 8 != 0 || p->D > p->ld) return -2;
+  if (p->n_failing < 0 || p->n_failing > 32 || p->n_failing > p->N - 2) return -2;
+  const int H = win_h(p->N, p->n_failing);
+  if (H == 0) return -2;
+  if (p->work_pairs < fast_work_pairs(p->D) || p->work_pairs % 256 != 0 || p->work_stride < fast_work_words(p->D))
+    return -1;
+  if (p->N <= 64) launch_win<1>(*p, H, stream);
+  else if (p->N <= 128) launch_win<2>(*p, H, stream);
+  else launch_win<4>(*p, H, stream);
+  return (int)hipGetLastError();
+}

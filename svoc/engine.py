@@ -79,6 +79,7 @@ class ConsensusEngine:
         self._active = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.wave_hint = 0
         self.rounds = 0
+        self._work = None   # window-kernel workspace (GPU fast mode), allocated on first use
         # health counters folded in by every round's epilogue: [rel2 sum (2^-32 units fast / wsad
         # exact), committed, processed, reverted]
         self.metrics_fx = torch.zeros(4, dtype=torch.int64, device=dev)
@@ -129,7 +130,7 @@ class ConsensusEngine:
             self._ops.fast_round(self.values, self._active, self.D, self.cfg.n_failing_oracles,
                                  self.cfg.constrained, float(mx), self.c1, self.consensus, self.skew,
                                  self.kurt, self.rel, self.qr, self.reliable, self.status, self.wave_hint,
-                                 0, 0, self.cfg.legacy)
+                                 0, 0, self.cfg.legacy, self.work())
         else:
             self._ops.exact_round(self.values, self._active, self.cfg.n_failing_oracles, self.cfg.constrained,
                                   self.cfg.max_spread_wsad, self.c1, self.consensus, self.skew, self.kurt,
@@ -137,6 +138,19 @@ class ConsensusEngine:
         self._ops.round_epilogue(self._active, self.status, self.rel, self.consensus_active, self.touched,
                                  self.metrics_fx)
         self.rounds += 1
+
+    def work(self) -> Optional[torch.Tensor]:
+        """Workspace of the one-network window kernel (34 window keys + 8 power sums + 2 cleanup
+        list slots per column pair: 176 B per column pair and instance); None where that kernel does not run (CPU, small
+        instances, more than 32 failing oracles)."""
+        if self.mode != "fast" or self.device.type != "cuda":
+            return None
+        if not svops.fast_work_applies(self.N, self.D, self.cfg.n_failing_oracles):
+            return None
+        if self._work is None:
+            self._work = torch.empty(svops.fast_work_numel(self.B, self.D), dtype=torch.int32,
+                                     device=self.device)
+        return self._work
 
     def metrics(self) -> torch.Tensor:
         """[sum rel2 of committed rounds, committed, processed, reverted] as float64 (device)."""

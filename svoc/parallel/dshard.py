@@ -36,9 +36,10 @@ def run_round_sharded(engine, d_global: int, group=None, world: int = 1) -> None
     args = (e.values, e._active, e.D, e.cfg.n_failing_oracles, e.cfg.constrained, mx, e.c1, e.consensus,
             e.skew, e.kurt, e.rel, e.qr, e.reliable, e.status, e.wave_hint)
     lg = e.cfg.legacy
-    e._ops.fast_round(*args, 1, d_global, lg)      # pass 1: local c1 + qr partials
+    w = e.work()                                     # window kernel: pass 1 -> pass 2 state
+    e._ops.fast_round(*args, 1, d_global, lg, w)   # pass 1: local c1 + qr partials
     if world > 1:
         dist.all_reduce(e.qr, op=dist.ReduceOp.SUM, group=group)
-    e._ops.fast_round(*args, 2, d_global, lg)      # pass 2 from the global qr
+    e._ops.fast_round(*args, 2, d_global, lg, w)   # pass 2 from the global qr
     e._ops.round_epilogue(e._active, e.status, e.rel, e.consensus_active, e.touched, e.metrics_fx)
     e.rounds += 1

@@ -21,13 +21,18 @@ def alloc_exact_out(B, N, D, device):
         status=torch.full((B,), -1, dtype=torch.int32, device=device))
 
 
-def run_fast(values, D, n_failing, constrained, max_spread=1.0, active=None, wave_hint=0, legacy=False):
+def run_fast(values, D, n_failing, constrained, max_spread=1.0, active=None, wave_hint=0, legacy=False,
+             work=None):
     B, N = values.shape[:2]
     o = alloc_fast_out(B, N, D, values.device)
     svops.ops().fast_round(values, active, D, n_failing, constrained, max_spread, o["c1"], o["consensus"],
                            o["skew"], o["kurt"], o["rel"], o["qr"], o["reliable"], o["status"], wave_hint,
-                           0, 0, legacy)
+                           0, 0, legacy, work)
     return o
+
+
+def fast_work(B, D, device):
+    return torch.empty(svops.fast_work_numel(B, D), dtype=torch.int32, device=device)
 
 
 def run_exact(values, n_failing, constrained, max_spread=0, active=None, legacy=False):

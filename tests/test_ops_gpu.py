@@ -156,7 +156,7 @@ def test_fast_hip_split_modes_match_full(N, D, f, constrained):
     B = 6
     x, _ = beta_oracles(B, N, D, f, seed=N)
     xg = x.to(DEV)
-    full = run_fast(xg, D, f, constrained, 1.0)
+    full = run_fast(xg, D, f, constrained, 1.0, wave_hint=-7)   # two-network kernel (split = no workspace)
     from helpers import alloc_fast_out
     o = alloc_fast_out(B, N, D, DEV)
     args = (xg, None, D, f, constrained, 1.0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"], o["qr"],
