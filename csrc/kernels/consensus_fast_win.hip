@@ -11,7 +11,7 @@
 //     keep H keys on either side of the median (window_group, sortnet.hpp), written to a workspace;
 //     the qr loop (the reg kernel's) also accumulates the all-row power sums of d = x - c1;
 //   rank mask: unchanged (sort by (qr asc, idx desc), the first R are reliable);
-//   pass 2 (phase B, two lanes per column pair): only the f removed rows are read.  Their keys
+//   pass 2 (phase B, one lane per column pair): only the f removed rows are read.  Their keys
 //     (f + 2 <= 2H slots with -inf / +inf sentinels around them) are sorted by a small network and
 //     compared slot by slot with the window:
 //       med_lo = min{ w_j : w_j < u'_j },  med_hi = min{ w_j : w_j < u'_(j-1) }
@@ -368,24 +368,21 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   }
 
   // ------------------------------------------------------------ phase B: pass 2 (contract.cairo:476-500)
-  // two lanes per column pair; lane parity = window part (0: lower, true keys; 1: upper, complemented
-  // keys) = the column whose moments / outputs the lane finalises
+  // one lane per column pair: the removed keys are sorted once (true key order) and ranked against
+  // both window halves; packed power sums for the two columns
   const float n = (float)R;
   const int sh = H - 1 - (N / 2 - R / 2);   // -inf sentinels in front of the removed keys
   const int npairs = (D + 1) >> 1;
   const int64_t ob = (int64_t)b * D;
-  const int part = lane & 1;
-  const uint32_t ppol = part ? ~0u : 0u;
   bool zv = false;
 #pragma nounroll
-  for (int base = wave * 32; base < npairs; base += WAVES * 32) {
-    const int pair = base + (lane >> 1);
+  for (int base = wave * 64; base < npairs; base += WAVES * 64) {
+    const int pair = base + lane;
     const int pr = pair < npairs ? pair : npairs - 1;
-    const int col = 2 * pr + part;
-    const bool cv = pair < npairs && col < D;
     const int vo = pr * 4;
     const float c1A = p.c1[ob + 2 * pr];
     const float c1B = 2 * pr + 1 < D ? p.c1[ob + 2 * pr + 1] : 0.f;
+    const f32x2 c2 = {c1A, c1B};
     // opaque per-iteration copies: otherwise LICM hoists the 2H slot offsets / masks (uniform,
     // loop-invariant) out of the pair loop and keeps them live in VGPRs (spills)
     int shl = sh, fl = f;
@@ -394,79 +391,84 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
     // 2H network slots (slot t = removed row t - sh; the others become sentinels below);
     // unconstrained: the f <= 32 removed rows
     constexpr int NS = CONS ? 2 * H : 32;
+    const int s0 = CONS ? shl : 0;
+    // slot bit masks (uniform): real = a removed row, low = a -inf sentinel
+    const uint64_t realm = ((fl >= 64 ? ~0ull : (1ull << fl) - 1)) << s0;
+    const uint64_t lowm = (1ull << s0) - 1;
     uint32_t uw[NS];
 #pragma unroll
     for (int t = 0; t < NS; ++t) {
-      const int row = CONS ? t - shl : t;
-      const bool real = row >= 0 && row < fl;
+      const int row = t - s0;
+      const bool real = (realm >> t) & 1;
       uw[t] = 0u;
       if (CONS || real) uw[t] = bload(rs, vo, __builtin_amdgcn_readfirstlane(urow[real ? row : 0]) * rowb);
     }
-    // removed rows' power sums of this lane's column (d = x - c1)
-    const float cc = part ? c1B : c1A;
-    const uint32_t hsh = part ? 0u : 16u;   // bf16 of the lane's column -> fp32 bits
-    float u1 = 0.f, u2 = 0.f, u3 = 0.f, u4 = 0.f;
+    // removed rows' power sums of d = x - c1 (both columns, packed)
+    f32x2 u1 = {0.f, 0.f}, u2 = u1, u3 = u1, u4 = u1;
 #pragma unroll
     for (int t = 0; t < NS; ++t) {
-      const int row = CONS ? t - shl : t;
-      if (row >= 0 && row < fl) {   // uniform
-        const float y = __builtin_bit_cast(float, (uw[t] << hsh) & 0xffff0000u) - cc;
-        const float q = y * y;
+      if ((realm >> t) & 1) {   // uniform
+        const f32x2 y = bf16x2_to_f32x2(uw[t]) - c2;
+        const f32x2 q = y * y;
         u1 += y;
         u2 += q;
-        u3 = fmaf(q, y, u3);
-        u4 = fmaf(q, q, u4);
+        u3 = __builtin_elementwise_fma(q, y, u3);
+        u4 = __builtin_elementwise_fma(q, q, u4);
       }
     }
 
-    float med = 0.f;
+    uint32_t medw = 0u;   // pass-2 middle pair (true keys) of both columns: lo, hi
+    uint32_t mhw = 0u;
     if constexpr (CONS) {
-      // removed keys + sentinels (2H slots) in this lane's polarity, sorted: ranks 0..H are consumed
+      // removed keys + sentinels: U'[t], t < 2H, ascending true keys
       u16x2 z[64];
 #pragma unroll
       for (int t = 0; t < 64; ++t) {
         if (t < 2 * H) {
-          const int row = t - shl;
-          const bool real = row >= 0 && row < fl;
           // scalar masks only: real slot -> key, else the -inf (0) / +inf (~0) sentinel
-          const uint32_t mreal = real ? ~0u : 0u;
-          const uint32_t kx = real ? 0x80008000u : (t < shl ? 0u : ~0u);
-          z[t] = as_k((uw[t] & mreal) ^ kx ^ ppol);
+          const uint32_t mreal = 0u - (uint32_t)((realm >> t) & 1);
+          const uint32_t kx = (0x80008000u & mreal) | (~mreal & (0u - (uint32_t)(((~lowm) >> t) & 1)));
+          z[t] = as_k((uw[t] & mreal) ^ kx);
         } else {
           z[t] = as_k(~0u);
         }
       }
       sort_oem<64>(z);
-      uint32_t clo = ~0u, chi = ~0u;
+      // lower window half: position c - H + m pairs with U'[m] (lo) / U'[m - 1] (hi); upper half
+      // (stored complemented, position c + H - 1 - m): U'[2H - 1 - m] (lo) / U'[2H - 2 - m] (hi)
+      u16x2 clo = as_k(~0u), chi = as_k(~0u);
 #pragma unroll
       for (int m = 0; m < H; ++m) {
-        const u16x2 wt = as_k(bload(ws, (part * Dp + pr) * 4, 2 * m * Dp * 4) ^ ppol);
-        const u16x2 zl = as_k(as_u32(z[m]) ^ ppol);
-        const uint32_t zprev = m == 0 ? 0u : as_u32(z[m - 1]);
-        const u16x2 zh = as_k(blend(zprev, as_u32(z[m + 1]), ppol) ^ ppol);
-        clo = as_u32(kmin(as_k(clo), win_cand(wt, zl)));
-        chi = as_u32(kmin(as_k(chi), win_cand(wt, zh)));
+        const u16x2 wl = as_k(bload(ws, pr * 4, 2 * m * Dp * 4));
+        const u16x2 wu = ~as_k(bload(ws, (Dp + pr) * 4, 2 * m * Dp * 4));
+        clo = kmin(clo, win_cand(wl, z[m]));
+        if (m) chi = kmin(chi, win_cand(wl, z[m - 1]));
+        clo = kmin(clo, win_cand(wu, z[2 * H - 1 - m]));
+        chi = kmin(chi, win_cand(wu, z[2 * H - 2 - m]));
       }
-      clo = as_u32(kmin(as_k(clo), as_k(xor_lane_u32<1>(clo))));
-      chi = as_u32(kmin(as_k(chi), as_k(xor_lane_u32<1>(chi))));
-      const uint32_t lo = key_to_pos(as_k(clo)), hi = key_to_pos(as_k(chi));
-      med = part ? 0.5f * (bf16_hi(lo) + bf16_hi(hi)) : 0.5f * (bf16_lo(lo) + bf16_lo(hi));
+      medw = key_to_pos(clo);
+      mhw = key_to_pos(chi);
     }
 
     // reliable rows' power sums = all-row sums (phase A) - removed rows' sums
-    const int mo = pr * 8 + part * 4;
-    const float sa2 = bloadf(ws, mo, MOM + Dp * 8), sa4 = bloadf(ws, mo, MOM + 3 * Dp * 8);
-    const float t1 = bloadf(ws, mo, MOM) - u1;
-    const float t2 = sa2 - u2;
-    const float t3 = bloadf(ws, mo, MOM + 2 * Dp * 8) - u3;
-    const float t4 = sa4 - u4;
-    const bool good = t2 > 0.f && sa2 <= p.win_cancel * t2 && sa4 <= p.win_cancel * t4;
-    if (cv) {
-      float dl, sk, ku;
-      const bool nz = moments_from_sums(n, t1, t2, t3, t4, dl, sk, ku);
-      if (CONS) p.consensus[ob + col] = med;
+    const int mo = pr * 8;
+    const f32x2 sa1 = {bloadf(ws, mo, MOM), bloadf(ws, mo + 4, MOM)};
+    const f32x2 sa2 = {bloadf(ws, mo, MOM + Dp * 8), bloadf(ws, mo + 4, MOM + Dp * 8)};
+    const f32x2 sa3 = {bloadf(ws, mo, MOM + 2 * Dp * 8), bloadf(ws, mo + 4, MOM + 2 * Dp * 8)};
+    const f32x2 sa4 = {bloadf(ws, mo, MOM + 3 * Dp * 8), bloadf(ws, mo + 4, MOM + 3 * Dp * 8)};
+    const f32x2 t1 = sa1 - u1, t2 = sa2 - u2, t3 = sa3 - u3, t4 = sa4 - u4;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int col = 2 * pr + h;
+      if (!(pair < npairs && col < D)) continue;
+      const float a2 = h ? sa2.y : sa2.x, a4 = h ? sa4.y : sa4.x;
+      const float r2 = h ? t2.y : t2.x, r4 = h ? t4.y : t4.x;
+      const bool good = r2 > 0.f && a2 <= p.win_cancel * r2 && a4 <= p.win_cancel * r4;
+      if (CONS) p.consensus[ob + col] = h ? 0.5f * (bf16_hi(medw) + bf16_hi(mhw)) : 0.5f * (bf16_lo(medw) + bf16_lo(mhw));
       if (good) {
-        if (!CONS) p.consensus[ob + col] = cc + dl;
+        float dl, sk, ku;
+        const bool nz = moments_from_sums(n, h ? t1.y : t1.x, r2, h ? t3.y : t3.x, r4, dl, sk, ku);
+        if (!CONS) p.consensus[ob + col] = (h ? c1B : c1A) + dl;
         p.skew[ob + col] = p.legacy ? 0.f : sk;
         p.kurt[ob + col] = p.legacy ? 0.f : ku;
         zv |= !nz;

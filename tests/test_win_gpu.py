@@ -24,12 +24,15 @@ def _both(x, D, f, cons, ms=1.0, legacy=False):
 
 
 def _same(win, reg, constrained=True):
-    """Same order statistics -> identical c1 / qr / rel / mask / constrained consensus; the moments and
-    the unconstrained mean differ in rounding only (shift c1 here, first reliable row there)."""
+    """Same order statistics -> identical c1 / mask / constrained consensus; qr, rel, the moments and the
+    unconstrained mean differ in rounding only (shift c1 here, first reliable row there)."""
     assert torch.equal(win["status"], reg["status"])
     ok = win["status"] == 0
-    for k in ("c1", "qr", "rel", "reliable") + (("consensus",) if constrained else ()):
+    for k in ("c1", "reliable") + (("consensus",) if constrained else ()):
         assert torch.equal(win[k][ok], reg[k][ok]), k
+    # qr: same terms, last-bit freedom in the compiler's FMA contraction of (x - c)^2 sums
+    torch.testing.assert_close(win["qr"][ok], reg["qr"][ok], rtol=2e-6, atol=0)
+    torch.testing.assert_close(win["rel"][ok], reg["rel"][ok], rtol=1e-6, atol=1e-7)
     if not constrained:
         torch.testing.assert_close(win["consensus"][ok], reg["consensus"][ok], rtol=1e-5, atol=1e-5)
     torch.testing.assert_close(win["skew"][ok], reg["skew"][ok], rtol=1e-3, atol=1e-3)
@@ -66,7 +69,7 @@ def test_win_ties(N, f, levels):
     win, reg = _both(xg, D, f, True)
     assert torch.equal(win["status"], reg["status"])
     ok = win["status"] == 0
-    for k in ("consensus", "rel", "reliable"):
+    for k in ("consensus", "reliable"):
         assert torch.equal(win[k][ok], reg[k][ok]), k
     r = torch_ref.fast_round(xg[:, :, :D], f, True, 1.0)
     ok = ok & (r["status"] == 0) if "status" in r else ok
