@@ -16,6 +16,10 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 fi
 
+stage smoke
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; tail -2 gpurun_out/smoke.log; [ $rc -ne 0 ] && exit $rc
+
 BENCHES="${BENCHES:-c2:10:2 c3:10:2}"
 for spec in $BENCHES; do
   IFS=: read cfg steps warm <<< "$spec"
