@@ -33,7 +33,7 @@ CONFIGS = {
     "c1": dict(model="plumbing: 4 oracles x 2 dims, one exact (wsad) round per step on the CPU engine", N=4, D=2,
                f=0, batch=1, update_frac=0.0, device="cpu", mode="exact", dtype="int64-wsad"),
     "c3": dict(model="svoc-consensus N=256 D=4096 streaming (f=32, constrained)", N=256, D=4096, f=32,
-               batch=1024, update_frac=0.25),
+               batch=1024, update_frac=0.25, pipeline=2),
     "c2": dict(model="svoc-consensus N=64 D=1024 batched (f=8, constrained)", N=64, D=1024, f=8,
                batch=10000, update_frac=0.0),
     "c4": dict(model="sentiment oracles: BERT-base (12x768, bf16) on 30-comment windows -> 7 oracles x 6 dims",
@@ -54,6 +54,10 @@ def main():
     ap.add_argument("--batch", type=int, default=0, help="instances per GPU (default per config)")
     ap.add_argument("--wave-hint", type=int, default=0)
     ap.add_argument("--graph", type=int, default=1, help="capture the step in a HIP graph")
+    ap.add_argument("--pipeline", type=int, default=-1,
+                    help="streaming configs: overlap the update scatter of one instance range with the round "
+                         "of the previous one over K ranges (ConsensusEngine.step_pipelined); 1 = serial, "
+                         "-1 = the config's default")
     ap.add_argument("--mode", default=None, choices=["fast", "exact"],
                     help="override the config's engine mode (exact = bit-exact wsad int64 path)")
     ap.add_argument("--dshard", action="store_true",
@@ -153,6 +157,11 @@ def main():
         extra["state_bytes_per_instance"] = eng.bytes_per_instance(c["N"], c["D"], "fast") + 3 * 4 * 8 + 3 * 8 + 3 * (1 + 4 + 32) + c["N"] * 32
         extra["instances_per_288GB"] = int(288e9 // extra["state_bytes_per_instance"])
 
+    pipeline = args.pipeline if args.pipeline >= 0 else c.get("pipeline", 1)
+    if dshard or mode != "fast" or dev.type != "cuda":
+        pipeline = 1
+    extra["pipeline_chunks"] = pipeline
+
     def run_round():
         if dshard:
             run_round_sharded(eng, c["D"], world=world)   # includes the qr all-reduce
@@ -164,8 +173,11 @@ def main():
             pipe.fetch(*toks[i % 2])
         elif stream is not None:
             inst, orc, vals = stream.batch(i)
-            eng.apply_updates(inst, orc, vals, unique=True)   # the stream has distinct (instance, oracle)
-            run_round()
+            if pipeline > 1:   # the stream has distinct (instance, oracle), grouped by instance
+                eng.step_pipelined(inst, orc, vals, U_per_inst, chunks=pipeline)
+            else:
+                eng.apply_updates(inst, orc, vals, unique=True)
+                run_round()
         else:
             eng.touched.fill_(1)
             run_round()

@@ -139,6 +139,57 @@ class ConsensusEngine:
                                  self.metrics_fx)
         self.rounds += 1
 
+    def _run_round_range(self, b0: int, b1: int, only_touched: bool = True) -> None:
+        """run_round over instances [b0, b1) only (views of the state; fast mode)."""
+        sl = slice(b0, b1)
+        self._ops.round_prologue(self.n_active[sl], self.touched[sl], self.N, bool(only_touched), self._active[sl])
+        w = self.work()
+        if w is not None:
+            words = w.numel() // self.B
+            w = w[b0 * words:b1 * words]
+        self._ops.fast_round(self.values[sl], self._active[sl], self.D, self.cfg.n_failing_oracles,
+                             self.cfg.constrained, float(self.cfg.unconstrained_max_spread), self.c1[sl],
+                             self.consensus[sl], self.skew[sl], self.kurt[sl], self.rel[sl], self.qr[sl],
+                             self.reliable[sl], self.status[sl], self.wave_hint, 0, 0, self.cfg.legacy, w)
+        self._ops.round_epilogue(self._active[sl], self.status[sl], self.rel[sl], self.consensus_active[sl],
+                                 self.touched[sl], self.metrics_fx)
+
+    def step_pipelined(self, inst: torch.Tensor, oracle: torch.Tensor, vals: torch.Tensor,
+                       updates_per_instance: int, chunks: int = 2) -> None:
+        """apply_updates(unique=True) + run_round, pipelined over ``chunks`` instance ranges on HIP streams.
+
+        The update scatter is HBM-bound and the round kernel is latency-bound, so they overlap: the
+        updates of range k+1 (one update stream, in order) run while the round of range k runs on its
+        own stream.  The batch must be grouped by instance, ``updates_per_instance`` distinct oracles
+        per instance in instance order (SyntheticUpdateStream's layout).  Same results as
+        ``apply_updates(..., unique=True); run_round()`` (ranges are disjoint instances).  GPU fast mode
+        only; graph-capturable (fork/join through stream waits)."""
+        U = int(updates_per_instance)
+        if self.mode != "fast" or self.device.type != "cuda" or chunks <= 1:
+            self.apply_updates(inst, oracle, vals, unique=True)
+            self.run_round()
+            return
+        if inst.numel() != self.B * U:
+            raise ValueError("step_pipelined: expects updates_per_instance updates for every instance")
+        cur = torch.cuda.current_stream(self.device)
+        if getattr(self, "_pipe_streams", None) is None or len(self._pipe_streams) != chunks + 1:
+            self._pipe_streams = [torch.cuda.Stream(self.device) for _ in range(chunks + 1)]
+        su, sc = self._pipe_streams[0], self._pipe_streams[1:]
+        su.wait_stream(cur)
+        step = (self.B + chunks - 1) // chunks
+        for k in range(chunks):
+            b0, b1 = k * step, min(self.B, (k + 1) * step)
+            if b0 >= b1:
+                break
+            with torch.cuda.stream(su):
+                self.apply_updates(inst[b0 * U:b1 * U], oracle[b0 * U:b1 * U], vals[b0 * U:b1 * U], unique=True)
+            sc[k].wait_stream(su)
+            with torch.cuda.stream(sc[k]):
+                self._run_round_range(b0, b1)
+        for s in self._pipe_streams:
+            cur.wait_stream(s)
+        self.rounds += 1
+
     def work(self) -> Optional[torch.Tensor]:
         """Workspace of the one-network window kernel (34 window keys + 8 power sums + 2 cleanup
         list slots per column pair: 176 B per column pair and instance); None where that kernel does not run (CPU, small

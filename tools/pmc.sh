@@ -6,6 +6,7 @@ CFG=${CFG:-c2}
 SETS=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU"
       "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_ANY SQ_INSTS_SMEM SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE SQ_INST_LEVEL_LDS SQ_INSTS_VMEM")
 [ -n "${MEMSET:-}" ] && SETS+=("$MEMSET")
+[ -n "${MEMSET2:-}" ] && SETS+=("$MEMSET2")
 i=0
 for set in "${SETS[@]}"; do
   i=$((i+1))
