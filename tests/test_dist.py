@@ -1,4 +1,4 @@
-"""Multi-process paths on CPU with the gloo backend (world_size 2): DP and D-sharding."""
+"""Multi-process paths on CPU with the gloo backend (world sizes 2 and 4): DP and D-sharding."""
 import os
 import socket
 import tempfile
@@ -46,20 +46,21 @@ def _dp_worker(rank, world, port, outdir):
     dist.destroy_process_group()
 
 
-def test_data_parallel_gloo():
-    world = 2
+@pytest.mark.parametrize("world", [2, 4])
+def test_data_parallel_gloo(world):
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_dp_worker, args=(world, _free_port(), d), nprocs=world, join=True)
         r = [torch.load(os.path.join(d, f"dp{i}.pt"), weights_only=True) for i in range(world)]
-    assert torch.equal(r[0]["g"], r[1]["g"])
-    assert r[0]["g"][2].item() == 6            # 2 ranks x 3 instances processed
+    for k in range(1, world):
+        assert torch.equal(r[0]["g"], r[k]["g"])
+    assert r[0]["g"][2].item() == 3 * world            # world ranks x 3 instances processed
     # rel2 sum over committed rounds (fixed-point 2^-32 counters, all-reduced as integers)
-    rel2 = torch.cat([r[0]["rel"][:, 1], r[1]["rel"][:, 1]]).double().sum().item()
-    assert abs(r[0]["g"][0].item() - rel2) < 1e-6 and r[0]["g"][1].item() == 6
+    rel2 = torch.cat([r[k]["rel"][:, 1] for k in range(world)]).double().sum().item()
+    assert abs(r[0]["g"][0].item() - rel2) < 1e-6 and r[0]["g"][1].item() == 3 * world
     full = r[0]["summ"]["consensus"]
-    assert torch.allclose(full[:3].float(), r[0]["local"].float())
-    assert torch.allclose(full[3:].float(), r[1]["local"].float())
-    assert r[1]["ids"].tolist() == [3, 4, 5]
+    for k in range(world):
+        assert torch.allclose(full[3 * k:3 * k + 3].float(), r[k]["local"].float())
+        assert r[k]["ids"].tolist() == [3 * k, 3 * k + 1, 3 * k + 2]
 
 
 def _ds_worker(rank, world, port, outdir, x, cfgd):
@@ -80,15 +81,14 @@ def _ds_worker(rank, world, port, outdir, x, cfgd):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("constrained", [True, False])
-def test_dsharding_matches_single_process(constrained):
+@pytest.mark.parametrize("constrained,world", [(True, 2), (False, 2), (True, 4)])
+def test_dsharding_matches_single_process(constrained, world):
     from helpers import beta_oracles, run_fast
     B, N, D, f = 4, 32, 40, 4
     x, _ = beta_oracles(B, N, D, f, seed=11)
     x = x[:, :, :D].contiguous()
     ref = run_fast(x, D, f, constrained, 1.0)
     cfgd = dict(n_oracles=N, dimension=D, n_failing_oracles=f, constrained=constrained, unconstrained_max_spread=1.0)
-    world = 2
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_ds_worker, args=(world, _free_port(), d, x, cfgd), nprocs=world, join=True)
         r = [torch.load(os.path.join(d, f"ds{i}.pt"), weights_only=True) for i in range(world)]
