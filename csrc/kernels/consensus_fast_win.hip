@@ -131,6 +131,54 @@ SVOC_DEV void qr_moments(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t m
                                      std::make_integer_sequence<int, 64 / P>{});
 }
 
+// qr pass with half of the slab staged in LDS (N = NPAD = 256, constrained): trees 0 and 1 (rows
+// i % 4 < 2, 32 rows) were written to the wave's LDS region as keys right after the pass-1 load; trees
+// 2 and 3 (32 rows) are re-read from memory, all 32 loads issued first so their latency overlaps the
+// LDS trees.  Same trees, same order of accumulation as qr_moments: bit-identical results.
+template <int P, bool MASKW>
+SVOC_DEV void qr_moments_staged(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, uint32_t kp,
+                                const uint32_t* st, int lane, const QrCtx& c, float* acc, f32x2& s1, f32x2& s2,
+                                f32x2& s3, f32x2& s4) {
+  static_assert(P == 16, "staging layout: KEEP = 4 trees of 16 rows");
+  constexpr int KEEP = 4, S = 4;
+  uint32_t wm[64];   // trees 2 and 3 from memory (indices i % 4 >= 2)
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    wm[2 + KEEP * m] = bload(rs, vo, (2 + KEEP * m) * rowb);
+    wm[3 + KEEP * m] = bload(rs, vo, (3 + KEEP * m) * rowb);
+  }
+  {
+    uint32_t wv[64];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      wv[KEEP * m] = st[(2 * m) * 64 + lane] ^ kp;
+      if (MASKW) wv[KEEP * m] &= mW;
+    }
+    acc[0] += qr_tree<S, 0, P, false>(c, wv, s1, s2, s3, s4);
+    asm volatile("" : "+v"(acc[0]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
+  }
+  {
+    uint32_t wv[64];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      wv[1 + KEEP * m] = st[(2 * m + 1) * 64 + lane] ^ kp;
+      if (MASKW) wv[1 + KEEP * m] &= mW;
+    }
+    acc[1] += qr_tree<S, 1, P, false>(c, wv, s1, s2, s3, s4);
+    asm volatile("" : "+v"(acc[1]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
+  }
+  if (MASKW) {
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      wm[2 + KEEP * m] &= mW;
+      wm[3 + KEEP * m] &= mW;
+    }
+  }
+  acc[2] += qr_tree<S, 2, P, false>(c, wm, s1, s2, s3, s4);
+  asm volatile("" : "+v"(acc[2]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
+  acc[3] += qr_tree<S, 3, P, false>(c, wm, s1, s2, s3, s4);
+}
+
 template <int NSEG, int WAVES, int H, bool CONS, int MODE>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4))) void consensus_fast_win_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // column pairs per wave (phase A)
@@ -138,6 +186,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   constexpr int W = WAVES * P * 2;      // columns per workgroup step (phase A)
   constexpr int NT = WAVES * 64;
   constexpr int KEEP = 64 / P;
+  // N = 256 constrained: half of each slab (32 rows x 64 lanes, keys) staged per wave for the qr pass
+  constexpr bool STAGE = CONS && NSEG == 4 && MODE != 2;
+  __shared__ uint32_t stage[STAGE ? WAVES * 32 * 64 : 1];
   __shared__ float qr_part[WAVES * NPAD];
   __shared__ float qr_lds[NPAD];
   __shared__ uint64_t relmask[4];
@@ -168,6 +219,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   const int nl = N + lo1 - seg * 64;
   const int seg_off = seg * 64 * rowb;
   const uint32_t pol = group_polarity<NSEG>(seg);
+  const uint32_t kp = 0x80008000u ^ pol;   // constrained key = raw ^ kp
+  uint32_t* const stw = stage + (STAGE ? wave * 32 * 64 : 0);
 
   float acc[KEEP];
 #pragma unroll
@@ -189,9 +242,15 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
       u16x2 r[64];
       if (N == NPAD) {
         if (CONS) {
-          const uint32_t kp = 0x80008000u ^ pol;
 #pragma unroll
           for (int i = 0; i < 64; ++i) r[i] = as_k(bload(rs, vo, i * rowb) ^ kp);
+          if constexpr (STAGE) {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+              stw[(2 * m) * 64 + lane] = as_u32(r[4 * m]);
+              stw[(2 * m + 1) * 64 + lane] = as_u32(r[4 * m + 1]);
+            }
+          }
         } else {
 #pragma unroll
           for (int i = 0; i < 64; ++i) r[i] = as_k(as_u32(to_key<CONS>(bload(rs, vo, i * rowb))) ^ pol);
@@ -239,7 +298,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
     asm volatile("" : "+v"(vo2) : "v"(cA), "v"(cB));
     const QrCtx qc{nvl, lane, f32x2{vA ? cA : 0.f, vB ? cB : 0.f}};
     f32x2 s1 = {0.f, 0.f}, s2 = s1, s3 = s1, s4 = s1;
-    if ((s + 1) * W <= D) {
+    if (STAGE && N == NPAD) {
+      if constexpr (STAGE) {
+        if ((s + 1) * W <= D) qr_moments_staged<P, false>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
+        else qr_moments_staged<P, true>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
+      }
+    } else if ((s + 1) * W <= D) {
       if (N == NPAD) qr_moments<P, false, false>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
       else qr_moments<P, false, true>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
     } else {
