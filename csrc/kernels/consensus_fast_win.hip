@@ -179,6 +179,33 @@ SVOC_DEV void qr_moments_staged(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uin
   acc[3] += qr_tree<S, 3, P, false>(c, wm, s1, s2, s3, s4);
 }
 
+// qr pass with half of the slab staged in LDS for N <= 64 (NSEG 1, constrained; the KEEP = 2 form is
+// kept compiling but not used): the even rows (tree 0 when KEEP = 2; the first butterfly half of the
+// single tree when KEEP = 1) come from the wave's
+// LDS region, the odd rows are re-read from memory with all 32 loads issued before the LDS reads.
+// Same trees, same leaf order as qr_moments: bit-identical results.
+template <int P, bool MASKW>
+SVOC_DEV void qr_moments_staged_even(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, uint32_t kp,
+                                     const uint32_t* st, int lane, const QrCtx& c, float* acc, f32x2& s1,
+                                     f32x2& s2, f32x2& s3, f32x2& s4) {
+  constexpr int KEEP = 64 / P, S = __builtin_ctz(P);
+  static_assert(KEEP <= 2, "even-row staging: one or two trees");
+  uint32_t wv[64];
+#pragma unroll
+  for (int m = 0; m < 32; ++m) wv[2 * m + 1] = bload(rs, vo, (2 * m + 1) * rowb);
+#pragma unroll
+  for (int m = 0; m < 32; ++m) wv[2 * m] = st[m * 64 + lane] ^ kp;
+  if (MASKW) {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) wv[i] &= mW;
+  }
+  acc[0] += qr_tree<S, 0, P, false>(c, wv, s1, s2, s3, s4);
+  if constexpr (KEEP == 2) {
+    asm volatile("" : "+v"(acc[0]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
+    acc[1] += qr_tree<S, 1, P, false>(c, wv, s1, s2, s3, s4);
+  }
+}
+
 template <int NSEG, int WAVES, int H, bool CONS, int MODE>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4))) void consensus_fast_win_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // column pairs per wave (phase A)
@@ -186,8 +213,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   constexpr int W = WAVES * P * 2;      // columns per workgroup step (phase A)
   constexpr int NT = WAVES * 64;
   constexpr int KEEP = 64 / P;
-  // N = 256 constrained: half of each slab (32 rows x 64 lanes, keys) staged per wave for the qr pass
-  constexpr bool STAGE = CONS && NSEG == 4 && MODE != 2;
+  // constrained: half of each slab (32 rows x 64 lanes, keys) staged per wave for the qr pass
+  // (N = 256: rows i % 4 < 2; N <= 64: even rows).  Not for N <= 128 (NSEG 2): measured 21% slower
+  // there (profiles/r1_stage_ab.txt), the old two-tree re-read keeps fewer words live.
+  constexpr bool STAGE = CONS && NSEG != 2 && MODE != 2;
   __shared__ uint32_t stage[STAGE ? WAVES * 32 * 64 : 1];
   __shared__ float qr_part[WAVES * NPAD];
   __shared__ float qr_lds[NPAD];
@@ -244,12 +273,15 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
         if (CONS) {
 #pragma unroll
           for (int i = 0; i < 64; ++i) r[i] = as_k(bload(rs, vo, i * rowb) ^ kp);
-          if constexpr (STAGE) {
+          if constexpr (STAGE && NSEG == 4) {
 #pragma unroll
             for (int m = 0; m < 16; ++m) {
               stw[(2 * m) * 64 + lane] = as_u32(r[4 * m]);
               stw[(2 * m + 1) * 64 + lane] = as_u32(r[4 * m + 1]);
             }
+          } else if constexpr (STAGE) {
+#pragma unroll
+            for (int m = 0; m < 32; ++m) stw[m * 64 + lane] = as_u32(r[2 * m]);
           }
         } else {
 #pragma unroll
@@ -299,9 +331,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
     const QrCtx qc{nvl, lane, f32x2{vA ? cA : 0.f, vB ? cB : 0.f}};
     f32x2 s1 = {0.f, 0.f}, s2 = s1, s3 = s1, s4 = s1;
     if (STAGE && N == NPAD) {
-      if constexpr (STAGE) {
+      if constexpr (STAGE && NSEG == 4) {
         if ((s + 1) * W <= D) qr_moments_staged<P, false>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
         else qr_moments_staged<P, true>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
+      } else if constexpr (STAGE) {
+        if ((s + 1) * W <= D) qr_moments_staged_even<P, false>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
+        else qr_moments_staged_even<P, true>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
       }
     } else if ((s + 1) * W <= D) {
       if (N == NPAD) qr_moments<P, false, false>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
