@@ -179,9 +179,9 @@ SVOC_DEV void qr_moments_staged(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uin
   acc[3] += qr_tree<S, 3, P, false>(c, wm, s1, s2, s3, s4);
 }
 
-// qr pass with half of the slab staged in LDS for N <= 64 (NSEG 1, constrained; the KEEP = 2 form is
-// kept compiling but not used): the even rows (tree 0 when KEEP = 2; the first butterfly half of the
-// single tree when KEEP = 1) come from the wave's
+// qr pass with half of the slab staged in LDS for N <= 128 (NSEG 1 and 2, constrained): the even rows
+// (tree 0 when KEEP = 2, read into its own array so only that tree's words are live next to the 32
+// in-flight loads; the first butterfly half of the single tree when KEEP = 1) come from the wave's
 // LDS region, the odd rows are re-read from memory with all 32 loads issued before the LDS reads.
 // Same trees, same leaf order as qr_moments: bit-identical results.
 template <int P, bool MASKW>
@@ -190,19 +190,36 @@ SVOC_DEV void qr_moments_staged_even(__amdgpu_buffer_rsrc_t rs, int vo, int rowb
                                      f32x2& s2, f32x2& s3, f32x2& s4) {
   constexpr int KEEP = 64 / P, S = __builtin_ctz(P);
   static_assert(KEEP <= 2, "even-row staging: one or two trees");
-  uint32_t wv[64];
+  if constexpr (KEEP == 1) {
+    uint32_t wv[64];
 #pragma unroll
-  for (int m = 0; m < 32; ++m) wv[2 * m + 1] = bload(rs, vo, (2 * m + 1) * rowb);
+    for (int m = 0; m < 32; ++m) wv[2 * m + 1] = bload(rs, vo, (2 * m + 1) * rowb);
 #pragma unroll
-  for (int m = 0; m < 32; ++m) wv[2 * m] = st[m * 64 + lane] ^ kp;
-  if (MASKW) {
+    for (int m = 0; m < 32; ++m) wv[2 * m] = st[m * 64 + lane] ^ kp;
+    if (MASKW) {
 #pragma unroll
-    for (int i = 0; i < 64; ++i) wv[i] &= mW;
-  }
-  acc[0] += qr_tree<S, 0, P, false>(c, wv, s1, s2, s3, s4);
-  if constexpr (KEEP == 2) {
-    asm volatile("" : "+v"(acc[0]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
-    acc[1] += qr_tree<S, 1, P, false>(c, wv, s1, s2, s3, s4);
+      for (int i = 0; i < 64; ++i) wv[i] &= mW;
+    }
+    acc[0] += qr_tree<S, 0, P, false>(c, wv, s1, s2, s3, s4);
+  } else {
+    uint32_t wm[64];   // tree 1 (odd rows) from memory, loads issued first
+#pragma unroll
+    for (int m = 0; m < 32; ++m) wm[2 * m + 1] = bload(rs, vo, (2 * m + 1) * rowb);
+    {
+      uint32_t wv[64];
+#pragma unroll
+      for (int m = 0; m < 32; ++m) {
+        wv[2 * m] = st[m * 64 + lane] ^ kp;
+        if (MASKW) wv[2 * m] &= mW;
+      }
+      acc[0] += qr_tree<S, 0, P, false>(c, wv, s1, s2, s3, s4);
+      asm volatile("" : "+v"(acc[0]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
+    }
+    if (MASKW) {
+#pragma unroll
+      for (int m = 0; m < 32; ++m) wm[2 * m + 1] &= mW;
+    }
+    acc[1] += qr_tree<S, 1, P, false>(c, wm, s1, s2, s3, s4);
   }
 }
 
@@ -214,9 +231,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   constexpr int NT = WAVES * 64;
   constexpr int KEEP = 64 / P;
   // constrained: half of each slab (32 rows x 64 lanes, keys) staged per wave for the qr pass
-  // (N = 256: rows i % 4 < 2; N <= 64: even rows).  Not for N <= 128 (NSEG 2): measured 21% slower
-  // there (profiles/r1_stage_ab.txt), the old two-tree re-read keeps fewer words live.
-  constexpr bool STAGE = CONS && NSEG != 2 && MODE != 2;
+  // (N = 256: rows i % 4 < 2; N <= 128: even rows; profiles/r1_stage_ab.txt)
+  constexpr bool STAGE = CONS && MODE != 2;
   __shared__ uint32_t stage[STAGE ? WAVES * 32 * 64 : 1];
   __shared__ float qr_part[WAVES * NPAD];
   __shared__ float qr_lds[NPAD];
