@@ -44,6 +44,22 @@ CONFIGS = {
 METRIC = "consensus updates/sec (N oracles x D dims, batched)"
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _launch_ranks(n: int) -> int:
+    """Re-run this script as ``n`` ranks under torch.distributed.run (rendezvous on 127.0.0.1)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -69,7 +85,13 @@ def main():
                     "after the timed region and add the per-kernel table to the log record")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start N ranks (one process per GPU) under
+        # torch.distributed.run as a child and exit with its code.  Nothing here has touched the GPU.
+        sys.exit(_launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.config_file:

@@ -86,3 +86,23 @@ def test_bench_two_ranks_dp_and_dshard_gloo(tmp_path):
     ds = _run_dist(["--config-file", cfg, "--gpus", "2", "--steps", "4", "--warmup", "1", "--dshard"])
     assert ds["scaling"] == "strong" and ds["config"]["parallelism"] == "dshard2"
     assert ds["config"]["global_batch"] == 8 and ds["config"]["ok_fraction"] == 1.0
+
+
+def test_bench_gpus_flag_spawns_ranks_gloo(tmp_path):
+    """The driver's plain form `python bench.py --gpus 2` (no launcher) starts two ranks itself."""
+    cfg = _cpu_cfg(tmp_path)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config-file", cfg, "--gpus", "2",
+                        "--steps", "3", "--warmup", "1"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout          # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 16
+
+
+def test_bench_gpus_world_mismatch_fails(tmp_path):
+    cfg = _cpu_cfg(tmp_path)
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config-file", cfg, "--gpus", "2",
+                        "--steps", "2", "--warmup", "0"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
