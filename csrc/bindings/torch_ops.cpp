@@ -118,6 +118,9 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
   TORCH_CHECK(ld % 8 == 0, "row stride (ld) must be a multiple of 8 bf16 (16 B)");
   TORCH_CHECK(((uintptr_t)values.data_ptr() & 15) == 0 && values.stride(0) % 8 == 0, "values must be 16-B aligned");
   TORCH_CHECK(B < (1ll << 31) && D < (1 << 30), "size limits");
+  // the kernels address one instance with 32-bit buffer offsets (rows x ld x 2 B, workspace x 4 B)
+  TORCH_CHECK(N * ld * 2 < (1ll << 31) && fast_work_words(D) * 4 < (1ll << 31),
+              "instance too large for 32-bit buffer offsets (N * ld * 2 B and the workspace must stay < 2 GiB)");
   FastParams p{};
   p.values = values.data_ptr();
   p.active = active_ptr(active, B, values.device());
@@ -149,9 +152,11 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
     TORCH_CHECK(work->numel() >= fast_work_numel(B, D), "work: needs ", fast_work_numel(B, D),
                 " elements (svoc.ops.fast_work_numel)");
     p.work = (uint32_t*)work->data_ptr();
-  } else if (mode == 0 && (N > 16 || D > 128) && n_failing <= 32) {
+  } else if (mode != 1 && !(mode == 0 && wave_hint == 0 && N <= 16 && D <= 128)) {
+    // a temporary one: every kernel but the small-instance one stages its pass-2 outputs there
     wtmp = at::empty({fast_work_numel(B, D)}, values.options().dtype(at::kInt));
     p.work = (uint32_t*)wtmp.data_ptr();
+    p.work_fresh = 1;
   }
   {
     const char* wc = std::getenv("SVOC_WIN_CANCEL");   // tests / experiments: force or avoid the cleanup

@@ -9,6 +9,10 @@
 // every CRC before handing bytes back (a torn or corrupted checkpoint fails loudly).
 #include "svoc_io.hpp"
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -41,7 +45,23 @@ struct File {
   void r(void* p, size_t n) {
     if (n && std::fread(p, 1, n, f) != n) throw std::runtime_error("svoc_io: truncated file");
   }
+  uint64_t remaining() {   // bytes between the read position and the end of the file
+    const long pos = std::ftell(f);
+    struct stat st;
+    if (pos < 0 || fstat(fileno(f), &st) != 0 || st.st_size < pos) throw std::runtime_error("svoc_io: cannot stat");
+    return (uint64_t)(st.st_size - pos);
+  }
 };
+
+// fsync of a path's parent directory (the rename itself must be durable too)
+void sync_dir(const std::string& path) {
+  const size_t k = path.find_last_of('/');
+  const std::string dir = k == std::string::npos ? "." : (k == 0 ? "/" : path.substr(0, k));
+  const int fd = ::open(dir.c_str(), O_RDONLY | O_DIRECTORY);
+  if (fd < 0) return;   // best effort: some filesystems refuse directory handles
+  ::fsync(fd);
+  ::close(fd);
+}
 
 template <class T>
 void wv(File& f, T v) { f.w(&v, sizeof(T)); }
@@ -87,9 +107,13 @@ void save(const std::string& path, const std::string& meta, const std::vector<Se
       wv<uint32_t>(f, crc32(s.bytes.data(), s.bytes.size()));
       f.w(s.bytes.data(), s.bytes.size());
     }
+    // crash safety: the data must be on disk before the rename publishes it, else a power loss can
+    // leave the new name pointing at a truncated file in place of the previous good checkpoint
     if (std::fflush(f.f) != 0) throw std::runtime_error("svoc_io: flush failed");
+    if (::fsync(fileno(f.f)) != 0) throw std::runtime_error("svoc_io: fsync failed");
   }
   if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("svoc_io: rename failed");
+  sync_dir(path);
 }
 
 std::string load(const std::string& path, std::vector<Section>& secs) {
@@ -100,6 +124,7 @@ std::string load(const std::string& path, std::vector<Section>& secs) {
   if (rv<uint32_t>(f) != 1) throw std::runtime_error("svoc_io: unsupported version");
   const uint32_t n = rv<uint32_t>(f);
   const uint32_t ml = rv<uint32_t>(f);
+  if (ml > f.remaining()) throw std::runtime_error("svoc_io: corrupt metadata length");
   std::string meta(ml, '\0');
   f.r(&meta[0], ml);
   secs.clear();
@@ -111,14 +136,22 @@ std::string load(const std::string& path, std::vector<Section>& secs) {
     f.r(&s.name[0], nl);
     s.dtype = (DType)rv<uint8_t>(f);
     const uint8_t nd = rv<uint8_t>(f);
-    size_t numel = 1;
+    const size_t es = elem_size(s.dtype);
+    if (es == 0 || nd > 8) throw std::runtime_error("svoc_io: corrupt section header in " + s.name);
+    uint64_t numel = 1;
     for (int k = 0; k < nd; ++k) {
-      s.shape.push_back((int64_t)rv<uint64_t>(f));
-      numel *= (size_t)s.shape.back();
+      const uint64_t d = rv<uint64_t>(f);
+      if (d > (uint64_t)INT64_MAX || __builtin_mul_overflow(numel, d, &numel))
+        throw std::runtime_error("svoc_io: shape overflow in " + s.name);
+      s.shape.push_back((int64_t)d);
     }
+    uint64_t want;
+    if (__builtin_mul_overflow(numel, (uint64_t)es, &want)) throw std::runtime_error("svoc_io: shape overflow in " + s.name);
     const uint64_t nb = rv<uint64_t>(f);
-    if (nb != numel * elem_size(s.dtype)) throw std::runtime_error("svoc_io: size mismatch in " + s.name);
+    if (nb != want) throw std::runtime_error("svoc_io: size mismatch in " + s.name);
     const uint32_t crc = rv<uint32_t>(f);
+    // never allocate more than the file still holds (a corrupt header must fail, not exhaust memory)
+    if (nb > f.remaining()) throw std::runtime_error("svoc_io: truncated file in " + s.name);
     s.bytes.resize(nb);
     f.r(s.bytes.data(), nb);
     if (crc32(s.bytes.data(), nb) != crc) throw std::runtime_error("svoc_io: CRC mismatch in " + s.name);

@@ -35,6 +35,27 @@ SVOC_DEV float bloadf(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
 
+// Staged pass-2 outputs (launch.hpp, fast_work_words): [3][D2] floats (consensus, skewness,
+// kurtosis) at byte offset `stg` of the instance's workspace.
+SVOC_DEV void stage_out(__amdgpu_buffer_rsrc_t ws, int stg, int D2, int which, int col, float v) {
+  bstore(ws, __builtin_bit_cast(uint32_t, v), col * 4, stg + which * D2 * 4);
+}
+// Copy of the staged outputs of one instance to consensus / skew / kurt (the round's status is OK),
+// by all NT threads of the workgroup after a barrier.  sc0 loads: the words were stored by other
+// waves of this workgroup (workgroup-scope coherence, as in the LLVM AMDGPU memory model).
+template <int NT>
+SVOC_DEV void commit_staged(__amdgpu_buffer_rsrc_t ws, int stg, int D2, int D, int tid, float* cons, float* skew,
+                            float* kurt) {
+  for (int c = tid; c < D; c += NT) {
+    const uint32_t a = __builtin_amdgcn_raw_buffer_load_b32(ws, c * 4, stg, 1);
+    const uint32_t s = __builtin_amdgcn_raw_buffer_load_b32(ws, c * 4, stg + D2 * 4, 1);
+    const uint32_t k = __builtin_amdgcn_raw_buffer_load_b32(ws, c * 4, stg + 2 * D2 * 4, 1);
+    cons[c] = __builtin_bit_cast(float, a);
+    skew[c] = __builtin_bit_cast(float, s);
+    kurt[c] = __builtin_bit_cast(float, k);
+  }
+}
+
 // Sort keys of two bf16 columns: constrained values ([0, 1]) by one XOR, general bf16 otherwise.
 template <bool CONS>
 SVOC_DEV u16x2 to_key(uint32_t raw) {

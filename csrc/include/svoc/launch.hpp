@@ -26,18 +26,25 @@ struct FastParams {
   uint8_t* reliable;        // [B, N]
   int32_t* status;          // [B]
   int legacy;               // obsolete-contract variant: reliability without /D, no moments (C30/C31)
-  // window kernel workspace (consensus_fast_win.hip): per instance [H][2][work_pairs] window keys +
-  // [4][work_pairs] float2 all-row power sums + a [2 work_pairs] cleanup column list; null = the
-  // two-network kernels
+  // workspace (layout: fast_work_words below); required by every kernel but the small-instance one
   uint32_t* work;
   int work_pairs;           // column pairs per instance in `work` (multiple of 256, >= ceil(D / 2))
   int64_t work_stride;      // u32 words per instance in `work`
   float win_cancel;         // window kernel: max all-row / reliable power-sum ratio trusted (else cleanup)
+  int work_fresh;           // the workspace holds no pass-1 state (mode 2 must not use the window kernel)
 };
 
-// Workspace words per instance for the window kernel (H = 17 upper bound; see consensus_fast_win.hip).
+// Workspace per instance of the LDS-free fast kernels, in u32 words (Dp = fast_work_pairs(D)):
+//   [17][2][Dp]  window keys (consensus_fast_win.hip; H = 17 upper bound)
+//   [4][Dp]      float2 all-row power sums
+//   [2 Dp]       cleanup column list
+//   [3][2 Dp]    staged pass-2 outputs (consensus, skewness, kurtosis): a round writes them here and
+//                copies them to the outputs only once its status is known to be OK, so a reverted
+//                round leaves every output untouched (contract.cairo:588-603: a failed assert
+//                reverts the whole transaction)
 inline int64_t fast_work_pairs(int64_t D) { return ((D + 1) / 2 + 255) / 256 * 256; }
-inline int64_t fast_work_words(int64_t D) { return fast_work_pairs(D) * (2 * 17 + 8 + 2); }
+inline int64_t fast_work_stage_word(int64_t D) { return fast_work_pairs(D) * (2 * 17 + 8 + 2); }
+inline int64_t fast_work_words(int64_t D) { return fast_work_pairs(D) * (2 * 17 + 8 + 2 + 6); }
 inline int64_t fast_work_numel(int64_t B, int64_t D) { return B * fast_work_words(D); }
 
 struct ExactParams {

@@ -21,11 +21,13 @@
 //   * pass 2 re-sorts each column with unreliable rows forced to the max key and reads moments as
 //     shifted power sums (one LDS pass).  When the whole instance fits in one slab the LDS tile is
 //     reused and the instance is read from HBM exactly once.
-// Reverts (rel outside [0,1], too few reliable rows) leave every output of the instance untouched
-// and only set status[b]; zero variance is a non-fatal flag in fast mode (skew = kurt = 0).
+// Reverts (rel outside [0,1], too few reliable rows, a zero-variance reliable column) leave every
+// output of the instance untouched and only set status[b]: pass 2 stages its outputs in the
+// workspace and copies them out once the status is final (contract.cairo:588-603).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "svoc/bufload.hpp"
 #include "svoc/launch.hpp"
 #include "svoc/sortnet.hpp"
 #include "svoc/status.hpp"
@@ -278,10 +280,10 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
     if (tid == 0) p.status[b] = misc_i[0];
     return;  // revert: outputs untouched
   }
-  if (tid < N) {
-    p.reliable[(int64_t)b * N + tid] = (relmask[tid >> 6] >> (tid & 63)) & 1;
-    p.qr[(int64_t)b * N + tid] = qr_lds[tid];
-  }
+  // pass-2 outputs are staged in the workspace and committed at the end once the status is final
+  const int Dp = p.work_pairs, D2 = 2 * Dp;
+  const int STG = Dp * (2 * 17 + 8 + 2) * 4;   // launch.hpp: fast_work_stage_word
+  const __amdgpu_buffer_rsrc_t ws = instance_rsrc(p.work + (int64_t)b * p.work_stride, (uint32_t)(p.work_stride * 4));
   const float n = (float)R;
   const int m2 = R >> 1;
   // reliable rows held by this lane after the masked sort: sorted positions [0, cnt)
@@ -380,19 +382,29 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_bf16_kernel(FastPar
         } else {
           zv = true;
         }
-        const int64_t o = (int64_t)b * D + colA + h;
-        p.consensus[o] = CONS ? sh : sh + dl;
-        p.skew[o] = p.legacy ? 0.f : sk;
-        p.kurt[o] = p.legacy ? 0.f : ku;
+        stage_out(ws, STG, D2, 0, colA + h, CONS ? sh : sh + dl);
+        stage_out(ws, STG, D2, 1, colA + h, p.legacy ? 0.f : sk);
+        stage_out(ws, STG, D2, 2, colA + h, p.legacy ? 0.f : ku);
       }
       if (zv && !p.legacy) misc_i[1] = 1;
     }
   }
   __syncthreads();
+  // ------------------------------------------------------------ commit (only a successful round)
+  if (misc_i[1]) {
+    if (tid == 0) p.status[b] = ST_ZERO_VARIANCE;
+    return;
+  }
+  const int64_t ob = (int64_t)b * D;
+  commit_staged<G::NT>(ws, STG, D2, D, tid, p.consensus + ob, p.skew + ob, p.kurt + ob);
+  if (tid < N) {
+    p.reliable[(int64_t)b * N + tid] = (relmask[tid >> 6] >> (tid & 63)) & 1;
+    p.qr[(int64_t)b * N + tid] = qr_lds[tid];
+  }
   if (tid == 0) {
     p.rel[2 * (int64_t)b] = misc_f[0];
     p.rel[2 * (int64_t)b + 1] = misc_f[1];
-    p.status[b] = misc_i[1] ? ST_ZERO_VARIANCE : ST_OK;
+    p.status[b] = ST_OK;
   }
 }
 
@@ -420,8 +432,8 @@ extern "C" int svoc_fast_round_bf16_win(const FastParams* p, hipStream_t stream)
 
 extern "C" int svoc_fast_round_bf16(const FastParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
-  // default (0) and negative hints: register-streaming kernel (consensus_fast_reg.hip; -1 = split
-  // into two launches).  Positive hints select this LDS-tiled kernel (1 = its default geometry).
+  // default (0) and negative hints: register-streaming kernel (consensus_fast_reg.hip).  Positive
+  // hints select this LDS-tiled kernel (1 = its default geometry).
   // small instances (N <= 16, D <= 128, full round): several instances per wave, registers only
   if (p->wave_hint == 0 && p->mode == 0 && p->N <= 16 && p->D <= 128) return svoc_fast_round_bf16_small(p, stream);
   // default: one-network window kernel (consensus_fast_win.hip) when it applies (workspace given,
@@ -437,6 +449,8 @@ extern "C" int svoc_fast_round_bf16(const FastParams* p, hipStream_t stream) {
   }
   if (p->wave_hint <= 0) return svoc_fast_round_bf16_reg(p, stream);
   if (p->N < 2 || p->N > 256 || p->ld % 8 != 0 || p->D > p->ld) return -1;
+  if (p->mode != 1 && (!p->work || p->work_pairs < fast_work_pairs(p->D) || p->work_stride < fast_work_words(p->D)))
+    return -1;   // pass 2 stages its outputs in the workspace
   if (p->N <= 64) {
     // wave_hint: 2 / 4 / 8 waves per workgroup = 256 / 512 / 1024-column slabs (32/64/128 KiB LDS)
     if (p->wave_hint == 2) return launch_fast<1, 2>(*p, stream);

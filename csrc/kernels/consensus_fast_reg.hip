@@ -18,9 +18,8 @@
 
 namespace svoc {
 
-// MODE 0: fused round; 1: pass 1 only (c1 + qr -> global); 2: rank + pass 2 from the global qr.
-// The default launch runs MODE 1 then MODE 2: each half gets its own register allocation (~110
-// VGPRs instead of ~230 for the fused body), i.e. twice the resident waves per SIMD.
+// MODE 0: fused round; 1: pass 1 only (c1 + qr -> global); 2: rank + pass 2 from the global qr
+// (D-sharding: the caller all-reduces the qr partials in between).
 template <int NSEG, int WAVES, bool CONS, int MODE, bool RAW = false>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW ? 2 : 4))) void consensus_fast_reg_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // column pairs per wave
@@ -250,10 +249,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW 
     if (tid == 0) p.status[b] = misc_i[0];
     return;
   }
-  for (int t = tid; t < N; t += NT) {
-    p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
-    p.qr[(int64_t)b * N + t] = qr_lds[t];
-  }
+  // pass-2 outputs are staged in the workspace and committed at the end once the status is final
+  const int Dp = p.work_pairs, D2 = 2 * Dp;
+  const int STG = Dp * (2 * 17 + 8 + 2) * 4;   // launch.hpp: fast_work_stage_word
+  const __amdgpu_buffer_rsrc_t ws = instance_rsrc(p.work + (int64_t)b * p.work_stride, (uint32_t)(p.work_stride * 4));
   const float n = (float)R;
   const uint64_t mymask = relmask[seg];
   const uint64_t mylow = lowmask[seg];
@@ -341,19 +340,29 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW 
         } else {
           zv = true;
         }
-        const int64_t o = (int64_t)b * D + colA + h;
-        p.consensus[o] = CONS ? med : sh + dl;
-        p.skew[o] = p.legacy ? 0.f : sk;
-        p.kurt[o] = p.legacy ? 0.f : ku;
+        stage_out(ws, STG, D2, 0, colA + h, CONS ? med : sh + dl);
+        stage_out(ws, STG, D2, 1, colA + h, p.legacy ? 0.f : sk);
+        stage_out(ws, STG, D2, 2, colA + h, p.legacy ? 0.f : ku);
       }
       if (zv && !p.legacy) misc_i[1] = 1;
     }
   }
   __syncthreads();
+  // ------------------------------------------------------------ commit (only a successful round)
+  if (misc_i[1]) {
+    if (tid == 0) p.status[b] = ST_ZERO_VARIANCE;
+    return;
+  }
+  const int64_t ob = (int64_t)b * D;
+  commit_staged<NT>(ws, STG, D2, D, tid, p.consensus + ob, p.skew + ob, p.kurt + ob);
+  for (int t = tid; t < N; t += NT) {
+    p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
+    p.qr[(int64_t)b * N + t] = qr_lds[t];
+  }
   if (tid == 0) {
     p.rel[2 * (int64_t)b] = misc_f[0];
     p.rel[2 * (int64_t)b + 1] = misc_f[1];
-    p.status[b] = misc_i[1] ? ST_ZERO_VARIANCE : ST_OK;
+    p.status[b] = ST_OK;
   }
 }
 
@@ -372,11 +381,10 @@ static int launch_reg(const FastParams& p, hipStream_t stream) {
     launch_reg_mode<NSEG, WAVES, 2>(p, stream);
   } else if (p.wave_hint == -6) {
     launch_reg_mode<NSEG, WAVES, 0, true>(p, stream);  // fused, raw words kept in VGPRs (no re-read)
-  } else if (p.wave_hint != -1) {
-    launch_reg_mode<NSEG, WAVES, 0>(p, stream);  // fused single launch (default)
   } else {
-    launch_reg_mode<NSEG, WAVES, 1>(p, stream);  // split: pass 1 ...
-    launch_reg_mode<NSEG, WAVES, 2>(p, stream);  // ... then rank + pass 2
+    // fused single launch.  (The former split form, hint -1, published the qr partials into the
+    // output qr between its two launches: not revert-safe, removed.)
+    launch_reg_mode<NSEG, WAVES, 0>(p, stream);
   }
   return (int)hipGetLastError();
 }
@@ -388,6 +396,8 @@ using namespace svoc;
 extern "C" int svoc_fast_round_bf16_reg(const FastParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
   if (p->N < 2 || p->N > 256 || p->ld % 8 != 0 || p->D > p->ld) return -1;
+  if (p->mode != 1 && (!p->work || p->work_pairs < fast_work_pairs(p->D) || p->work_stride < fast_work_words(p->D)))
+    return -1;   // pass 2 stages its outputs in the workspace
   // wave_hint -3 / -4: 8 / 2 waves per workgroup (fused); default 4 (16 waves per CU at <= 128 VGPRs)
   if (p->N <= 64) {
     if (p->wave_hint == -3) return launch_reg<1, 8>(*p, stream);

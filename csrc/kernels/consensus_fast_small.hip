@@ -166,14 +166,6 @@ __global__ __launch_bounds__(256) void consensus_fast_small_kernel(FastParams p)
     if (live && g == 0) p.status[b] = st;
     return;           // uniform over the group
   }
-  if (live) {
-#pragma unroll
-    for (int i = 0; i < NR; ++i)  // constant register indices only (a runtime index spills to scratch)
-      if (i < N && i % G == g) {
-        p.reliable[b * N + i] = (relbits >> i) & 1u;
-        p.qr[b * N + i] = qr[i];
-      }
-  }
   // ---- pass 2 (contract.cairo:476-500) from the words still in registers
   int first_rel = 0;
 #pragma unroll
@@ -217,6 +209,7 @@ __global__ __launch_bounds__(256) void consensus_fast_small_kernel(FastParams p)
   const float k3 = n / ((n - 1.f) * (n - 2.f));
   const float k4a = n * (n + 1.f) / (n - 1.f), k4b = 3.f * (n - 1.f) * (n - 1.f), k4c = (n - 2.f) * (n - 3.f);
   int zv = 0;
+  float cons_o[2], sk_o[2], ku_o[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const bool v = h ? vB : vA;
@@ -235,18 +228,35 @@ __global__ __launch_bounds__(256) void consensus_fast_small_kernel(FastParams p)
     } else if (v) {
       zv = 1;
     }
-    if (live && v) {
-      const int64_t o = b * D + colA + h;
-      p.consensus[o] = CONS ? med : shh + dl;
-      p.skew[o] = p.legacy ? 0.f : sk;
-      p.kurt[o] = p.legacy ? 0.f : ku;
-    }
+    cons_o[h] = CONS ? med : shh + dl;
+    sk_o[h] = p.legacy ? 0.f : sk;
+    ku_o[h] = p.legacy ? 0.f : ku;
   }
   zv = group_or<G>(zv);
-  if (live && g == 0) {
+  if (!live) return;
+  if (zv && !p.legacy) {   // revert: no output is written (contract.cairo:588-603)
+    if (g == 0) p.status[b] = ST_ZERO_VARIANCE;
+    return;
+  }
+  // ---- commit: the whole round succeeded
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (!(h ? vB : vA)) continue;
+    const int64_t o = b * D + colA + h;
+    p.consensus[o] = cons_o[h];
+    p.skew[o] = sk_o[h];
+    p.kurt[o] = ku_o[h];
+  }
+#pragma unroll
+  for (int i = 0; i < NR; ++i)  // constant register indices only (a runtime index spills to scratch)
+    if (i < N && i % G == g) {
+      p.reliable[b * N + i] = (relbits >> i) & 1u;
+      p.qr[b * N + i] = qr[i];
+    }
+  if (g == 0) {
     p.rel[2 * b] = rel1;
     p.rel[2 * b + 1] = rel2;
-    p.status[b] = (zv && !p.legacy) ? ST_ZERO_VARIANCE : ST_OK;
+    p.status[b] = ST_OK;
   }
 }
 

@@ -477,17 +477,66 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
     if (tid == 0) p.status[b] = misc_i[0];
     return;
   }
-  for (int t = tid; t < N; t += NT) {
-    p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
-    p.qr[(int64_t)b * N + t] = qr_lds[t];
+  const int npairs = (D + 1) >> 1;
+
+  // ------------------------------------------------------------ zero-variance pre-check (constrained)
+  // A reliable column of zero variance reverts the whole round (sqrt(0) -> wsad_div by zero,
+  // math.cairo:322,331; contract.cairo:588-603).  Fast mode: ZERO_VARIANCE <=> the reliable values of
+  // some column are all equal.  It is decided here, before any output is written.  The R equal values
+  // would form a sorted run covering positions [f, N - f - 1]; when f + H <= N/2 that run contains the
+  // whole pass-1 window, so only columns whose window is constant (lowest key == highest key) qualify
+  // -- usually none -- and only those are compared against the reliable rows.  Otherwise every
+  // column is.  (Unconstrained rounds stage their outputs instead: no window.)
+  if (CONS && !p.legacy) {
+    const bool inwin = f + H <= N / 2;
+    int fr = 0;   // first reliable row
+    for (int w = 0; w < 4; ++w)
+      if (relmask[w]) { fr = 64 * w + __builtin_ctzll(relmask[w]); break; }
+    bool zv = false;
+#pragma nounroll
+    for (int base = wave * 64; base < npairs; base += WAVES * 64) {
+      const int pair = base + lane;
+      const int pr = pair < npairs ? pair : npairs - 1;
+      bool cA = pair < npairs, cB = pair < npairs && 2 * pair + 1 < D;
+      if (inwin) {
+        const uint32_t lo = bload(ws, pr * 4, 0), hi = ~bload(ws, (Dp + pr) * 4, 0);
+        cA = cA && ((lo ^ hi) & 0xffffu) == 0;
+        cB = cB && ((lo ^ hi) >> 16) == 0;
+      }
+      if (__ballot(cA || cB)) {   // rare: compare the reliable rows with the first one
+        const uint32_t w0 = bload(rs, pr * 4, fr * rowb);
+        const float rA = bf16_lo(w0), rB = bf16_hi(w0);
+        for (int i = fr + 1; i < N; ++i) {
+          if (!((relmask[i >> 6] >> (i & 63)) & 1)) continue;   // uniform
+          const uint32_t w = bload(rs, pr * 4, i * rowb);
+          cA = cA && bf16_lo(w) == rA;
+          cB = cB && bf16_hi(w) == rB;
+        }
+        zv = zv || cA || cB;
+      }
+    }
+    if (zv) misc_i[1] = 1;
+    __syncthreads();
+    if (misc_i[1]) {
+      if (tid == 0) p.status[b] = ST_ZERO_VARIANCE;
+      return;
+    }
   }
+  if (CONS) {
+    for (int t = tid; t < N; t += NT) {
+      p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
+      p.qr[(int64_t)b * N + t] = qr_lds[t];
+    }
+  }
+  // unconstrained: pass-2 outputs are staged in the workspace and committed at the end
+  const int D2 = 2 * Dp;
+  const int STG = Dp * (2 * 17 + 8 + 2) * 4;   // launch.hpp: fast_work_stage_word
 
   // ------------------------------------------------------------ phase B: pass 2 (contract.cairo:476-500)
   // one lane per column pair: the removed keys are sorted once (true key order) and ranked against
   // both window halves; packed power sums for the two columns
   const float n = (float)R;
   const int sh = H - 1 - (N / 2 - R / 2);   // -inf sentinels in front of the removed keys
-  const int npairs = (D + 1) >> 1;
   const int64_t ob = (int64_t)b * D;
   bool zv = false;
 #pragma nounroll
@@ -578,15 +627,23 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
       if (!(pair < npairs && col < D)) continue;
       const float a2 = h ? sa2.y : sa2.x, a4 = h ? sa4.y : sa4.x;
       const float r2 = h ? t2.y : t2.x, r4 = h ? t4.y : t4.x;
-      const bool good = r2 > 0.f && a2 <= p.win_cancel * r2 && a4 <= p.win_cancel * r4;
+      // trusted: no deep cancellation in the all-minus-removed difference, and the reliable mean
+      // within 2 sigma of the shift c1 (moments about a far shift cancel like (dl^2 / mu2)^2)
+      const float rdl = (h ? t1.y : t1.x) / n, rmu2 = r2 / n - rdl * rdl;
+      const bool good = r2 > 0.f && a2 <= p.win_cancel * r2 && a4 <= p.win_cancel * r4 && rdl * rdl <= 4.f * rmu2;
       if (CONS) p.consensus[ob + col] = h ? 0.5f * (bf16_hi(medw) + bf16_hi(mhw)) : 0.5f * (bf16_lo(medw) + bf16_lo(mhw));
       if (good) {
         float dl, sk, ku;
         const bool nz = moments_from_sums(n, h ? t1.y : t1.x, r2, h ? t3.y : t3.x, r4, dl, sk, ku);
-        if (!CONS) p.consensus[ob + col] = (h ? c1B : c1A) + dl;
-        p.skew[ob + col] = p.legacy ? 0.f : sk;
-        p.kurt[ob + col] = p.legacy ? 0.f : ku;
-        zv |= !nz;
+        if (CONS) {
+          p.skew[ob + col] = p.legacy ? 0.f : sk;
+          p.kurt[ob + col] = p.legacy ? 0.f : ku;
+        } else {
+          stage_out(ws, STG, D2, 0, col, (h ? c1B : c1A) + dl);
+          stage_out(ws, STG, D2, 1, col, p.legacy ? 0.f : sk);
+          stage_out(ws, STG, D2, 2, col, p.legacy ? 0.f : ku);
+          zv |= !nz;
+        }
       } else {
         // exact recomputation over the reliable rows below (each column listed once: <= D entries)
         const int k = atomicAdd(&misc_i[2], 1);
@@ -594,9 +651,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
       }
     }
   }
-  if (zv && !p.legacy) misc_i[1] = 1;
+  if (!CONS && zv && !p.legacy) misc_i[1] = 1;
   __syncthreads();
-  // cleanup: one wave per listed column, lanes stride the rows, wave reduction (math.cairo:320-363)
+  // cleanup: one wave per listed column, lanes stride the rows, two-pass wave reductions
+  // (math.cairo:320-363): the reliable mean first, then the power sums about it (no cancellation)
   const int nredo = misc_i[2];
   if (nredo) {
     for (int k = wave; k < nredo; k += WAVES) {
@@ -604,41 +662,70 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
       const int col = (int)__builtin_amdgcn_readfirstlane(__builtin_amdgcn_raw_buffer_load_b32(ws, 0, LST + k * 4, 1));
       const float cc = p.c1[ob + col];
       const uint16_t* xc = inst + col;
-      float t1 = 0.f, t2 = 0.f, t3 = 0.f, t4 = 0.f;
+      float y[NSEG];
+      float t1 = 0.f;
 #pragma unroll
       for (int g = 0; g < NSEG; ++g) {
         const int i = g * 64 + lane;
         const bool use = i < N && ((relmask[g] >> lane) & 1);
-        if (use) {
-          const float y = __builtin_bit_cast(float, (uint32_t)xc[(int64_t)i * p.ld] << 16) - cc;
-          const float q = y * y;
-          t1 += y;
-          t2 += q;
-          t3 = fmaf(q, y, t3);
-          t4 = fmaf(q, q, t4);
-        }
+        y[g] = use ? __builtin_bit_cast(float, (uint32_t)xc[(int64_t)i * p.ld] << 16) - cc : 0.f;
+        t1 += y[g];
       }
-      t1 += xor_lane<1>(t1); t2 += xor_lane<1>(t2); t3 += xor_lane<1>(t3); t4 += xor_lane<1>(t4);
-      t1 += xor_lane<2>(t1); t2 += xor_lane<2>(t2); t3 += xor_lane<2>(t3); t4 += xor_lane<2>(t4);
-      t1 += xor_lane<4>(t1); t2 += xor_lane<4>(t2); t3 += xor_lane<4>(t3); t4 += xor_lane<4>(t4);
-      t1 += xor_lane<8>(t1); t2 += xor_lane<8>(t2); t3 += xor_lane<8>(t3); t4 += xor_lane<8>(t4);
-      t1 += xor_lane<16>(t1); t2 += xor_lane<16>(t2); t3 += xor_lane<16>(t3); t4 += xor_lane<16>(t4);
-      t1 += xor_lane<32>(t1); t2 += xor_lane<32>(t2); t3 += xor_lane<32>(t3); t4 += xor_lane<32>(t4);
+      t1 += xor_lane<1>(t1); t1 += xor_lane<2>(t1); t1 += xor_lane<4>(t1);
+      t1 += xor_lane<8>(t1); t1 += xor_lane<16>(t1); t1 += xor_lane<32>(t1);
+      const float mu = t1 / n;   // reliable mean - c1
+      float c1s = 0.f, t2 = 0.f, t3 = 0.f, t4 = 0.f;
+#pragma unroll
+      for (int g = 0; g < NSEG; ++g) {
+        const int i = g * 64 + lane;
+        const bool use = i < N && ((relmask[g] >> lane) & 1);
+        const float d = use ? y[g] - mu : 0.f;
+        const float q = d * d;
+        c1s += d;
+        t2 += q;
+        t3 = fmaf(q, d, t3);
+        t4 = fmaf(q, q, t4);
+      }
+      c1s += xor_lane<1>(c1s); t2 += xor_lane<1>(t2); t3 += xor_lane<1>(t3); t4 += xor_lane<1>(t4);
+      c1s += xor_lane<2>(c1s); t2 += xor_lane<2>(t2); t3 += xor_lane<2>(t3); t4 += xor_lane<2>(t4);
+      c1s += xor_lane<4>(c1s); t2 += xor_lane<4>(t2); t3 += xor_lane<4>(t3); t4 += xor_lane<4>(t4);
+      c1s += xor_lane<8>(c1s); t2 += xor_lane<8>(t2); t3 += xor_lane<8>(t3); t4 += xor_lane<8>(t4);
+      c1s += xor_lane<16>(c1s); t2 += xor_lane<16>(t2); t3 += xor_lane<16>(t3); t4 += xor_lane<16>(t4);
+      c1s += xor_lane<32>(c1s); t2 += xor_lane<32>(t2); t3 += xor_lane<32>(t3); t4 += xor_lane<32>(t4);
       if (lane == 0) {
         float dl, sk, ku;
-        const bool nz = moments_from_sums(n, t1, t2, t3, t4, dl, sk, ku);
-        if (!CONS) p.consensus[ob + col] = cc + dl;
-        p.skew[ob + col] = p.legacy ? 0.f : sk;
-        p.kurt[ob + col] = p.legacy ? 0.f : ku;
-        if (!nz && !p.legacy) misc_i[1] = 1;
+        const bool nz = moments_from_sums(n, c1s, t2, t3, t4, dl, sk, ku);
+        if (CONS) {
+          p.skew[ob + col] = p.legacy ? 0.f : sk;
+          p.kurt[ob + col] = p.legacy ? 0.f : ku;
+        } else {
+          stage_out(ws, STG, D2, 0, col, cc + mu + dl);
+          stage_out(ws, STG, D2, 1, col, p.legacy ? 0.f : sk);
+          stage_out(ws, STG, D2, 2, col, p.legacy ? 0.f : ku);
+          if (!nz && !p.legacy) misc_i[1] = 1;
+        }
       }
     }
     __syncthreads();
   }
+  // ------------------------------------------------------------ commit
+  // (constrained: the outputs were written in place -- the pre-check ruled out every revert;
+  // unconstrained: copied from the staging area, only when the round succeeded)
+  if (!CONS) {
+    if (misc_i[1]) {
+      if (tid == 0) p.status[b] = ST_ZERO_VARIANCE;
+      return;
+    }
+    commit_staged<NT>(ws, STG, D2, D, tid, p.consensus + ob, p.skew + ob, p.kurt + ob);
+    for (int t = tid; t < N; t += NT) {
+      p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
+      p.qr[(int64_t)b * N + t] = qr_lds[t];
+    }
+  }
   if (tid == 0) {
     p.rel[2 * (int64_t)b] = misc_f[0];
     p.rel[2 * (int64_t)b + 1] = misc_f[1];
-    p.status[b] = misc_i[1] ? ST_ZERO_VARIANCE : ST_OK;
+    p.status[b] = ST_OK;
   }
 }
 
@@ -673,6 +760,7 @@ using namespace svoc;
 extern "C" int svoc_fast_round_bf16_win(const FastParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
   if (!p->work || p->N < 2 || p->N > 256 || p->ld % 8 != 0 || p->D > p->ld) return -2;
+  if (p->mode == 2 && p->work_fresh) return -2;   // pass 1 ran elsewhere: no windows to read
   if (p->n_failing < 0 || p->n_failing > 32 || p->n_failing > p->N - 2) return -2;
   const int H = win_h(p->N, p->n_failing);
   if (H == 0) return -2;

@@ -63,7 +63,7 @@ from . import torch_ref  # noqa: E402,F401
 def fast_work_words(D: int) -> int:
     """u32 words per instance of the window kernel's workspace (csrc/include/svoc/launch.hpp)."""
     pairs = ((D + 1) // 2 + 255) // 256 * 256
-    return pairs * (2 * 17 + 8 + 2)
+    return pairs * (2 * 17 + 8 + 2 + 6)
 
 
 def fast_work_numel(B: int, D: int) -> int:
@@ -72,7 +72,7 @@ def fast_work_numel(B: int, D: int) -> int:
 
 
 def fast_work_applies(N: int, D: int, n_failing: int) -> bool:
-    """Whether the default GPU fast round uses the one-network window kernel (consensus_fast_win.hip):
-    not the small-instance kernel (N <= 16 and D <= 128) and at most 32 failing oracles."""
-    return (N > 16 or D > 128) and 0 <= n_failing <= min(32, N - 2)
+    """Whether the default GPU fast round needs the workspace: every kernel but the small-instance
+    one (N <= 16 and D <= 128) keeps its window state and staged pass-2 outputs there."""
+    return N > 16 or D > 128
 

@@ -11,6 +11,11 @@ Every rank then computes the identical rank mask from the identical reduced qr (
 no broadcast needed).  The constrained reliability divides by the GLOBAL dimension (rel_dim).
 One all-reduce per round, batched over all B local instances -- sized for xGMI, where a few-KB
 message is latency-bound (survey §5.8 b).
+
+Per-instance atomicity across shards (survey §2.6; contract.cairo:588-603 reverts the whole tx): the
+zero-variance check of pass 2 sees only the local columns, so pass 2 writes into shadow outputs, the
+[B] status words are all-reduced (MAX: any shard's failure code wins, OK = 0), and only instances
+whose reduced status is OK commit -- on every rank, or on none.
 """
 from __future__ import annotations
 
@@ -26,20 +31,48 @@ def shard_bounds(D: int, rank: int, world: int):
     return lo, min(D, lo + per)
 
 
+class _Shadow:
+    """Scratch outputs of one sharded round (allocated once per engine)."""
+
+    def __init__(self, e):
+        self.qr = torch.zeros_like(e.qr)
+        self.consensus = torch.zeros_like(e.consensus)
+        self.skew = torch.zeros_like(e.skew)
+        self.kurt = torch.zeros_like(e.kurt)
+        self.rel = torch.zeros_like(e.rel)
+        self.reliable = torch.zeros_like(e.reliable)
+
+
 def run_round_sharded(engine, d_global: int, group=None, world: int = 1) -> None:
     """Consensus round for an engine holding a column shard of every instance."""
     if engine.mode != "fast":
         raise NotImplementedError("D-sharding is implemented for the fast (float) engine")
     e = engine
+    sh = getattr(e, "_dshard_shadow", None)
+    if sh is None:
+        sh = e._dshard_shadow = _Shadow(e)
     e._ops.round_prologue(e.n_active, e.touched, e.N, True, e._active)
     mx = float(e.cfg.unconstrained_max_spread)
-    args = (e.values, e._active, e.D, e.cfg.n_failing_oracles, e.cfg.constrained, mx, e.c1, e.consensus,
-            e.skew, e.kurt, e.rel, e.qr, e.reliable, e.status, e.wave_hint)
     lg = e.cfg.legacy
     w = e.work()                                     # window kernel: pass 1 -> pass 2 state
-    e._ops.fast_round(*args, 1, d_global, lg, w)   # pass 1: local c1 + qr partials
+    head = (e.values, e._active, e.D, e.cfg.n_failing_oracles, e.cfg.constrained, mx, e.c1)
+    # pass 1: local c1 + qr partials (into the shadow qr: the committed qr stays intact)
+    e._ops.fast_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status,
+                      e.wave_hint, 1, d_global, lg, w)
     if world > 1:
-        dist.all_reduce(e.qr, op=dist.ReduceOp.SUM, group=group)
-    e._ops.fast_round(*args, 2, d_global, lg, w)   # pass 2 from the global qr
+        dist.all_reduce(sh.qr, op=dist.ReduceOp.SUM, group=group)
+    # pass 2 from the global qr, into the shadow outputs; status = this shard's verdict
+    e._ops.fast_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status,
+                      e.wave_hint, 2, d_global, lg, w)
+    if world > 1:
+        dist.all_reduce(e.status, op=dist.ReduceOp.MAX, group=group)
+    ok = (e._active != 0) & (e.status == int(Status.OK))
+    ok1 = ok[:, None]
+    e.consensus.copy_(torch.where(ok1, sh.consensus, e.consensus))
+    e.skew.copy_(torch.where(ok1, sh.skew, e.skew))
+    e.kurt.copy_(torch.where(ok1, sh.kurt, e.kurt))
+    e.rel.copy_(torch.where(ok1, sh.rel, e.rel))
+    e.qr.copy_(torch.where(ok1, sh.qr, e.qr))
+    e.reliable.copy_(torch.where(ok1, sh.reliable, e.reliable))
     e._ops.round_epilogue(e._active, e.status, e.rel, e.consensus_active, e.touched, e.metrics_fx)
     e.rounds += 1

@@ -30,7 +30,7 @@ class Status(enum.IntEnum):
     ALREADY_ORACLE = 19
     UNWRAP_NONE = 20          # majority reached on a None proposition (contract.cairo:572)
     WRONG_ADMIN_INDEX = 21    # which_admin >= n_admins (hardening; see governance.py)
-    # fast-mode only (float path): non-fatal diagnostics are never produced, these revert outputs
+    # fast-mode codes (float path); like every non-OK status they revert the round: no output moves
     ZERO_VARIANCE = 32        # a reliable column has sigma == 0 (exact mode reports DIV_BY_ZERO)
     TOO_FEW_RELIABLE = 33     # R < 4: kurtosis denominator (n-2)(n-3) == 0 (exact: DIV_BY_ZERO)
     NON_FINITE = 34           # unconstrained float update holding NaN / inf (no wsad counterpart)

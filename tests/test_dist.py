@@ -98,3 +98,65 @@ def test_dsharding_matches_single_process(constrained, world):
         torch.testing.assert_close(s["rel"], ref["rel"], rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(s["cons"], ref["consensus"][:, s["lo"]:s["hi"]], rtol=0, atol=1e-6)
         torch.testing.assert_close(s["skew"], ref["skew"][:, s["lo"]:s["hi"]], rtol=1e-4, atol=1e-4)
+
+
+def _ds_revert_worker(rank, world, port, outdir, x1, x2, cfgd):
+    _init(rank, world, port)
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    from svoc.parallel.dshard import run_round_sharded, shard_bounds
+    cfg = ConsensusConfig(**cfgd)
+    lo, hi = shard_bounds(cfg.dimension, rank, world)
+    e = ConsensusEngine(ConsensusConfig(**{**cfgd, "dimension": hi - lo}), x1.shape[0], device="cpu", mode="fast")
+    out = {}
+    for k, x in enumerate((x1, x2)):
+        e.values[:, :, : hi - lo] = x[:, :, lo:hi]
+        e.enabled.fill_(1); e.n_active.fill_(cfg.n_oracles); e.touched.fill_(1)
+        run_round_sharded(e, cfg.dimension, world=world)
+        out[k] = dict(cons=e.consensus.clone(), rel=e.rel.clone(), reliable=e.reliable.clone(), qr=e.qr.clone(),
+                      skew=e.skew.clone(), kurt=e.kurt.clone(), st=e.status.clone(), act=e.consensus_active.clone())
+    torch.save(dict(out=out, lo=lo, hi=hi), os.path.join(outdir, f"dsr{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_dsharding_revert_is_atomic_across_shards():
+    """Zero variance in one shard's columns only: every shard reverts that instance (no output moves)."""
+    from helpers import beta_oracles
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    B, N, D, f, world = 4, 32, 40, 4, 2
+    x1, _ = beta_oracles(B, N, D, f, seed=21)
+    x1 = x1[:, :, :D].contiguous()
+    x2, _ = beta_oracles(B, N, D, f, seed=22)
+    x2 = x2[:, :, :D].contiguous()
+    x2[1, :, 2] = 0.5           # column 2 lives in shard 0: constant -> zero variance there only
+    x2[3, :, 25] = 0.25         # column 25: shard 1 only
+    cfgd = dict(n_oracles=N, dimension=D, n_failing_oracles=f, constrained=True)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ds_revert_worker, args=(world, _free_port(), d, x1, x2, cfgd), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"dsr{i}.pt"), weights_only=True) for i in range(world)]
+    # single-process reference (CPU fast engine, all columns)
+    ref = ConsensusEngine(ConsensusConfig(**cfgd), B, device="cpu", mode="fast")
+    snaps = []
+    for x in (x1, x2):
+        ref.values[:, :, :D] = x
+        ref.enabled.fill_(1); ref.n_active.fill_(N); ref.touched.fill_(1)
+        ref.run_round()
+        snaps.append(dict(cons=ref.consensus.clone(), st=ref.status.clone(), rel=ref.rel.clone(), qr=ref.qr.clone(),
+                          reliable=ref.reliable.clone(), skew=ref.skew.clone()))
+    assert snaps[1]["st"].tolist() == [0, 32, 0, 32]
+    for s in r:
+        o1, o2 = s["out"][0], s["out"][1]
+        assert o2["st"].tolist() == [0, 32, 0, 32]
+        for inst in (1, 3):   # reverted: every output identical to round 1, bit for bit
+            for k in ("cons", "rel", "reliable", "qr", "skew", "kurt"):
+                assert torch.equal(o2[k][inst], o1[k][inst]), (k, inst)
+        for inst in (0, 2):
+            assert not torch.equal(o2["cons"][inst], o1["cons"][inst])
+        assert torch.equal(o2["reliable"], snaps[1]["reliable"])
+        torch.testing.assert_close(o2["cons"], snaps[1]["cons"][:, s["lo"]:s["hi"]], rtol=0, atol=1e-6)
+        torch.testing.assert_close(o2["rel"], snaps[1]["rel"], rtol=1e-5, atol=1e-6)
+    # the single-process engine reverts the same instances and leaves round 1's outputs
+    for inst in (1, 3):
+        assert torch.equal(snaps[1]["cons"][inst], snaps[0]["cons"][inst])
+        assert torch.equal(snaps[1]["qr"][inst], snaps[0]["qr"][inst])

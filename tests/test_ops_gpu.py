@@ -30,10 +30,10 @@ _SHAPES = [(7, 6, 2, True), (64, 1024, 8, True), (64, 1000, 8, False), (50, 300,
            (7, 6, 2, False), (16, 100, 3, True), (9, 1, 2, True), (12, 128, 4, False), (8, 33, 2, True)]
 
 
-# hint 0: register-streaming fused kernel (default); -1: its split two-launch form; -3 / -4: 8 / 2
+# hint 0: default dispatch (window kernel / small kernel); -7: register-streaming kernel; -3 / -4: 8 / 2
 # waves per workgroup; 1 / 2 / 8: the LDS-tiled kernel (consensus_fast.hip)
 @pytest.mark.parametrize("N,D,f,constrained,hint",
-                         [s + (h,) for s in _SHAPES for h in (0, -1, 1)]
+                         [s + (h,) for s in _SHAPES for h in (0, -7, 1)]
                          + [(64, 1024, 8, True, h) for h in (-3, -4, 2, 8)] + [(33, 70, 4, False, h) for h in (-3, -4)])
 def test_fast_hip_vs_torch(N, D, f, constrained, hint):
     B = 12
@@ -54,7 +54,7 @@ def test_fast_small_kernel_batch_edges():
     """Deployed config 7 x 6: partial last workgroup, inactive instances, reverts, vs the CPU engine."""
     B, N, D = 1000, 7, 6
     x, _ = beta_oracles(B, N, D, 2, seed=21)
-    x[5] = 0.0                               # zero variance (non-fatal flag)
+    x[5] = 0.0                               # zero variance -> ZERO_VARIANCE (the round reverts)
     x[6, :4, :D] = 0.0                       # rel1 < 0 -> RELIABILITY_INTERVAL
     x[6, 4:, :D] = 1.0
     active = (torch.arange(B) % 7 != 3).to(torch.uint8)
@@ -70,7 +70,7 @@ def test_fast_small_kernel_batch_edges():
 def test_fast_hip_active_mask_and_revert():
     B, N, D = 6, 64, 128
     x, _ = beta_oracles(B, N, D, 8, seed=3)
-    x[1] = 0.0                          # zero-variance everywhere -> ZERO_VARIANCE flag (non fatal)
+    x[1] = 0.0                          # zero variance everywhere -> ZERO_VARIANCE (the round reverts)
     x[2, :40, :D] = 0.0                 # c1 = 0, 24/64 rows at distance 1: rel1 = 1 - 2*sqrt(.375) < 0
     x[2, 40:, :D] = 1.0
     xg = x.to(DEV)

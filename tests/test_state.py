@@ -59,6 +59,39 @@ def test_corruption_detected(tmp_path):
         state.load(p)
 
 
+def test_corrupt_header_rejected_without_allocation(tmp_path):
+    """A section header claiming a huge shape (overflowing numel, or more bytes than the file holds)
+    fails cleanly instead of allocating: the load checks sizes against the bytes left in the file."""
+    import struct
+    cfg = ConsensusConfig(n_oracles=7, dimension=3, n_failing_oracles=2, n_admins=3)
+    a = ConsensusService(cfg, 2, ADMINS, ORACLES, device="cpu", mode="exact")
+    p = os.path.join(tmp_path, "s.svoc")
+    state.save(a, p)
+    raw = bytearray(open(p, "rb").read())
+    ml = struct.unpack_from("<I", raw, 12)[0]
+    o = 16 + ml                                  # first section header
+    nl = struct.unpack_from("<I", raw, o)[0]
+    o += 4 + nl + 1                              # name, dtype
+    nd = raw[o]
+    assert nd >= 1
+    for huge, msg in ((1 << 62, "overflow|size mismatch|truncated"), (1 << 40, "size mismatch|truncated")):
+        bad = bytearray(raw)
+        struct.pack_into("<Q", bad, o + 1, huge)
+        open(p, "wb").write(bytes(bad))
+        with pytest.raises(Exception, match=msg):
+            state.load(p)
+    # a consistent header (shape and nbytes agree) that promises more bytes than the file holds
+    bad = bytearray(raw)
+    es_nb_off = o + 1 + 8 * nd
+    old_nb = struct.unpack_from("<Q", bad, es_nb_off)[0]
+    old_d0 = struct.unpack_from("<Q", bad, o + 1)[0]
+    struct.pack_into("<Q", bad, o + 1, old_d0 * 10**9)
+    struct.pack_into("<Q", bad, es_nb_off, old_nb * 10**9)
+    open(p, "wb").write(bytes(bad))
+    with pytest.raises(Exception, match="truncated"):
+        state.load(p)
+
+
 def test_fast_mode_roundtrip(tmp_path):
     cfg = ConsensusConfig(n_oracles=16, dimension=20, n_failing_oracles=2, n_admins=2)
     a = ConsensusService(cfg, 4, ADMINS[:2], [100 + i for i in range(16)], device="cpu", mode="fast")

@@ -100,7 +100,7 @@ def test_win_zero_variance_flag():
     xg = x.to(DEV)
     win, reg = _both(xg, D, f, True)
     assert torch.equal(win["status"], reg["status"])
-    assert int(win["status"][0]) == 32      # ZERO_VARIANCE (non-fatal flag)
+    assert int(win["status"][0]) == 32      # ZERO_VARIANCE: the round reverts
 
 
 def test_win_legacy():
