@@ -76,6 +76,8 @@ def main():
                          "-1 = the config's default")
     ap.add_argument("--mode", default=None, choices=["fast", "exact"],
                     help="override the config's engine mode (exact = bit-exact wsad int64 path)")
+    ap.add_argument("--storage", default=None, choices=["bf16", "int64", "int32"],
+                    help="engine value storage (exact mode: int64 default, int32 for constrained configs)")
     ap.add_argument("--dshard", action="store_true",
                     help="strong scaling: every rank holds a column slice of ALL instances (D-sharding, one "
                          "[B, N] qr all-reduce per round) instead of its own instances (DP, default)")
@@ -129,7 +131,7 @@ def main():
     mode = args.mode or c.get("mode", "fast")
     if dshard and (mode != "fast" or args.config in ("c4", "c5")):
         raise SystemExit("--dshard is for the fast column-sharded configs (c2, c3)")
-    eng = ConsensusEngine(cfg, batch=B, device=dev, mode=mode)
+    eng = ConsensusEngine(cfg, batch=B, device=dev, mode=mode, storage=args.storage)
     eng.wave_hint = args.wave_hint
     dp = DataParallelConsensus(eng, rank=rank, world=world)
     eng.randomize(seed=1000 + (0 if dshard else rank))
@@ -269,7 +271,7 @@ def main():
             "metric": METRIC, "value": value, "unit": "consensus rounds/s", "n_gpus": world,
             "steps": steps_done, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "strong" if dshard else "weak", "vs_baseline": None,
-            "dtype": "int64-wsad" if mode == "exact" else c.get("dtype", "bf16"), "data": "synthetic",
+            "dtype": f"{eng.storage}-wsad" if mode == "exact" else c.get("dtype", "bf16"), "data": "synthetic",
             "config": {"model": c["model"], "global_batch": B * (1 if dshard else world), "seq_len": c["D"],
                        "parallelism": f"dshard{world}" if dshard else f"dp{world}", "engine_mode": mode, "n_oracles": c["N"], "dimension": c["D"],
                        "n_failing": c["f"], "updates_per_instance_per_step": U_per_inst,

@@ -17,7 +17,8 @@ int dtype_code(at::ScalarType t) {
   if (t == at::kBFloat16) return 0;
   if (t == at::kFloat) return 1;
   if (t == at::kLong) return 2;
-  TORCH_CHECK(false, "values dtype must be bf16, fp32 or int64 (wsad)");
+  if (t == at::kInt) return 3;
+  TORCH_CHECK(false, "values dtype must be bf16, fp32, int64 or int32 (wsad)");
   return -1;
 }
 
@@ -67,7 +68,7 @@ bool in_range_cpu(const UpdateParams& p, int64_t u, int d) {
     const float f = ((const float*)p.upd)[u * p.D + d];
     return f >= 0.f && f <= 1.f;
   }
-  const int64_t v = ((const int64_t*)p.upd)[u * p.D + d];
+  const int64_t v = p.dtype == 3 ? (int64_t)((const int32_t*)p.upd)[u * p.D + d] : ((const int64_t*)p.upd)[u * p.D + d];
   return v >= 0 && v <= 1000000;
 }
 
@@ -85,7 +86,7 @@ void apply_updates_cpu(at::Tensor values, at::Tensor enabled, at::Tensor n_activ
     if (st == ST_OK && p.constrained)
       for (int d = 0; d < p.D; ++d)
         if (!in_range_cpu(p, u, d)) { st = ST_INTERVAL_INPUT; break; }
-    if (st == ST_OK && !p.constrained && p.dtype != 2)
+    if (st == ST_OK && !p.constrained && p.dtype <= 1)
       for (int d = 0; d < p.D; ++d) {
         const float f = p.dtype == 1 ? ((const float*)p.upd)[u * p.D + d] : [&] {
           uint32_t w = (uint32_t)((const uint16_t*)p.upd)[u * p.D + d] << 16;

@@ -173,8 +173,9 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
 void exact_checks(const at::Tensor& values, const at::Tensor& c1, const at::Tensor& cons, const at::Tensor& skew,
                   const at::Tensor& kurt, const at::Tensor& rel, const at::Tensor& qr, const at::Tensor& reliable,
                   const at::Tensor& status) {
-  TORCH_CHECK(values.dim() == 3 && values.scalar_type() == at::kLong && values.is_contiguous(),
-              "values: contiguous int64 [B, N, D] wsad");
+  TORCH_CHECK(values.dim() == 3 && (values.scalar_type() == at::kLong || values.scalar_type() == at::kInt) &&
+                  values.is_contiguous(),
+              "values: contiguous int64 or int32 [B, N, D] wsad");
   const int64_t B = values.size(0), N = values.size(1), D = values.size(2);
   const auto dev = values.device();
   check_out(c1, at::kLong, {B, D}, "c1", dev);
@@ -192,6 +193,11 @@ void exact_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& 
                      at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable, at::Tensor status,
                      bool legacy) {
   exact_checks(values, c1, cons, skew, kurt, rel, qr, reliable, status);
+  if (values.scalar_type() == at::kInt) {   // int32 wsad storage: the CPU engine works on int64
+    exact_round_cpu(values.to(at::kLong), active, n_failing, constrained, max_spread, c1, cons, skew, kurt, rel, qr,
+                    reliable, status, legacy);
+    return;
+  }
   ExactBatch eb{};
   eb.legacy = legacy;
   eb.values = values.data_ptr<int64_t>();
@@ -218,7 +224,8 @@ void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& 
   exact_checks(values, c1, cons, skew, kurt, rel, qr, reliable, status);
   ExactParams p{};
   p.legacy = legacy ? 1 : 0;
-  p.values = values.data_ptr<int64_t>();
+  p.values = values.data_ptr();
+  p.val32 = values.scalar_type() == at::kInt ? 1 : 0;
   p.B = (int)values.size(0); p.N = (int)values.size(1); p.D = (int)values.size(2);
   TORCH_CHECK(p.N >= 1 && p.N <= 256, "GPU exact path supports N <= 256");
   p.active = active_ptr(active, p.B, values.device());
@@ -237,6 +244,18 @@ void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& 
   if ((int64_t)p.D * 6 * 8 > 64 * 1024) {  // wide instances: per-column intermediates in HBM
     work = at::empty({(int64_t)p.B, 6, (int64_t)p.D}, values.options());
     p.work = work.data_ptr<int64_t>();
+  }
+  // column-parallel kernel (consensus_wsad.hip) for constrained rounds, the i128 kernel for the
+  // instances it flags; SVOC_EXACT_I128=1 forces the i128 kernel everywhere (tests, A/B)
+  at::Tensor stage, fallback;
+  const char* force = std::getenv("SVOC_EXACT_I128");
+  if (constrained && !legacy && p.N >= 4 && !(force && force[0] == '1')) {
+    stage = at::empty({(int64_t)p.B, 4, (int64_t)p.D}, values.options().dtype(at::kInt));
+    fallback = at::empty({(int64_t)p.B}, values.options().dtype(at::kByte));
+    p.stage = stage.data_ptr<int32_t>();
+    p.fallback = fallback.data_ptr<uint8_t>();
+    const char* only = std::getenv("SVOC_EXACT_WSAD_ONLY");
+    p.skip_fallback = only && only[0] == '1';
   }
   auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
   const int rc = svoc_exact_round(&p, stream);

@@ -48,7 +48,7 @@ inline int64_t fast_work_words(int64_t D) { return fast_work_pairs(D) * (2 * 17 
 inline int64_t fast_work_numel(int64_t B, int64_t D) { return B * fast_work_words(D); }
 
 struct ExactParams {
-  const int64_t* values;    // [B, N, D] wsad
+  const void* values;       // [B, N, D] wsad, int64 (or int32 when val32)
   const uint8_t* active;    // [B] or null
   int B, N, D;
   int n_failing;
@@ -64,6 +64,12 @@ struct ExactParams {
   int32_t* status;          // [B]
   int legacy;               // obsolete-contract variant (see FastParams)
   int64_t* work;            // [B, 6, D] workspace for wide instances (null: per-column data in LDS)
+  int val32;                // values are int32 wsad
+  // column-parallel kernel (consensus_wsad.hip): per-instance staging [B, 4, D] int32 and the [B]
+  // fallback flags of the instances it hands to the i128 kernel (null: i128 kernel only)
+  int32_t* stage;
+  uint8_t* fallback;
+  int skip_fallback;        // tests: leave the flagged instances alone (shows which rounds it took)
 };
 
 }  // namespace svoc
@@ -91,7 +97,7 @@ struct UpdateParams {
   int64_t inst_stride;      // elements
   int B, N, D, ld, U;
   int elem_bytes;           // 2 (bf16), 4 (fp32) or 8 (int64 wsad)
-  int dtype;                // 0 bf16, 1 fp32, 2 int64
+  int dtype;                // 0 bf16, 1 fp32, 2 int64 wsad, 3 int32 wsad
   int constrained;
   int unique;               // caller guarantees distinct (instance, oracle) pairs: one fused pass
 };

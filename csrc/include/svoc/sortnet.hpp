@@ -29,6 +29,12 @@ SVOC_DEV u16x2 kmin(u16x2 a, u16x2 b) { return __builtin_elementwise_min(a, b); 
 SVOC_DEV u16x2 kmax(u16x2 a, u16x2 b) { return __builtin_elementwise_max(a, b); }
 SVOC_DEV uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
 SVOC_DEV u16x2 as_k(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+// 32-bit keys (one column per lane: the wsad kernel's int32 values) share the networks below
+SVOC_DEV uint32_t kmin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+SVOC_DEV uint32_t kmax(uint32_t a, uint32_t b) { return a < b ? b : a; }
+SVOC_DEV uint32_t as_u32(uint32_t v) { return v; }
+template <class K>
+SVOC_DEV K key_from(uint32_t v) { return __builtin_bit_cast(K, v); }
 
 // bf16 bit pattern -> order-preserving unsigned key (and back), two lanes-halves at a time.
 SVOC_DEV u16x2 bf16x2_to_key(uint32_t raw) {
@@ -69,6 +75,7 @@ SVOC_DEV uint32_t bit_mask(uint64_t m, int i) {  // bit i set
 }
 
 SVOC_DEV u16x2 shfl_xor_k(u16x2 v, int m) { return as_k((uint32_t)__shfl_xor((int)as_u32(v), m)); }
+SVOC_DEV uint32_t shfl_xor_k(uint32_t v, int m) { return (uint32_t)__shfl_xor((int)v, m); }
 
 // Value of lane ^ M (compile-time M) without __shfl_xor's per-call lane-index arithmetic:
 // DPP quad_perm for M = 1, 2 (VALU, foldable into the consumer), ds_swizzle xor-mode for 4..16,
@@ -155,14 +162,15 @@ SVOC_DEV void sort64_oem(u16x2 (&r)[64]) {
 }
 
 // Ascending half-cleaner cascade (strides 32..1): sorts a bitonic lane-local sequence.
-SVOC_DEV void merge64(u16x2 (&r)[64]) {
+template <class K>
+SVOC_DEV void merge64(K (&r)[64]) {
 #pragma unroll
   for (int j = 32; j > 0; j >>= 1) {
 #pragma unroll
     for (int i = 0; i < 64; ++i) {
       const int l = i ^ j;
       if (l > i) {
-        const u16x2 a = r[i], b = r[l];
+        const K a = r[i], b = r[l];
         r[i] = kmin(a, b);
         r[l] = kmax(a, b);
       }
@@ -289,36 +297,36 @@ SVOC_DEV void xswap(uint32_t& x, uint32_t& y) {
 
 // Half-cleaner between lanes l and l ^ XM (lower lane keeps the minima); the upper lane's keys are
 // in the opposite polarity.  Afterwards both lanes hold keys in the lower lane's polarity.
-template <int XM>
-SVOC_DEV void xhc_swap(u16x2 (&r)[64]) {
+template <int XM, class K>
+SVOC_DEV void xhc_swap(K (&r)[64]) {
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
     uint32_t x = as_u32(r[2 * k]), y = as_u32(r[2 * k + 1]);
     xswap<XM>(x, y);               // x: lower lane's key, y: upper lane's key (complemented)
     y = ~y;
-    const u16x2 lo = kmin(as_k(x), as_k(y)), hi = kmax(as_k(x), as_k(y));
+    const K lo = kmin(key_from<K>(x), key_from<K>(y)), hi = kmax(key_from<K>(x), key_from<K>(y));
     x = as_u32(lo);
     y = as_u32(hi);
     xswap<XM>(x, y);               // lower lanes get the minima, upper lanes the maxima
-    r[2 * k] = as_k(x);
-    r[2 * k + 1] = as_k(y);
+    r[2 * k] = key_from<K>(x);
+    r[2 * k + 1] = key_from<K>(y);
   }
 }
 
 // Final half-cleaner of a bitonic sequence whose lower half ends at the median: the two middle
 // order statistics are max(lower half) and min(upper half), so the compare-exchange results are
 // folded into a running max / min instead of being written back (no swap back, no merge).
-template <int XM>
-SVOC_DEV void xhc_middle(const u16x2 (&r)[64], u16x2& mx, u16x2& mn) {
-  mx = as_k(0u);
-  mn = as_k(0xffffffffu);
+template <int XM, class K>
+SVOC_DEV void xhc_middle(const K (&r)[64], K& mx, K& mn) {
+  mx = key_from<K>(0u);
+  mn = key_from<K>(0xffffffffu);
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
     uint32_t x = as_u32(r[2 * k]), y = as_u32(r[2 * k + 1]);
     xswap<XM>(x, y);
     y = ~y;
-    mx = kmax(mx, kmin(as_k(x), as_k(y)));
-    mn = kmin(mn, kmax(as_k(x), as_k(y)));
+    mx = kmax(mx, kmin(key_from<K>(x), key_from<K>(y)));
+    mn = kmin(mn, kmax(key_from<K>(x), key_from<K>(y)));
   }
 }
 
@@ -335,9 +343,9 @@ SVOC_DEV uint32_t group_polarity(int seg) {
 //   NSEG 1: odd-even merge sort, pruned by DCE to the two outputs (~414 compare-exchanges).
 //   NSEG 2: full in-lane sort, final cross-lane half-cleaner folded into max / min.
 //   NSEG 4: in-lane sort, stage-2 exchange (lane ^ 16) + bitonic merge, final stage folded.
-template <int NSEG>
-SVOC_DEV void median_group(u16x2 (&r)[64], u16x2& lo, u16x2& hi) {
-  sort64_oem(r);
+template <int NSEG, class K>
+SVOC_DEV void median_group(K (&r)[64], K& lo, K& hi) {
+  sort_oem<64>(r);
   if constexpr (NSEG == 1) {
     lo = r[31];
     hi = r[32];
@@ -346,7 +354,7 @@ SVOC_DEV void median_group(u16x2 (&r)[64], u16x2& lo, u16x2& hi) {
       xhc_swap<16>(r);
       merge64(r);
     }
-    u16x2 mx, mn;
+    K mx, mn;
     xhc_middle<32>(r, mx, mn);               // final stage: lower half = lanes with bit 5 clear
 #pragma unroll
     for (int m = 16; m <= 32; m <<= 1) {   // lanes of the group: ^16 (NSEG 4), ^32

@@ -1,0 +1,72 @@
+// Exact fast paths of the wsad operations (signed_decimal.cairo:52-116, math.cairo:170-173,
+// 271-292, 320-363) for BOUNDED operands -- the constrained domain [0, 1e6] of the column-parallel
+// exact kernel (consensus_wsad.hip).  fp64 arithmetic on integral values instead of i128: every
+// routine returns the identical integer that wsad.hpp computes, under the precondition stated on it
+// (the kernel checks the preconditions and hands any instance that violates one to the i128 kernel).
+//
+// Why fp64 is exact here: integers below 2^53 are exact doubles, fma(a, b, c) rounds the exact
+// a*b + c once (exact when that result is an integer below 2^53), and a quotient estimated through a
+// reciprocal is within 1 of the truth whenever the dividend is below 2^51 -- one remainder test then
+// fixes it.  CDNA4 runs fp64 VALU at half the fp32 rate; a 64-bit integer division is ~40 instructions.
+#pragma once
+
+#include <math.h>
+#include <stdint.h>
+
+#include "wsad.hpp"
+
+namespace svoc {
+
+// floor(t / d) for integral 0 <= t < 2^51 and integral 1 <= d < 2^31, given inv = 1.0 / d.
+SVOC_HD double floor_div_d(double t, double d, double inv) {
+  double q = floor(t * inv);          // |error| of t * inv < 0.5: q is the quotient or one off
+  const double r = fma(-q, d, t);     // exact remainder (a small integer)
+  q = r < 0.0 ? q - 1.0 : (r >= d ? q + 1.0 : q);
+  return q;
+}
+
+// I128Div(a, d) = trunc(a / d) toward zero (signed_decimal.cairo:52-63) for |a| < 2^51, 1 <= d < 2^31.
+SVOC_HD double trunc_div_d(double a, double d, double inv) {
+  const double q = floor_div_d(fabs(a), d, inv);
+  return a < 0.0 ? -q : q;
+}
+
+constexpr double kW = 1e6, kInvW = 1e-6, kHalfW = 5e5;
+
+// wsad_mul(a, b) = I128Div(a * b + HALF_WSAD, WSAD) for |a * b| < 2^50 (signed_decimal.cairo:110-112).
+SVOC_HD double wmul_d(double a, double b) { return trunc_div_d(fma(a, b, kHalfW), kW, kInvW); }
+
+// quadratic_deviation(a, b) = wsad_mul(a - b, a - b) for |a - b| < 2^25 (math.cairo:170-173).
+SVOC_HD double qdev_d(double a, double b) {
+  const double d = a - b;
+  return floor_div_d(fma(d, d, kHalfW), kW, kInvW);
+}
+
+// wsad_div(a, b) = I128Div(a * WSAD + I128Div(b, 2), b) for 1 <= b < 2^31, |a| < 2^31
+// (signed_decimal.cairo:114-116); inv = 1.0 / b.
+SVOC_HD double wdiv_d(double a, double b, double inv) {
+  return trunc_div_d(fma(a, kW, floor(b * 0.5)), b, inv);
+}
+
+// sqrt (math.cairo:271-292) for integral 0 <= v < 2^31: the same Newton steps and stop rule
+// (g == previous g, at most 50 iterations).  Returns false where the contract reverts: a zero
+// divisor (sqrt(1) -- g = 0 after the first halving).
+SVOC_HD bool wsqrt_d(double v, double& out) {
+  if (v == 0.0) {
+    out = 0.0;
+    return true;
+  }
+  double g = floor(v * 0.5);
+  double g2 = g + kW;
+  for (int i = 0; i < MAX_SQRT_ITERATIONS; ++i) {
+    if (g == g2) break;
+    if (g == 0.0) return false;
+    const double n = wdiv_d(v, g, 1.0 / g);
+    g2 = g;
+    g = floor((g + n) * 0.5);
+  }
+  out = g;
+  return true;
+}
+
+}  // namespace svoc

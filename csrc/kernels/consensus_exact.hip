@@ -122,7 +122,7 @@ __device__ i128 smooth_median_w(const Rows<RPL>& r, const Grp<GS>& g, int n_rows
   return idiv_pos64(add(a, b, st), 2, st);
 }
 
-template <int RPL, int GS>
+template <int RPL, int GS, class T>
 __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
   constexpr int IPW = 64 / GS;  // instances per wave (= per workgroup)
   extern __shared__ __attribute__((aligned(16))) int64_t lds[];
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
   int64_t* vars = ws + 3 * D;
   int64_t* sk = ws + 4 * D;
   int64_t* ku = ws + 5 * D;
-  const int64_t* X = p.values + (int64_t)b * N * D;
+  const T* X = (const T*)p.values + (int64_t)b * N * D;
   int st = ST_OK;  // group-uniform by construction (every lane runs the same checked reductions)
 
   Rows<RPL> rows;
@@ -311,7 +311,7 @@ static int launch_exact(const ExactParams& p, hipStream_t stream) {
   constexpr int IPW = 64 / GS;
   const size_t lds = p.work ? 0 : (size_t)IPW * p.D * 6 * sizeof(int64_t);
   if (lds > 64 * 1024) return -2;  // the binding passes a global workspace for wide instances
-  auto k = consensus_exact_kernel<RPL, GS>;
+  auto k = p.val32 ? consensus_exact_kernel<RPL, GS, int32_t> : consensus_exact_kernel<RPL, GS, int64_t>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(k, dim3((unsigned)((p.B + IPW - 1) / IPW)), dim3(64), lds, stream, p);
@@ -322,12 +322,13 @@ static int launch_exact(const ExactParams& p, hipStream_t stream) {
 
 using namespace svoc;
 
-// Lane group per instance: the smallest of 8 / 16 / 32 lanes holding one row each (several
-// instances per wave, e.g. the deployed 7 x 6 config runs 8 per wave), else a full wave with 1 or 4
-// rows per lane.  Wide instances (6*D int64 > LDS budget) use the HBM workspace and a full wave.
-extern "C" int svoc_exact_round(const ExactParams* p, hipStream_t stream) {
-  if (p->B <= 0) return 0;
-  if (p->N < 1 || p->N > 256 || p->D < 1) return -1;
+extern "C" int svoc_exact_round_wsad(const ExactParams* p, hipStream_t stream);
+
+// i128 kernel over every active instance (the reference-order path; any status).  Lane group per
+// instance: the smallest of 8 / 16 / 32 lanes holding one row each (several instances per wave, e.g.
+// the deployed 7 x 6 config runs 8 per wave), else a full wave with 1 or 4 rows per lane.  Wide
+// instances (6*D int64 > LDS budget) use the HBM workspace and a full wave.
+static int exact_round_i128(const ExactParams* p, hipStream_t stream) {
   const size_t per_inst = (size_t)p->D * 6 * sizeof(int64_t);
   if (!p->work) {
     if (p->N <= 8 && 8 * per_inst <= 64 * 1024) return launch_exact<1, 8>(*p, stream);
@@ -335,4 +336,23 @@ extern "C" int svoc_exact_round(const ExactParams* p, hipStream_t stream) {
     if (p->N <= 32 && 2 * per_inst <= 64 * 1024) return launch_exact<1, 32>(*p, stream);
   }
   return p->N <= 64 ? launch_exact<1, 64>(*p, stream) : launch_exact<4, 64>(*p, stream);
+}
+
+// Exact round: the column-parallel kernel (consensus_wsad.hip) takes every instance it can prove
+// bit-exact in fp64 / int32 arithmetic (constrained, values in [0, 1e6], a successful round); the
+// others -- any revert, out-of-domain values, unconstrained or legacy rounds -- are flagged and run
+// through the i128 kernel right after it on the same stream.
+extern "C" int svoc_exact_round(const ExactParams* p, hipStream_t stream) {
+  if (p->B <= 0) return 0;
+  if (p->N < 1 || p->N > 256 || p->D < 1) return -1;
+  if (p->stage && p->fallback) {
+    const int rc = svoc_exact_round_wsad(p, stream);
+    if (rc != -2) {
+      if (rc != 0 || p->skip_fallback) return rc;
+      ExactParams q = *p;
+      q.active = p->fallback;
+      return exact_round_i128(&q, stream);
+    }
+  }
+  return exact_round_i128(p, stream);
 }

@@ -1,0 +1,356 @@
+// Column-parallel exact (wsad) consensus round: bit-identical to the i128 kernel (consensus_exact.hip)
+// and to the CPU golden engine (csrc/engine/reference_cpu.cpp) on every round it accepts.
+//
+// Semantics: contract/src/contract.cairo:442-503 (constrained) in the exact integer arithmetic of
+// signed_decimal.cairo:52-116 and math.cairo:113-398 (smooth median, quadratic risk, reliability,
+// rank mask, mean, variance, sqrt, skewness, kurtosis; Appendix A.2 of SURVEY.md).  Accepted:
+// constrained, non-legacy rounds over values in [0, 1e6] (the interval the contract enforces on
+// every update, contract.cairo:591-593) that succeed.  Everything else -- every revert, whose status
+// code must come out in the reference's stage order, out-of-domain values, unconstrained or legacy
+// rounds -- is flagged in p.fallback and recomputed right after by the i128 kernel.
+//
+// Why it is fast: the i128 kernel gives each instance one wave and loops over the columns with a
+// group reduction per column per statistic (5 GB/s at 64 x 1024).  Here a lane owns a COLUMN (NSEG
+// lanes of 64 rows each for N > 64: the fast kernels' lane-group layout, one 32-bit key per lane
+// instead of a bf16 pair), every per-column statistic is lane-local, and the integer arithmetic runs
+// in fp64 on integral values (wsad_fast.hpp: exact under bounds the constrained domain guarantees):
+//   pass 1: smooth median per column (median_group on u32 keys with the sentinel split), the
+//           column's quadratic deviations qdev(x, c1), summed over the wave's columns by a
+//           transposing butterfly -> per-oracle qr (u64, exact) in LDS;
+//   rank mask (qr asc, idx desc; sort.cairo:96-101), rel1 / rel2 by the wsad.hpp routines;
+//   pass 2: smooth median of the reliable rows (the others become sentinels), then from the same
+//           registers: mean, variance, wsqrt, z = wsad_div(x - mean, sd), wsad_mul powers ->
+//           skewness / kurtosis.  Per-column results are staged in p.stage and copied to the outputs
+//           only after every column passed its checks: a flagged instance leaves them untouched.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "svoc/bufload.hpp"
+#include "svoc/launch.hpp"
+#include "svoc/sortnet.hpp"
+#include "svoc/status.hpp"
+#include "svoc/wsad.hpp"
+#include "svoc/wsad_fast.hpp"
+
+namespace svoc {
+
+constexpr uint32_t kWsadMax = 1000000u;
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+// The lane's column value in row `soff` (bytes): int32, or the low word of an int64 (`hiw` gets its
+// high word, which must be 0 for a value in [0, 1e6]).
+template <bool V32>
+SVOC_DEV uint32_t wload(__amdgpu_buffer_rsrc_t rs, int voff, int soff, uint32_t& hiw) {
+  if constexpr (V32) {
+    hiw = 0;
+    return bload(rs, voff, soff);
+  } else {
+    const u32x2_t v = __builtin_amdgcn_raw_buffer_load_b64(rs, voff, soff, 0);
+    hiw = v[1];
+    return v[0];
+  }
+}
+
+// Transposing butterfly over the wave's P columns (the fast kernels' qr tree, exact u32 sums):
+// stage L exchanges with lane ^ (P >> L); the lane ends with rows I + base(lane) of all P columns.
+template <int L, int I, int P>
+SVOC_DEV uint32_t qtree(const uint32_t (&q)[64], int lane) {
+  if constexpr (L == 0) {
+    return q[I];
+  } else {
+    constexpr int msk = P >> L;
+    const uint32_t lo_v = qtree<L - 1, I, P>(q, lane);
+    const uint32_t hi_v = qtree<L - 1, I + (64 >> L), P>(q, lane);
+    const bool up = (lane & msk) != 0;
+    const uint32_t send = up ? lo_v : hi_v;
+    const uint32_t keep = up ? hi_v : lo_v;
+    return keep + xor_lane_u32<msk>(send);
+  }
+}
+template <int P, int... Is>
+SVOC_DEV void qtree_all(const uint32_t (&q)[64], int lane, uint64_t* acc, std::integer_sequence<int, Is...>) {
+  ((acc[Is] += qtree<__builtin_ctz(P), Is, P>(q, lane)), ...);
+}
+
+// sum over the NSEG lanes of a column group (lanes lane ^ t*P)
+template <int NSEG, int P, class T>
+SVOC_DEV T group_sum(T v) {
+#pragma unroll
+  for (int t = 1; t < NSEG; t <<= 1) v += __shfl_xor(v, t * P);
+  return v;
+}
+
+template <int NSEG, int WAVES, bool V32>
+__global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams p) {
+  constexpr int P = 64 / NSEG;      // columns per wave
+  constexpr int NPAD = 64 * NSEG;   // padded oracle rows
+  constexpr int W = WAVES * P;      // columns per tile
+  constexpr int NT = WAVES * 64;
+  constexpr int KEEP = 64 / P;      // qr rows a lane holds after the butterfly
+  constexpr int ESZ = V32 ? 4 : 8;
+  __shared__ uint64_t qr_part[WAVES * NPAD];
+  __shared__ uint64_t qr_lds[NPAD];
+  __shared__ uint64_t relmask[4], lowmask[4];
+  __shared__ int64_t rels[2];
+  __shared__ int flag;
+
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (p.active && !p.active[b]) {
+    if (tid == 0) p.fallback[b] = 0;
+    return;
+  }
+  if (tid == 0) flag = 0;
+  const int seg = lane / P, cw = lane % P;
+  const int N = p.N, D = p.D;
+  const int rowb = D * ESZ;
+  const __amdgpu_buffer_rsrc_t rs =
+      instance_rsrc((const unsigned char*)p.values + (int64_t)b * N * rowb, (uint32_t)(N * rowb));
+  int32_t* const stg = p.stage + (int64_t)b * 4 * D;   // [4][D]: c1, consensus, skewness, kurtosis
+  const int nslab = (D + W - 1) / W;
+  const int lo1 = (NPAD - N + 1) >> 1;   // pass-1 sentinel split (rows >= N): -inf first, then +inf
+  const int nv = N - seg * 64;           // this lane's rows < nv are real
+  const int nl = N + lo1 - seg * 64;
+  const int seg_off = seg * 64 * rowb;
+  const uint32_t pol = group_polarity<NSEG>(seg);
+  uint32_t badv = 0;                     // a value outside [0, 1e6]
+  uint32_t hw_;                          // (high words of re-read values: validated in pass 1)
+
+  uint64_t acc[KEEP];
+#pragma unroll
+  for (int k = 0; k < KEEP; ++k) acc[k] = 0;
+
+  // ------------------------------------------------------------ pass 1 (contract.cairo:455-463)
+#pragma nounroll
+  for (int s = 0; s < nslab; ++s) {
+    const int col = s * W + wave * P + cw;
+    const bool vc = col < D;
+    const int vo = seg_off + (vc ? col : 0) * ESZ;
+    uint32_t c1;
+    {
+      uint32_t r[64];
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        uint32_t hw;
+        const uint32_t x = wload<V32>(rs, vo, i * rowb, hw);
+        const bool real = i < nv;
+        badv |= (vc && real && (x > kWsadMax || hw != 0)) ? 1u : 0u;   // outside [0, 1e6]
+        r[i] = (real ? x : (i < nl ? 0u : ~0u)) ^ pol;
+      }
+      uint32_t lo, hi;
+      median_group<NSEG>(r, lo, hi);   // smooth median: ranks N/2 - 1, N/2 (math.cairo:113-126)
+      c1 = (lo + hi) >> 1;             // idiv_pos64(a + b, 2) of non-negative values
+    }
+    if (seg == 0 && vc) stg[col] = (int32_t)c1;
+    __builtin_amdgcn_sched_barrier(0);
+    // quadratic risk (math.cairo:225-238): this column's qdev of every row, summed over the columns
+    uint32_t q[64];
+    const double cd = (double)c1;
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
+      q[i] = (vc && i < nv) ? (uint32_t)qdev_d((double)x, cd) : 0u;
+    }
+    qtree_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
+  }
+  {
+    int base = 0;
+#pragma unroll
+    for (int h = 32, msk = P / 2; msk >= 1; h >>= 1, msk >>= 1) base += (lane & msk) ? h : 0;
+#pragma unroll
+    for (int k = 0; k < KEEP; ++k) qr_part[wave * NPAD + seg * 64 + base + k] = acc[k];
+  }
+  __syncthreads();
+  for (int t = tid; t < NPAD; t += NT) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) v += qr_part[w * NPAD + t];
+    qr_lds[t] = v;
+  }
+  __syncthreads();
+
+  // ------------------------------------------------------------ rank mask (contract.cairo:345-363)
+  const int f = p.n_failing;
+  const int R = N - f;
+  for (int base = 0; base < NPAD; base += NT) {
+    const int t = base + tid;
+    bool rel = false;
+    if (t < N) {
+      const uint64_t myq = qr_lds[t];
+      int rank = 0;
+      for (int j = 0; j < N; ++j) {
+        const uint64_t qj = qr_lds[j];
+        rank += (qj < myq || (qj == myq && j > t)) ? 1 : 0;   // (qr asc, idx desc)
+      }
+      rel = rank < R;
+    }
+    const uint64_t bal = __ballot(rel);
+    if (lane == 0 && (t >> 6) < 4) relmask[t >> 6] = bal;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    // reliabilities with the wsad.hpp routines (contract.cairo:436-439); any failure -> i128 kernel
+    int st = ST_OK;
+    i128 s_all = 0, s_rel = 0;
+    for (int t = 0; t < N; ++t) {
+      const i128 qv = (i128)qr_lds[t];
+      s_all = add(s_all, qv, st);
+      if ((relmask[t >> 6] >> (t & 63)) & 1) s_rel = add(s_rel, qv, st);
+    }
+    const i128 rel1 = constrained_reliability(idiv(s_all, (i128)N, st), D, st);
+    if (!in_unit_interval(rel1)) st = ST_RELIABILITY_INTERVAL;
+    if (f < 0 || R < 4) st = ST_TOO_FEW_RELIABLE;
+    i128 rel2 = 0;
+    if (st == ST_OK) {
+      rel2 = constrained_reliability(idiv(s_rel, (i128)R, st), D, st);
+      if (!in_unit_interval(rel2)) st = ST_RELIABILITY_INTERVAL;
+    }
+    rels[0] = (int64_t)rel1;
+    rels[1] = (int64_t)rel2;
+    if (st != ST_OK) flag = 1;
+    // pass-2 sentinel split: the first (NPAD - R + 1) / 2 non-reliable rows (row order) become -inf
+    int need = (NPAD - R + 1) >> 1;
+    for (int w = 0; w < 4; ++w) {
+      uint64_t nr = w < NSEG ? ~relmask[w] : 0ull, lm = 0ull;
+      while (need > 0 && nr) {
+        const uint64_t bit = nr & (0ull - nr);
+        lm |= bit;
+        nr ^= bit;
+        --need;
+      }
+      lowmask[w] = lm;
+    }
+  }
+  if (badv) flag = 1;
+  __syncthreads();
+  if (flag) {
+    if (tid == 0) p.fallback[b] = 1;
+    return;
+  }
+
+  // ------------------------------------------------------------ pass 2 (contract.cairo:476-500)
+  const uint64_t mymask = relmask[seg];
+  const uint64_t mylow = lowmask[seg];
+  const double Rd = (double)R, invR = 1.0 / Rd;
+  const double k3 = (double)((R - 1) * (R - 2)), ik3 = 1.0 / k3;
+  bool bad = false;
+#pragma nounroll
+  for (int s = 0; s < nslab; ++s) {
+    const int col = s * W + wave * P + cw;
+    const bool vc = col < D;
+    const int vo = seg_off + (vc ? col : 0) * ESZ;
+    uint64_t mm = mymask, ml = mylow;
+    asm volatile("" : "+v"(mm), "+v"(ml));   // keep the 64 row masks out of the slab loop's live set
+    uint32_t cons;
+    {
+      uint32_t r[64];
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
+        const uint32_t mk = bit_mask(mm, i), low = bit_mask(ml, i);
+        r[i] = ((x & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else -inf (low) / +inf
+      }
+      uint32_t lo, hi;
+      median_group<NSEG>(r, lo, hi);
+      cons = (lo + hi) >> 1;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // the column is re-read per statistic (L2-hot) instead of held in 64 more VGPRs: the fp64 work
+    // below needs the registers, and occupancy hides the re-read latency
+    // mean (math.cairo:240-254): idiv(sum, R) of non-negative values
+    uint32_t sx = 0;
+#pragma unroll 16
+    for (int i = 0; i < 64; ++i) sx += wload<V32>(rs, vo, i * rowb, hw_) & bit_mask(mm, i);
+    sx = group_sum<NSEG, P>(sx);
+    const double mu = floor_div_d((double)sx, Rd, invR);
+    // population variance (math.cairo:208-222): mean of qdev(x, mu) over the reliable rows
+    uint32_t sv = 0;
+#pragma unroll 16
+    for (int i = 0; i < 64; ++i) {
+      const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
+      sv += bit_mask(mm, i) & (uint32_t)qdev_d((double)x, mu);
+    }
+    sv = group_sum<NSEG, P>(sv);
+    const double var = floor_div_d((double)sv, Rd, invR);
+    // var 0 (sqrt 0 -> wsad_div by zero) and var 1 (sqrt(1) divides by zero) revert the round
+    double sd = 1.0;
+    const bool ok_sd = var >= 2.0 && wsqrt_d(var, sd);
+    if (vc && !ok_sd) bad = true;
+    const double isd = 1.0 / sd;
+    // z-score powers (math.cairo:320-363), reliable rows only (a masked row has z = 0: all powers 0)
+    double s3 = 0.0, s4 = 0.0;
+#pragma unroll 8
+    for (int i = 0; i < 64; ++i) {
+      const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
+      const double dx = bit_mask(mm, i) ? (double)x - mu : 0.0;
+      const double z = wdiv_d(dx, sd, isd);
+      const double z2 = wmul_d(z, z);
+      bad = bad || z2 >= 33554432.0;   // 2^25: keeps every product below wmul_d's 2^50 bound
+      s3 += wmul_d(z2, z);
+      s4 += wmul_d(z2, z2);
+    }
+    s3 = group_sum<NSEG, P>(s3);
+    s4 = group_sum<NSEG, P>(s4);
+    // skewness = idiv(s3 * n, (n-1)(n-2)); kurtosis = idiv(idiv(s4 n (n+1), n-1) - 3W(n-1)^2, (n-2)(n-3))
+    const double sk = trunc_div_d(s3 * Rd, k3, ik3);
+    const int64_t t1 = ((int64_t)s4 * (int64_t)R * (int64_t)(R + 1)) / (int64_t)(R - 1);
+    const int64_t t2 = 3ll * 1000000ll * (int64_t)(R - 1) * (int64_t)(R - 1);
+    const int64_t ku = (t1 - t2) / ((int64_t)(R - 2) * (int64_t)(R - 3));
+    if (vc && (fabs(sk) > 2147483647.0 || ku > INT32_MAX || ku < INT32_MIN)) bad = true;
+    if (seg == 0 && vc) {
+      stg[D + col] = (int32_t)cons;
+      stg[2 * D + col] = (int32_t)sk;
+      stg[3 * D + col] = (int32_t)ku;
+    }
+  }
+  if (bad) flag = 1;
+  __syncthreads();
+  if (flag) {
+    if (tid == 0) p.fallback[b] = 1;
+    return;
+  }
+
+  // ------------------------------------------------------------ commit (a successful round)
+  const int64_t ob = (int64_t)b * D;
+  for (int c = tid; c < D; c += NT) {
+    if (p.c1) p.c1[ob + c] = stg[c];
+    p.consensus[ob + c] = stg[D + c];
+    p.skew[ob + c] = stg[2 * D + c];
+    p.kurt[ob + c] = stg[3 * D + c];
+  }
+  for (int t = tid; t < N; t += NT) {
+    p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
+    p.qr[(int64_t)b * N + t] = (int64_t)qr_lds[t];
+  }
+  if (tid == 0) {
+    p.rel[2 * (int64_t)b] = rels[0];
+    p.rel[2 * (int64_t)b + 1] = rels[1];
+    p.status[b] = ST_OK;
+    p.fallback[b] = 0;
+  }
+}
+
+template <int NSEG>
+static int launch_wsad(const ExactParams& p, hipStream_t stream) {
+  constexpr int WAVES = 4;
+  auto k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true> : consensus_wsad_kernel<NSEG, WAVES, false>;
+  hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+  return (int)hipGetLastError();
+}
+
+}  // namespace svoc
+
+using namespace svoc;
+
+// -2: not applicable (the caller runs the i128 kernel on every instance).
+extern "C" int svoc_exact_round_wsad(const ExactParams* p, hipStream_t stream) {
+  if (p->B <= 0) return 0;
+  if (!p->constrained || p->legacy || p->N < 4 || p->N > 256 || p->D < 1) return -2;
+  if (!p->stage || !p->fallback) return -2;
+  if ((int64_t)p->N * p->D * (p->val32 ? 4 : 8) >= (1ll << 31)) return -2;   // 32-bit buffer offsets
+  if (p->N <= 64) return launch_wsad<1>(*p, stream);
+  if (p->N <= 128) return launch_wsad<2>(*p, stream);
+  return launch_wsad<4>(*p, stream);
+}

@@ -23,7 +23,7 @@ __device__ __forceinline__ bool in_range(const UpdateParams& p, int64_t u, int d
     const float f = ((const float*)p.upd)[u * p.D + d];
     return f >= 0.f && f <= 1.f;
   }
-  const int64_t v = ((const int64_t*)p.upd)[u * p.D + d];
+  const int64_t v = p.dtype == 3 ? (int64_t)((const int32_t*)p.upd)[u * p.D + d] : ((const int64_t*)p.upd)[u * p.D + d];
   return v >= 0 && v <= 1000000;
 }
 
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void upd_validate_kernel(UpdateParams p) {
     }
   }
   bool fin = true;
-  if (in && st == ST_OK && !p.constrained && p.dtype != 2)
+  if (in && st == ST_OK && !p.constrained && p.dtype <= 1)
     for (int d = sub; d < p.D; d += L) fin = fin && finite_at(p, u, d);
   ok = group_all<L>(ok);  // all lanes reach the ballots (no early return above)
   fin = group_all<L>(fin);
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
       } else {
         for (int d = sub; d < p.D; d += L) {
           if (p.constrained) ok = ok && in_range(p, u, d);
-          else if (p.dtype != 2) fin = fin && finite_at(p, u, d);
+          else if (p.dtype <= 1) fin = fin && finite_at(p, u, d);
         }
       }
     }

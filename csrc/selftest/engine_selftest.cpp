@@ -15,6 +15,7 @@
 
 #include "engine.hpp"
 #include "svoc/governance.hpp"
+#include "svoc/wsad_fast.hpp"
 #include "svoc_io.hpp"
 
 using namespace svoc;
@@ -141,9 +142,63 @@ static void io_roundtrip() {
   std::remove(path.c_str());
 }
 
+// The fp64 exact fast paths (wsad_fast.hpp, used by the column-parallel exact kernel) against the
+// i128 routines of wsad.hpp, on random and boundary operands inside their stated bounds.
+static void wsad_fast_paths() {
+  std::mt19937_64 rng(12345);
+  auto uni = [&](int64_t lo, int64_t hi) { return lo + (int64_t)(rng() % (uint64_t)(hi - lo + 1)); };
+  int bad = 0;
+  for (int it = 0; it < 2000000 && bad < 10; ++it) {
+    int st = ST_OK;
+    // quadratic deviation of constrained values
+    const int64_t a = uni(0, 1000000), b = uni(0, 1000000);
+    if ((int64_t)qdev_d((double)a, (double)b) != (int64_t)qdev(a, b, st)) ++bad;
+    // wsad_mul of z-score sized operands, both signs
+    const int64_t z = uni(-(1 << 25), 1 << 25), y = uni(-(1 << 24), 1 << 24);
+    if ((int64_t)wmul_d((double)z, (double)y) != (int64_t)wmul(z, y, st)) ++bad;
+    // wsad_div by a standard deviation
+    const int64_t num = uni(-1000000, 1000000), sd = uni(1, 2000000);
+    if ((int64_t)wdiv_d((double)num, (double)sd, 1.0 / (double)sd) != (int64_t)wdiv(num, sd, st)) ++bad;
+    // truncating division (means, variances)
+    const int64_t s = uni(-(1ll << 50), 1ll << 50), d = uni(1, 1 << 30);
+    if ((int64_t)trunc_div_d((double)s, (double)d, 1.0 / (double)d) != (int64_t)idiv(s, d, st)) ++bad;
+    // sqrt of variances
+    if (it % 16 == 0) {
+      const int64_t v = it % 32 == 0 ? uni(0, 2000000) : uni(0, (1ll << 31) - 1);
+      int st2 = ST_OK;
+      const int64_t ref = (int64_t)wsqrt(v, st2);
+      double out;
+      const bool ok = wsqrt_d((double)v, out);
+      if (ok != (st2 == ST_OK) || (ok && (int64_t)out != ref)) ++bad;
+    }
+    CHECK(st == ST_OK);
+  }
+  for (int64_t v : {(int64_t)0, (int64_t)1, (int64_t)2, (int64_t)3, (int64_t)4, (int64_t)999999, (int64_t)1000000, (int64_t)1000001, (int64_t)((1ll << 31) - 1)}) {
+    int st2 = ST_OK;
+    const int64_t ref = (int64_t)wsqrt(v, st2);
+    double out;
+    const bool ok = wsqrt_d((double)v, out);
+    CHECK(ok == (st2 == ST_OK) && (!ok || (int64_t)out == ref));
+  }
+  // boundary quotients: remainders 0 and d - 1 around large dividends
+  for (int64_t d : {(int64_t)1, (int64_t)2, (int64_t)3, (int64_t)7, (int64_t)1000000, (int64_t)999983, (int64_t)((1ll << 31) - 1)}) {
+    for (int64_t q : {(int64_t)0, (int64_t)1, (int64_t)12345, (int64_t)((1ll << 51) / d - 2)}) {
+      for (int64_t r : {(int64_t)0, d - 1}) {
+        const int64_t t = q * d + r;
+        if (t >= (1ll << 51)) continue;
+        int st = ST_OK;
+        CHECK((int64_t)trunc_div_d((double)t, (double)d, 1.0 / (double)d) == (int64_t)idiv(t, d, st));
+        CHECK((int64_t)trunc_div_d(-(double)t, (double)d, 1.0 / (double)d) == (int64_t)idiv(-t, d, st));
+      }
+    }
+  }
+  CHECK(bad == 0);
+}
+
 int main(int argc, char** argv) {
   const int threads = argc > 1 ? std::atoi(argv[1]) : 8;
   golden_fixture();
+  wsad_fast_paths();
   batch_vs_single(threads);
   governance_flow();
   io_roundtrip();

@@ -22,9 +22,10 @@ from .status import ConsensusRevert, Status
 class ConsensusService:
     """B contracts sharing one configuration. ``mode='exact'`` is bit-compatible with the contract."""
 
-    def __init__(self, cfg: ConsensusConfig, batch: int, admins, oracles, device="cpu", mode: str = "exact"):
+    def __init__(self, cfg: ConsensusConfig, batch: int, admins, oracles, device="cpu", mode: str = "exact",
+                 storage=None):
         self.cfg = cfg
-        self.engine = ConsensusEngine(cfg, batch, device=device, mode=mode)
+        self.engine = ConsensusEngine(cfg, batch, device=device, mode=mode, storage=storage)
         self.gov = Governance(batch, cfg.n_admins, cfg.n_oracles, device, cfg.enable_oracle_replacement,
                               cfg.required_majority)
         self.gov.set_addresses(admins, oracles)

@@ -11,9 +11,12 @@ mirrors its ``Storage`` struct (contract.cairo:80-102) as tensors with a leading
 
 Two numeric modes share one semantics:
 
-* ``exact``: int64 wsad storage, the bit-exact HIP kernel (csrc/kernels/consensus_exact.hip) or the
-  C++ CPU engine; updates are transactions (a reverted round rolls the update back, exactly like a
-  reverted Starknet tx) and are replayed in order per instance.
+* ``exact``: int64 wsad storage (or ``storage="int32"`` for constrained configs: every value is in
+  [0, 1e6], half the bytes), the bit-exact HIP kernels -- the column-parallel one
+  (csrc/kernels/consensus_wsad.hip) for the rounds it can prove, the i128 one
+  (csrc/kernels/consensus_exact.hip) for the rest -- or the C++ CPU engine; updates are transactions
+  (a reverted round rolls the update back, exactly like a reverted Starknet tx) and are replayed in
+  order per instance.
 * ``fast``: bf16 storage / fp32 math through the fused HIP kernel (csrc/kernels/consensus_fast.hip).
   Updates inside one step are coalesced (last writer wins) -- exact for the reference because a
   round is a pure function of the current values (survey §2.8-13); a reverted round keeps the stored
@@ -39,7 +42,7 @@ def _round_up(x: int, m: int) -> int:
 
 class ConsensusEngine:
     def __init__(self, cfg: ConsensusConfig, batch: int, device="cuda", mode: str = "fast",
-                 storage: str = "bf16"):
+                 storage: Optional[str] = None):
         cfg.validate()
         if mode not in ("fast", "exact"):
             raise ValueError("mode must be 'fast' or 'exact'")
@@ -53,15 +56,19 @@ class ConsensusEngine:
         B, N, D = self.B, self.N, self.D
         dev = self.device
         if mode == "fast":
-            self.vdtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[storage]
+            self.vdtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[storage or "bf16"]
             if self.device.type == "cuda" and self.vdtype != torch.bfloat16:
                 raise ValueError("the GPU fast path stores oracle values in bf16")
             self.ld = _round_up(D, 8)              # 16-B rows for global_load_lds
             odt = torch.float32
         else:
-            self.vdtype = torch.int64
+            self.vdtype = {"int64": torch.int64, "int32": torch.int32}[storage or "int64"]
+            if self.vdtype == torch.int32 and not cfg.constrained:
+                raise ValueError("int32 wsad storage is for constrained configs (values in [0, 1e6])")
             self.ld = D
             odt = torch.int64
+        self.storage = {torch.bfloat16: "bf16", torch.float32: "fp32", torch.int64: "int64",
+                        torch.int32: "int32"}[self.vdtype]
         self.values = torch.zeros(B, N, self.ld, dtype=self.vdtype, device=dev)
         self.enabled = torch.zeros(B, N, dtype=torch.uint8, device=dev)
         self.n_active = torch.zeros(B, dtype=torch.int32, device=dev)
@@ -88,7 +95,7 @@ class ConsensusEngine:
     @staticmethod
     def bytes_per_instance(n: int, d: int, mode: str = "fast") -> int:
         """HBM bytes of state per instance (survey §7.6 sizing)."""
-        s = 2 if mode == "fast" else 8
+        s = {"fast": 2, "exact": 8, "exact32": 4}[mode]
         o = 4 if mode == "fast" else 8
         ld = _round_up(d, 8) if mode == "fast" else d
         return n * ld * s + 4 * d * o + n * (1 + 1 + o + 4) + 2 * o + 4 + 4 + 2
@@ -98,7 +105,10 @@ class ConsensusEngine:
         if self.mode == "exact":
             if vals.dtype.is_floating_point:
                 raise TypeError("exact mode takes int64 wsad values (use svoc.codec.float_to_wsad)")
-            return vals.to(self.device, torch.int64).contiguous()
+            v = vals.to(self.device, torch.int64)
+            if self.vdtype == torch.int32:   # out of int32 -> -1: rejected by the interval check, not wrapped
+                v = torch.where((v < -(2 ** 31)) | (v >= 2 ** 31), torch.full_like(v, -1), v)
+            return v.to(self.vdtype).contiguous()
         return vals.to(self.device, self.vdtype).contiguous()
 
     def apply_updates(self, inst: torch.Tensor, oracle: torch.Tensor, vals: torch.Tensor,
@@ -264,7 +274,7 @@ class ConsensusEngine:
         g = torch.Generator(device=self.device).manual_seed(seed)
         x = beta_failing_oracles(self.B, self.N, self.D, self.cfg.n_failing_oracles, a, g, self.device)
         if self.mode == "exact":
-            self.values[:, :, : self.D] = (x.double() * WSAD).to(torch.int64)
+            self.values[:, :, : self.D] = (x.double() * WSAD).to(torch.int64).to(self.vdtype)
         else:
             self.values[:, :, : self.D] = x.to(self.vdtype)
         self.enabled.fill_(1)

@@ -26,14 +26,14 @@ def save(svc, path: str) -> None:
     exact = e.mode == "exact"
     num = "i128" if exact else ""
     meta = dict(format=FORMAT, mode=e.mode, batch=e.B, config=svc.cfg.to_dict(),
-                value_dtype=str(e.vdtype).replace("torch.", ""), rounds=e.rounds)
+                value_dtype=str(e.vdtype).replace("torch.", ""), storage=e.storage, rounds=e.rounds)
     secs = [
         ("admins", g.admins, "felt"),
         ("unconstrained_max_spread", torch.tensor([svc.cfg.max_spread_wsad], dtype=torch.int64), "i128"),
         ("oracle_address", g.oracle_addr, "felt"),
         ("enabled", e.enabled, ""),
         ("reliable", e.reliable, ""),
-        ("oracles_values", e.values[:, :, :D].contiguous(), num),
+        ("oracles_values", e.values[:, :, :D].to(torch.int64 if exact else e.vdtype).contiguous(), num),
         ("n_active_oracles", e.n_active, ""),
         ("consensus_active", e.consensus_active.to(torch.uint8), ""),
         ("vote_matrix_columns", g.votes, ""),
@@ -67,7 +67,7 @@ def load(path: str, device="cpu"):
     B = int(meta["batch"])
     admins = [[limbs_to_address(x) for x in r] for r in t["admins"].tolist()]
     oracles = [[limbs_to_address(x) for x in r] for r in t["oracle_address"].tolist()]
-    svc = ConsensusService(cfg, B, admins, oracles, device=device, mode=meta["mode"])
+    svc = ConsensusService(cfg, B, admins, oracles, device=device, mode=meta["mode"], storage=meta.get("storage"))
     e, g = svc.engine, svc.gov
     dev = e.device
     e.values[:, :, : e.D].copy_(t["oracles_values"].to(dev, e.vdtype))

@@ -108,3 +108,24 @@ def test_unconstrained_updates_reject_non_finite():
     st = e.apply_updates(torch.tensor([0, 0, 1, 1]), torch.tensor([0, 1, 2, 3]), vals)
     assert st.tolist() == [Status.OK, Status.NON_FINITE, Status.NON_FINITE, Status.OK]
     assert e.values[0, 0, :3].tolist() == [1.0, 2.0, 3.0] and int(e.enabled[0, 1]) == 0
+
+
+def test_exact_int32_storage_matches_int64_cpu():
+    """int32 wsad storage (constrained) gives the identical exact round as int64 storage."""
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    cfg = ConsensusConfig(n_oracles=16, dimension=20, n_failing_oracles=3, constrained=True)
+    e32 = ConsensusEngine(cfg, 6, device="cpu", mode="exact", storage="int32")
+    e64 = ConsensusEngine(cfg, 6, device="cpu", mode="exact")
+    assert e32.values.dtype == torch.int32
+    for e in (e32, e64):
+        e.randomize(seed=2)
+        e.run_round()
+    for k in ("consensus", "skew", "kurt", "rel", "qr", "reliable", "c1", "status"):
+        assert torch.equal(getattr(e32, k), getattr(e64, k)), k
+    # an update beyond int32 is rejected (not wrapped into range)
+    st = e32.step(torch.tensor([0]), torch.tensor([1]), torch.tensor([[2 ** 32 + 5] * 20]))
+    assert int(st[0]) != 0
+    with pytest.raises(ValueError):
+        ConsensusEngine(ConsensusConfig(n_oracles=8, dimension=2, n_failing_oracles=1, constrained=False), 1,
+                        device="cpu", mode="exact", storage="int32")

@@ -1,0 +1,127 @@
+"""Column-parallel exact kernel (csrc/kernels/consensus_wsad.hip) vs the i128 kernel and the CPU engine.
+
+Every round it accepts must be bit-identical (consensus, c1, qr, reliable, rel1/rel2, skewness,
+kurtosis); every other round (reverts, out-of-domain values) goes to the i128 kernel, so the combined
+result equals the CPU golden engine everywhere.  Reference semantics: contract.cairo:442-503,
+signed_decimal.cairo:52-116, math.cairo:113-398.
+"""
+import os
+
+import pytest
+import torch
+
+from fixtures import GOLDEN, N_FAILING
+from helpers import alloc_exact_out, beta_oracles
+from svoc import ops as svops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+OUTS = ("c1", "consensus", "skew", "kurt", "rel", "qr", "reliable", "status")
+
+
+def _wsad(B, N, D, f, seed, a=20.0):
+    x, _ = beta_oracles(B, N, D, f, a=a, seed=seed, dtype=torch.float64)
+    return (x[:, :, :D] * 1e6).to(torch.int64).contiguous()
+
+
+def _run(values, f, env=None, active=None):
+    B, N, D = values.shape
+    o = alloc_exact_out(B, N, D, values.device)
+    old = {k: os.environ.get(k) for k in ("SVOC_EXACT_I128", "SVOC_EXACT_WSAD_ONLY")}
+    try:
+        for k in old:
+            os.environ.pop(k, None)
+        os.environ.update(env or {})
+        svops.ops().exact_round(values, active, f, True, 0, o["c1"], o["consensus"], o["skew"], o["kurt"],
+                                o["rel"], o["qr"], o["reliable"], o["status"], False)
+        torch.cuda.synchronize()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    return {k: v.cpu() for k, v in o.items()}
+
+
+SHAPES = [(4, 3, 0), (7, 6, 2), (16, 33, 3), (50, 300, 5), (64, 1024, 8), (64, 1000, 20), (100, 260, 10),
+          (128, 512, 16), (200, 136, 20), (256, 600, 32), (256, 64, 100), (33, 1, 4)]
+
+
+@pytest.mark.parametrize("N,D,f", SHAPES)
+@pytest.mark.parametrize("dtype", [torch.int64, torch.int32])
+def test_wsad_kernel_bit_exact(N, D, f, dtype):
+    B = 16
+    v = _wsad(B, N, D, f, seed=N * 1000 + D)
+    vg = v.to(DEV, dtype)
+    fast = _run(vg, f, {"SVOC_EXACT_WSAD_ONLY": "1"})   # the column-parallel kernel alone
+    ref = _run(v.to(DEV), f, {"SVOC_EXACT_I128": "1"})   # the i128 kernel alone
+    took = fast["status"] == 0
+    assert took.sum() >= B - 1, fast["status"]         # it takes (almost) every round of Beta data
+    for k in OUTS:
+        assert torch.equal(fast[k][took], ref[k][took]), k
+    comb = _run(vg, f)                                   # dispatcher: column-parallel + i128 fallback
+    for k in OUTS:
+        assert torch.equal(comb[k], ref[k]), k
+
+
+def test_wsad_kernel_matches_cpu_engine():
+    B, N, D, f = 24, 64, 257, 8
+    v = _wsad(B, N, D, f, seed=5)
+    g = _run(v.to(DEV, torch.int32), f)
+    o = alloc_exact_out(B, N, D, "cpu")
+    svops.ops().exact_round(v, None, f, True, 0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"], o["qr"],
+                            o["reliable"], o["status"], False)
+    for k in OUTS:
+        assert torch.equal(g[k], o[k]), k
+
+
+@pytest.mark.parametrize("name", [n for n in GOLDEN if GOLDEN[n][1]])
+def test_wsad_kernel_goldens(name):
+    values, constrained, ms, gold = GOLDEN[name]
+    v = torch.tensor([values] * 3, dtype=torch.int64, device=DEV)
+    o = _run(v, N_FAILING, {"SVOC_EXACT_WSAD_ONLY": "1"})
+    assert o["status"].tolist() == [0, 0, 0]
+    assert o["consensus"][2].tolist() == gold["consensus"]
+    assert o["rel"][1].tolist() == [gold["rel1"], gold["rel2"]]
+    assert o["skew"][0].tolist() == gold["skewness"]
+    assert o["kurt"][0].tolist() == gold["kurtosis"]
+    assert o["qr"][0].tolist() == gold["qr"]
+
+
+def test_wsad_kernel_flags_reverts_and_out_of_domain():
+    """Reverting rounds and values outside [0, 1e6] are left to the i128 kernel (same statuses as
+    the CPU engine, outputs untouched)."""
+    B, N, D, f = 8, 64, 128, 8
+    v = _wsad(B, N, D, f, seed=9)
+    v[1, :, 5] = 400000                       # zero variance column -> DIV_BY_ZERO in the contract
+    v[2, : N // 2 + 1, :] = 0                 # rel1 < 0 -> RELIABILITY_INTERVAL
+    v[2, N // 2 + 1:, :] = 1000000
+    v[3, 7, 3] = 1000001                      # outside the constrained domain
+    v[4, 2, 2] = -5
+    v[5, :, 9] = 0                            # zero variance at 0
+    v[5, 0, 9] = 1                            # ... except one ulp: variance rounds to 0 in wsad
+    only = _run(v.to(DEV), f, {"SVOC_EXACT_WSAD_ONLY": "1"})
+    assert only["status"].tolist()[:6] == [0, -1, -1, -1, -1, -1] and only["status"][6:].eq(0).all()
+    comb = _run(v.to(DEV), f)
+    o = alloc_exact_out(B, N, D, "cpu")
+    svops.ops().exact_round(v, None, f, True, 0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"], o["qr"],
+                            o["reliable"], o["status"], False)
+    for k in OUTS:
+        assert torch.equal(comb[k], o[k]), k
+    assert comb["status"][1].item() != 0 and comb["status"][2].item() != 0
+
+
+def test_engine_exact_int32_storage_gpu():
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    cfg = ConsensusConfig(n_oracles=64, dimension=512, n_failing_oracles=8, constrained=True)
+    e32 = ConsensusEngine(cfg, 32, device=DEV, mode="exact", storage="int32")
+    e64 = ConsensusEngine(cfg, 32, device=DEV, mode="exact")
+    for e in (e32, e64):
+        e.randomize(seed=4)
+        e.run_round()
+    torch.cuda.synchronize()
+    assert (e64.status == 0).all()
+    for k in ("consensus", "skew", "kurt", "rel", "qr", "reliable", "c1", "status"):
+        assert torch.equal(getattr(e32, k), getattr(e64, k)), k
