@@ -16,14 +16,17 @@ def main(argv=None):
     ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
     ap.add_argument("--db", default=None, help="SQLite corpus (reference schema)")
     ap.add_argument("--encoder", default="tiny", choices=["tiny", "base"])
+    ap.add_argument("--refresh", type=float, default=5.0, help="auto_fetch period in seconds (client/common.py:11)")
     ap.add_argument("-c", "--command", action="append", default=[], help="run a command and exit")
     a = ap.parse_args(argv)
-    cl = Client(device=a.device, mode=a.mode, db_path=a.db, encoder=a.encoder, dimension=a.dimension)
+    cl = Client(device=a.device, mode=a.mode, db_path=a.db, encoder=a.encoder, dimension=a.dimension,
+                refresh_rate=a.refresh)
     cl.flags["scraper"] = a.scraper
     cl.flags["live_mode"] = a.live_mode
     if a.command:
         for c in a.command:
             print(cl.query(c))
+        cl.close()
         return 0
     if not a.disable_startup_fetch:
         print(cl.query("resume"))
@@ -32,8 +35,10 @@ def main(argv=None):
         try:
             line = input("svoc> ")
         except EOFError:
+            cl.close()
             return 0
         if line.strip() == "exit":
+            cl.close()
             return 0
         print(cl.query(line))
 

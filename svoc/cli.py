@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import os
 import tempfile
+import threading
 from typing import Callable, Dict, List, Optional
 
 import torch
@@ -58,12 +59,20 @@ For <admin> <oracle> arguments, you can either specify the index or the address 
 """
 
 N_ORACLES, N_FAILING, DIMENSION = 7, 2, 6        # client/common.py:8-9, 31
+SIMULATION_REFRESH_RATE = 5.0                      # seconds between auto fetches (client/common.py:11)
 
 
 class Client:
     def __init__(self, device: str = "cpu", mode: str = "exact", db_path: Optional[str] = None,
-                 encoder: str = "tiny", dimension: int = DIMENSION, seed: int = 0):
+                 encoder: str = "tiny", dimension: int = DIMENSION, seed: int = 0,
+                 refresh_rate: float = SIMULATION_REFRESH_RATE, emit: Callable[[str], None] = print):
         self.device = device
+        self.refresh_rate = float(refresh_rate)
+        self.emit = emit                      # where the auto-fetch loop writes (the reference's console)
+        self._lock = threading.RLock()        # one command at a time: the prompt and the auto-fetch loop
+        self._auto_stop = threading.Event()
+        self._auto_thread: Optional[threading.Thread] = None
+        self.auto_fetches = 0
         self.admins = [codec.shortstring(x) for x in ("Akashi", "Ozu", "Higuchi")]
         self.oracles = [codec.shortstring(f"oracle_{i:02d}") for i in range(N_ORACLES)]
         self.contract = OracleConsensus(self.admins, True, 2, N_FAILING, True, 0, dimension, self.oracles,
@@ -124,6 +133,41 @@ class Client:
             s += "\n" + self.commit()
         return s
 
+    # ---- auto fetch (simulation_mode, client/oracle_scheduler.py:163-171) -------------------------
+    def _auto_fetch_loop(self) -> None:
+        """Fetch, then sleep refresh_rate seconds, while auto_fetch stays on.  The reference runs this
+        loop inside the UI handler with eel.sleep; here it is a daemon thread next to the prompt."""
+        while not self._auto_stop.is_set():
+            with self._lock:
+                if not self.flags["auto_fetch"]:
+                    break
+                try:
+                    out = self.fetch()
+                except Exception as e:   # a failed fetch is reported, the loop keeps its period
+                    out = f"auto_fetch error: {e!r}"
+                self.auto_fetches += 1
+            self.emit(out)
+            self._auto_stop.wait(self.refresh_rate)
+
+    def set_auto_fetch(self, on: bool) -> str:
+        self.flags["auto_fetch"] = bool(on)
+        if on and (self._auto_thread is None or not self._auto_thread.is_alive()):
+            self._auto_stop.clear()
+            self._auto_thread = threading.Thread(target=self._auto_fetch_loop, name="svoc-auto-fetch", daemon=True)
+            self._auto_thread.start()
+            return "Auto-Fetch: ENABLED"
+        if not on:
+            self._auto_stop.set()
+            t = self._auto_thread
+            if t is not None and t is not threading.current_thread():
+                t.join(timeout=max(1.0, 2 * self.refresh_rate) + 60.0)
+            self._auto_thread = None
+            return "Auto-Fetch: DISABLE"
+        return "Auto-Fetch: ENABLED"
+
+    def close(self) -> None:
+        self.set_auto_fetch(False)
+
     def commit(self) -> str:
         """update_all_the_predictions (client/contract.py:200-208): one update per oracle, in order."""
         if self.predictions is None:
@@ -151,6 +195,13 @@ class Client:
         return "\n".join(s)
 
     def query(self, text: str) -> str:
+        sp = text.split()
+        if sp and sp[0] == "auto_fetch" and len(sp) == 2:   # outside the lock: it may join the loop
+            return self.set_auto_fetch(sp[1] == "on")
+        with self._lock:
+            return self._query(text)
+
+    def _query(self, text: str) -> str:
         sp = text.split()
         if not sp:
             return ""
@@ -180,7 +231,7 @@ class Client:
         try:
             if cmd in simple:
                 return simple[cmd]()
-            if cmd in ("auto_fetch", "auto_commit", "auto_resume", "scraper", "live_mode") and args:
+            if cmd in ("auto_commit", "auto_resume", "scraper", "live_mode") and args:
                 return onoff(cmd)
             if cmd == "update_proposition" and len(args) in (2, 3):
                 caller = self._admin(args[0])

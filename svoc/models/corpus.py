@@ -83,7 +83,7 @@ def synthetic_token_batch(B: int, S: int, vocab: int, gen: torch.Generator, devi
 # ---- SQLite (client/scraper.py:44-72, oracle_scheduler.py:44-69) ------------------------------
 
 def init_db(path: str) -> sqlite3.Connection:
-    conn = sqlite3.connect(path)
+    conn = sqlite3.connect(path, check_same_thread=False)   # callers serialise access (cli.Client lock)
     conn.execute("CREATE TABLE IF NOT EXISTS comments (id INTEGER PRIMARY KEY AUTOINCREMENT, "
                  "comment TEXT NOT NULL, timestamp TEXT NOT NULL)")
     conn.commit()

@@ -94,11 +94,26 @@ def smooth_median(col: Sequence[int]) -> int:
     return idiv(chk(s[mid - 1] + s[mid]), 2)
 
 
-def median(col: Sequence[int]) -> int:
-    """math.cairo:102-110 (sorted[len/2], located by value in the original array)."""
+def find_index(value: int, col: Sequence[int]) -> int:
+    """math.cairo:87-100: the first index holding ``value`` (linear scan; 'value not found' panics)."""
+    for i, v in enumerate(col):
+        if v == value:
+            return i
+    raise ConsensusRevert(Status.INDEX_OOB, "value not found")
+
+
+def median_index(col: Sequence[int]) -> int:
+    """math.cairo:102-106: sort a copy, take ``sorted[len / 2]``, then locate it in the ORIGINAL array
+    by value -- with duplicates this is the first occurrence, not necessarily the element the sort
+    moved there."""
     if not col:
         raise ConsensusRevert(Status.INDEX_OOB, "median on empty")
-    return sorted(col)[len(col) // 2]
+    return find_index(sorted(col)[len(col) // 2], col)
+
+
+def median(col: Sequence[int]) -> int:
+    """math.cairo:108-110: ``values[median_index(values)]`` (= sorted[len/2])."""
+    return col[median_index(col)]
 
 
 def average(col: Sequence[int]) -> int:

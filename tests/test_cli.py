@@ -37,3 +37,23 @@ def test_report_html(tmp_path):
     assert cl.query(f"report {out}").startswith("report written")
     doc = out.read_text()
     assert doc.count("<svg") == 3 and "reliability (second pass)" in doc and "optimism / anger" in doc
+
+
+def test_auto_fetch_is_a_periodic_loop(tmp_path):
+    """auto_fetch on: fetch, sleep refresh_rate, repeat while on (oracle_scheduler.py:163-171);
+    auto_commit chains a commit after each fetch; off stops the loop."""
+    import time
+    outs = []
+    cl = Client(db_path=str(tmp_path / "db.sqlite"), refresh_rate=0.05, emit=outs.append)
+    cl.query("auto_commit on")
+    assert cl.query("auto_fetch on") == "Auto-Fetch: ENABLED"
+    t0 = time.time()
+    while cl.auto_fetches < 3 and time.time() - t0 < 120:
+        time.sleep(0.02)
+    assert cl.query("auto_fetch off") == "Auto-Fetch: DISABLE"
+    n = cl.auto_fetches
+    assert n >= 3 and len(outs) >= 3 and all("fetched" in o for o in outs)
+    assert any("oracle 0x" in o for o in outs)          # auto_commit ran
+    time.sleep(0.2)
+    assert cl.auto_fetches == n                          # stopped
+    assert cl.position > 0                               # the window advanced (step += 50)

@@ -123,3 +123,17 @@ def test_coalescing_property():
         st, r = ref.round_status([last[o] for o in ORACLES], N_FAILING, True)
         assert st == Status.OK
         assert r.consensus == c.get_consensus_value() and r.rel2 == c.rel2
+
+
+def test_median_index_first_occurrence():
+    """math.cairo:87-110: median_index sorts a copy, takes sorted[len/2] and finds its FIRST index in the
+    original array by value (find_index), so duplicates resolve to the earliest position."""
+    from svoc import reference as r
+    assert r.median_index([20, 30, 29, 1, 300, 100]) == 1          # sorted[3] = 30 at index 1
+    assert r.median([20, 30, 29, 1, 300, 100]) == 30
+    assert r.median_index([5, 7, 7, 1, 7]) == 1                     # sorted[2] = 7: first 7 is index 1
+    assert r.median_index([3]) == 0
+    with pytest.raises(Exception):
+        r.median_index([])
+    with pytest.raises(Exception):
+        r.find_index(4, [1, 2, 3])                                  # 'value not found'
