@@ -8,9 +8,11 @@ K = 300 (contract/drafts/beta_kumaraswamy_algorithm_demo copy.ipynb cells 17-21)
   its ``b`` argument, survey §2.8-11), shuffled; median = numpy median (mean of the two middle values
   for even N); failing = the f largest |x - median|; success = exact mask match; distance =
   |median(predicted reliable) - median(true reliable)|; reliability = 100 (1 - 2 mean distance).
-* ``contract`` estimator: the same draws pushed through the consensus engine itself (smooth median,
-  squared risk, (qr asc, idx desc) rank mask -- the fused HIP kernel on GPU), scored the same way
-  with the engine's reliable mask.
+* ``contract`` estimator: the same draws quantised to wsad as the client does (int(x * 1e6),
+  client/contract.py:48-53) and pushed through one EXACT consensus round each (smooth median, wsad
+  squared risk, (qr asc, idx desc) rank mask -- the column-parallel exact kernel on GPU, the C++
+  golden engine on CPU), scored with the ``reliable`` flags that round wrote.  Rounds the contract
+  would revert (none on these draws in practice) are excluded and counted.
 
     python -m svoc.bench.statistical --trials 1000000 [--device cuda] [--json out.json]
 """
@@ -62,25 +64,18 @@ def notebook_estimator(x: torch.Tensor, f: int) -> torch.Tensor:
     return rank_from_top >= f
 
 
-def contract_estimator(x: torch.Tensor, f: int) -> torch.Tensor:
-    """The engine's own rank mask (fast HIP kernel on GPU / C++ engine on CPU)."""
+def contract_estimator(x: torch.Tensor, f: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """The contract's own rank mask: (reliable [B, N], round succeeded [B]) of one exact round per trial."""
     from .. import ops as svops
     B, N = x.shape
-    vals = torch.zeros(B, N, 8, dtype=torch.bfloat16, device=x.device)
-    vals[:, :, 0] = x.to(torch.bfloat16)
-    f32 = dict(dtype=torch.float32, device=x.device)
-    c1, cons, sk, ku = (torch.zeros(B, 1, **f32) for _ in range(4))
-    rel, qr = torch.zeros(B, 2, **f32), torch.zeros(B, N, **f32)
+    vals = (x * 1e6).floor().to(torch.int32).reshape(B, N, 1).contiguous()
+    i64 = dict(dtype=torch.int64, device=x.device)
+    c1, cons, sk, ku = (torch.zeros(B, 1, **i64) for _ in range(4))
+    rel, qr = torch.zeros(B, 2, **i64), torch.zeros(B, N, **i64)
     reliable = torch.zeros(B, N, dtype=torch.uint8, device=x.device)
-    st = torch.zeros(B, dtype=torch.int32, device=x.device)
-    svops.ops().fast_round(vals, None, 1, f, True, 1.0, c1, cons, sk, ku, rel, qr, reliable, st, 0, 1, 1)
-    # mode 1 produced qr; rank mask exactly as the contract: (qr asc, idx desc), first N - f reliable
-    idx = torch.arange(N, device=x.device).expand(B, N)
-    by_idx_desc = torch.argsort(-idx, dim=1, stable=True)
-    order = torch.gather(by_idx_desc, 1, torch.argsort(torch.gather(qr, 1, by_idx_desc), dim=1, stable=True))
-    rank = torch.empty_like(order)
-    rank.scatter_(1, order, torch.arange(N, device=x.device).expand(B, N))
-    return rank < (N - f)
+    st = torch.full((B,), -1, dtype=torch.int32, device=x.device)
+    svops.ops().exact_round(vals, None, f, True, 0, c1, cons, sk, ku, rel, qr, reliable, st, False)
+    return reliable.bool(), st == 0
 
 
 def score(x: torch.Tensor, pred: torch.Tensor, truth: torch.Tensor) -> Tuple[float, float]:
@@ -95,22 +90,32 @@ def run(trials: int, device="cpu", chunk: int = 1 << 18, seed: int = 0, estimato
     gen = torch.Generator(device=device).manual_seed(seed)
     out = []
     for N, f, a in grid:
-        acc = {e: [0.0, 0.0] for e in estimators}
+        acc = {e: [0.0, 0.0, 0] for e in estimators}   # success sum, reliability sum, scored trials
         done = 0
         t0 = time.perf_counter()
         while done < trials:
             B = min(chunk, trials - done)
             x, truth = draw(B, N, f, a, gen, device)
             for e in estimators:
-                pred = notebook_estimator(x, f) if e == "notebook" else contract_estimator(x, f)
-                s, r = score(x, pred, truth)
-                acc[e][0] += s * B
-                acc[e][1] += r * B
+                if e == "notebook":
+                    pred, ok = notebook_estimator(x, f), None
+                else:
+                    pred, ok = contract_estimator(x, f)
+                xs, ps, ts = (x, pred, truth) if ok is None else (x[ok], pred[ok], truth[ok])
+                n = xs.shape[0]
+                if n:
+                    s, r = score(xs, ps, ts)
+                    acc[e][0] += s * n
+                    acc[e][1] += r * n
+                    acc[e][2] += n
             done += B
         row = dict(N=N, f=f, a=a, trials=trials, seconds=time.perf_counter() - t0)
         for e in estimators:
-            row[f"{e}_success"] = acc[e][0] / trials
-            row[f"{e}_reliability"] = acc[e][1] / trials
+            n = max(acc[e][2], 1)
+            row[f"{e}_success"] = acc[e][0] / n
+            row[f"{e}_reliability"] = acc[e][1] / n
+            if e == "contract":
+                row["contract_reverted"] = trials - acc[e][2]
         pub = PUBLISHED.get((N, f), {}).get(a)
         if pub:
             row["published_success"] = pub[0]
