@@ -166,17 +166,9 @@ def main():
         gov.admins.copy_(torch.tensor([address_to_limbs(1000 + a) for a in range(3)], device=dev).expand(B, 3, 4))
         ora = torch.tensor([address_to_limbs(5000 + o) for o in range(c["N"])], device=dev)
         gov.oracle_addr.copy_(ora.expand(B, c["N"], 4))
-        K = max(1, int(B * c["gov_frac"]))
-        gg = torch.Generator(device=dev).manual_seed(7 + rank)
-        gov_batches = []
-        for i in range(2):      # alternate: proposals by admin 0, then a supporting vote by admin 1
-            inst = torch.randperm(B, generator=gg, device=dev)[:K]
-            caller = torch.tensor(address_to_limbs(1000 + i), device=dev).expand(K, 4).contiguous()
-            kind = torch.full((K,), i, dtype=torch.int32, device=dev)
-            a0 = torch.full((K,), 1 if i == 0 else 0, dtype=torch.int32, device=dev)
-            a1 = torch.randint(0, c["N"], (K,), generator=gg, device=dev) if i == 0 else torch.ones(K, dtype=torch.int64, device=dev)
-            addr = torch.randint(10**6, 10**9, (K, 4), generator=gg, device=dev)
-            gov_batches.append((inst, caller, kind, a0, a1, addr))
+        from svoc.stream import governance_stream
+        gov_batches = governance_stream(B, c["N"], [1000, 1001, 1002], dev, seed=rank, frac=c["gov_frac"])
+        K = gov_batches[0][0].numel()
         extra["governance_actions_per_step"] = K
         extra["state_bytes_per_instance"] = eng.bytes_per_instance(c["N"], c["D"], "fast") + 3 * 4 * 8 + 3 * 8 + 3 * (1 + 4 + 32) + c["N"] * 32
         extra["instances_per_288GB"] = int(288e9 // extra["state_bytes_per_instance"])
@@ -206,7 +198,7 @@ def main():
             eng.touched.fill_(1)
             run_round()
         if gov is not None:
-            gov.submit_tensors(*gov_batches[i % 2])
+            gov.submit_tensors(*gov_batches[i % len(gov_batches)])
         dp.accumulate()
 
     for i in range(args.warmup):
@@ -217,7 +209,11 @@ def main():
     graph = None
     if args.graph and dev.type == "cuda" and not dshard:   # (no collectives inside a captured graph)
         # the stream cycles with period `pool`: capture one period and replay it
-        period = stream.pool if stream is not None else (2 if (pipe is not None or gov is not None) else 1)
+        import math
+        period = 1
+        for k in (stream.pool if stream is not None else 1, len(gov_batches) if gov is not None else 1,
+                  2 if pipe is not None else 1):
+            period = period * k // math.gcd(period, k)
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):

@@ -49,8 +49,10 @@ class Governance:
     def set_addresses(self, admins: Sequence[Sequence[int]], oracles: Sequence[Sequence[int]]) -> None:
         """admins[b] / oracles[b]: address ints per instance (or one list broadcast to all)."""
         def pack(lst, n):
-            rows = lst if (lst and isinstance(lst[0], (list, tuple))) else [lst] * self.B
-            t = torch.tensor([[address_to_limbs(int(a)) for a in r] for r in rows], dtype=torch.int64)
+            if lst and isinstance(lst[0], (list, tuple)):
+                t = torch.tensor([[address_to_limbs(int(a)) for a in r] for r in lst], dtype=torch.int64)
+            else:   # one list for every instance: [n, 4] broadcast (no B-long host list)
+                t = torch.tensor([address_to_limbs(int(a)) for a in lst], dtype=torch.int64)[None].expand(self.B, -1, -1)
             assert t.shape[1] == n
             return t.to(self.device)
         if self.A:

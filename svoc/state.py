@@ -57,7 +57,6 @@ def save(svc, path: str) -> None:
 def load(path: str, device="cpu"):
     """Rebuild a :class:`svoc.api.ConsensusService` from a checkpoint."""
     from .api import ConsensusService
-    from .codec import limbs_to_address
     meta_s, names, tensors = svops.ops().load_state(path)
     meta = json.loads(meta_s)
     if meta.get("format") != FORMAT:
@@ -65,11 +64,16 @@ def load(path: str, device="cpu"):
     t: Dict[str, torch.Tensor] = dict(zip(names, tensors))
     cfg = ConsensusConfig.from_dict(meta["config"])
     B = int(meta["batch"])
-    admins = [[limbs_to_address(x) for x in r] for r in t["admins"].tolist()]
-    oracles = [[limbs_to_address(x) for x in r] for r in t["oracle_address"].tolist()]
-    svc = ConsensusService(cfg, B, admins, oracles, device=device, mode=meta["mode"], storage=meta.get("storage"))
+    # placeholder addresses, then the checkpoint's limb tensors copied in directly (no per-instance
+    # host conversion: a 1M-instance checkpoint restores in seconds)
+    svc = ConsensusService(cfg, B, [0] * cfg.n_admins, [0] * cfg.n_oracles, device=device, mode=meta["mode"],
+                           storage=meta.get("storage"))
     e, g = svc.engine, svc.gov
     dev = e.device
+    if cfg.n_admins:
+        g.admins.copy_(t["admins"].to(dev))
+    g.oracle_addr.copy_(t["oracle_address"].to(dev))
+    g._oracle_cache = None
     e.values[:, :, : e.D].copy_(t["oracles_values"].to(dev, e.vdtype))
     e.enabled.copy_(t["enabled"].to(dev))
     e.reliable.copy_(t["reliable"].to(dev))

@@ -65,3 +65,29 @@ class UpdateQueue:
         st = engine.step(torch.tensor(self.inst), torch.tensor(self.orc), torch.stack(self.vals))
         self.inst, self.orc, self.vals = [], [], []
         return st
+
+
+def governance_stream(B: int, n_oracles: int, admin_addresses, device, seed: int = 0, frac: float = 0.01,
+                      pairs: int = 4):
+    """Synthetic admin-replacement traffic (contract.cairo:661-738 -> :547-580), ``2 * pairs``
+    batches for ``Governance.submit_tensors``: batch 2k = a proposition by admin 0 on ``frac`` of the
+    instances (replace a random oracle by a fresh address), batch 2k+1 = admin 1's supporting vote on
+    the SAME instances -- with majority 2 every pair completes a replacement.  Cycle them in order."""
+    from .codec import address_to_limbs
+    dev = torch.device(device)
+    K = max(1, int(B * frac))
+    g = torch.Generator(device=dev).manual_seed(7919 + seed)
+    a0 = torch.tensor(address_to_limbs(int(admin_addresses[0])), device=dev).expand(K, 4).contiguous()
+    a1 = torch.tensor(address_to_limbs(int(admin_addresses[1])), device=dev).expand(K, 4).contiguous()
+    out = []
+    for _ in range(pairs):
+        inst = torch.randperm(B, generator=g, device=dev)[:K].contiguous()
+        which = torch.randint(0, n_oracles, (K,), generator=g, device=dev)
+        addr = torch.randint(10 ** 6, 10 ** 15, (K, 4), generator=g, device=dev)
+        out.append((inst, a0, torch.zeros(K, dtype=torch.int32, device=dev),
+                    torch.ones(K, dtype=torch.int32, device=dev), which, addr))          # propose(Some(idx, addr))
+        out.append((inst, a1, torch.ones(K, dtype=torch.int32, device=dev),
+                    torch.zeros(K, dtype=torch.int32, device=dev), torch.ones(K, dtype=torch.int64, device=dev),
+                    addr))                                                              # vote(admin 0, yes)
+    return out
+
