@@ -114,7 +114,7 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
   fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
   TORCH_CHECK(values.scalar_type() == at::kBFloat16, "GPU fast path stores values in bf16");
   const int64_t B = values.size(0), N = values.size(1), ld = values.size(2);
-  TORCH_CHECK(N >= 2 && N <= 256, "GPU fast path supports 2 <= N <= 256 oracles");
+  TORCH_CHECK(N >= 2 && N <= 1024, "GPU fast path supports 2 <= N <= 1024 oracles");
   TORCH_CHECK(ld % 8 == 0, "row stride (ld) must be a multiple of 8 bf16 (16 B)");
   TORCH_CHECK(((uintptr_t)values.data_ptr() & 15) == 0 && values.stride(0) % 8 == 0, "values must be 16-B aligned");
   TORCH_CHECK(B < (1ll << 31) && D < (1 << 30), "size limits");
@@ -227,7 +227,7 @@ void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& 
   p.values = values.data_ptr();
   p.val32 = values.scalar_type() == at::kInt ? 1 : 0;
   p.B = (int)values.size(0); p.N = (int)values.size(1); p.D = (int)values.size(2);
-  TORCH_CHECK(p.N >= 1 && p.N <= 256, "GPU exact path supports N <= 256");
+  TORCH_CHECK(p.N >= 1 && p.N <= 1024, "GPU exact path supports N <= 1024");
   p.active = active_ptr(active, p.B, values.device());
   p.n_failing = (int)n_failing;
   p.constrained = constrained ? 1 : 0;

@@ -335,7 +335,10 @@ static int exact_round_i128(const ExactParams* p, hipStream_t stream) {
     if (p->N <= 16 && 4 * per_inst <= 64 * 1024) return launch_exact<1, 16>(*p, stream);
     if (p->N <= 32 && 2 * per_inst <= 64 * 1024) return launch_exact<1, 32>(*p, stream);
   }
-  return p->N <= 64 ? launch_exact<1, 64>(*p, stream) : launch_exact<4, 64>(*p, stream);
+  if (p->N <= 64) return launch_exact<1, 64>(*p, stream);
+  if (p->N <= 256) return launch_exact<4, 64>(*p, stream);
+  if (p->N <= 512) return launch_exact<8, 64>(*p, stream);
+  return launch_exact<16, 64>(*p, stream);
 }
 
 // Exact round: the column-parallel kernel (consensus_wsad.hip) takes every instance it can prove
@@ -344,7 +347,7 @@ static int exact_round_i128(const ExactParams* p, hipStream_t stream) {
 // through the i128 kernel right after it on the same stream.
 extern "C" int svoc_exact_round(const ExactParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
-  if (p->N < 1 || p->N > 256 || p->D < 1) return -1;
+  if (p->N < 1 || p->N > 1024 || p->D < 1) return -1;
   if (p->stage && p->fallback) {
     const int rc = svoc_exact_round_wsad(p, stream);
     if (rc != -2) {

@@ -29,8 +29,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW 
   constexpr int KEEP = 64 / P;
   __shared__ float qr_part[WAVES * NPAD];
   __shared__ float qr_lds[NPAD];
-  __shared__ uint64_t relmask[4];
-  __shared__ uint64_t lowmask[4];  // non-reliable rows turned into -inf sentinels (pass 2)
+  constexpr int MW = NSEG < 4 ? 4 : NSEG;   // 64-row mask words
+  __shared__ uint64_t relmask[MW];
+  __shared__ uint64_t lowmask[MW];  // non-reliable rows turned into -inf sentinels (pass 2)
   __shared__ float misc_f[2];
   __shared__ int misc_i[2];
 
@@ -104,7 +105,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW 
         for (int i = 0; i < 64; ++i) r[i] = as_k(as_u32(r[i]) ^ pol);
       }
       u16x2 klo, khi;
-      median_group<NSEG>(r, klo, khi);
+      if constexpr (NSEG >= 8) median_group_wide<NSEG, P>(r, seg, lane, klo, khi);
+      else median_group<NSEG>(r, klo, khi);
       const uint32_t lo = from_key<CONS>(klo), hi = from_key<CONS>(khi);
       cA = 0.5f * (bf16_lo(lo) + bf16_lo(hi));
       cB = 0.5f * (bf16_hi(lo) + bf16_hi(hi));
@@ -197,7 +199,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW 
       rel = rank < R;
     }
     const uint64_t bal = __ballot(rel);
-    if (lane == 0 && (t >> 6) < 4) relmask[t >> 6] = bal;
+    if (lane == 0 && (t >> 6) < MW) relmask[t >> 6] = bal;
   }
   __syncthreads();
   if (tid < 64) {
@@ -215,7 +217,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW 
     if (tid == 0) {
       // pass-2 sentinel split: the first (NPAD - R) / 2 non-reliable rows become -inf
       int need = (NPAD - (N - p.n_failing) + 1) >> 1;
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < MW; ++w) {
         uint64_t nr = w < NSEG ? ~relmask[w] : 0ull, lm = 0ull;
         while (need > 0 && nr) {
           const uint64_t bit = nr & (0ull - nr);
@@ -257,7 +259,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW 
   const uint64_t mymask = relmask[seg];
   const uint64_t mylow = lowmask[seg];
   int first_rel = 0;
-  for (int w = 0; w < 4; ++w)
+  for (int w = 0; w < MW; ++w)
     if (relmask[w]) { first_rel = 64 * w + __builtin_ctzll(relmask[w]); break; }
 
   // ------------------------------------------------------------ pass 2 (contract.cairo:476-500)
@@ -305,7 +307,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW 
 #pragma unroll
       for (int i = 0; i < 64; ++i) r[i] = as_k(wv[i]);
       u16x2 klo, khi;
-      median_group<NSEG>(r, klo, khi);
+      if constexpr (NSEG >= 8) median_group_wide<NSEG, P>(r, seg, lane, klo, khi);
+      else median_group<NSEG>(r, klo, khi);
       const uint32_t lo = key_to_pos(klo), hi = key_to_pos(khi);
       cA = 0.5f * (bf16_lo(lo) + bf16_lo(hi));
       cB = 0.5f * (bf16_hi(lo) + bf16_hi(hi));
@@ -395,7 +398,7 @@ using namespace svoc;
 
 extern "C" int svoc_fast_round_bf16_reg(const FastParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
-  if (p->N < 2 || p->N > 256 || p->ld % 8 != 0 || p->D > p->ld) return -1;
+  if (p->N < 2 || p->N > 1024 || p->ld % 8 != 0 || p->D > p->ld) return -1;
   if (p->mode != 1 && (!p->work || p->work_pairs < fast_work_pairs(p->D) || p->work_stride < fast_work_words(p->D)))
     return -1;   // pass 2 stages its outputs in the workspace
   // wave_hint -3 / -4: 8 / 2 waves per workgroup (fused); default 4 (16 waves per CU at <= 128 VGPRs)
@@ -405,5 +408,7 @@ extern "C" int svoc_fast_round_bf16_reg(const FastParams* p, hipStream_t stream)
     return launch_reg<1, 4>(*p, stream);
   }
   if (p->N <= 128) return launch_reg<2, 4>(*p, stream);
-  return launch_reg<4, 4>(*p, stream);
+  if (p->N <= 256) return launch_reg<4, 4>(*p, stream);
+  if (p->N <= 512) return launch_reg<8, 4>(*p, stream);
+  return launch_reg<16, 4>(*p, stream);
 }
