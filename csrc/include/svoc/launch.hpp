@@ -105,3 +105,6 @@ struct UpdateParams {
 }  // namespace svoc
 
 extern "C" int svoc_apply_updates(const svoc::UpdateParams* p, hipStream_t stream);
+
+extern "C" int svoc_qr_probe(const uint16_t* X, const float* C, float* qr, int B, int N, int D, int ld, int variant,
+                             hipStream_t stream);

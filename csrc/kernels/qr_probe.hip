@@ -1,0 +1,136 @@
+// Quadratic-risk probe: the per-oracle quadratic risk qr_i = sum_d (x_id - c_d)^2 (math.cairo:225-238,
+// contract.cairo:463) of every instance, computed two ways over the same loads, to measure whether
+// the matrix cores pay on the consensus hot path.
+//
+//   variant 0 (VALU): sum_d (x - c)^2 in fp32 -- what the fused round kernels do;
+//   variant 1 (MFMA): the expanded form ||x||^2 - 2 x.c + ||c||^2 with x.c on the matrix cores
+//                     (mfma_f32_32x32x16_bf16: A = 32 oracle rows x 16 dims of the instance, B = the
+//                     centre as two bf16 columns c_hi + c_lo, exact to 16 bits), ||x||^2 on VALU.
+//
+// A per-instance GEMV has one useful B column (two with the hi / lo split): 30 of the 32 MFMA output
+// columns are idle, and the expanded form cancels (||x||^2 ~ 0.25 D against qr ~ 0.005 D for Beta
+// data), so the probe reports both the time and the rank-mask agreement.  Layout shared by both: one
+// workgroup per instance, a wave walks 32-row blocks, lane (r, hh) loads 8 dims (16 B) of row r.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace svoc {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef unsigned short u16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ float bf16_to_f(uint16_t h) { return __builtin_bit_cast(float, (uint32_t)h << 16); }
+__device__ __forceinline__ uint16_t f_to_bf16_rn(float f) {   // round to nearest even
+  const uint32_t u = __builtin_bit_cast(uint32_t, f);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+template <int VARIANT>
+__global__ __launch_bounds__(256) void qr_probe_kernel(const uint16_t* __restrict__ X, const float* __restrict__ C,
+                                                       float* __restrict__ qr, int N, int D, int ld) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* cf = (float*)smem;                            // [D] fp32 centre (VALU)
+  uint16_t* chi = (uint16_t*)smem;                     // [D] bf16 hi (MFMA)
+  uint16_t* clo = chi + ((D + 15) / 16) * 16;          // [D] bf16 lo
+  __shared__ float cnorm_part[4];
+  const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const float* c = C + (int64_t)b * D;
+  const int Dp = ((D + 15) / 16) * 16;
+  float cn = 0.f;
+  for (int d = tid; d < Dp; d += 256) {
+    const float v = d < D ? c[d] : 0.f;
+    cn = fmaf(v, v, cn);
+    if (VARIANT == 0) {
+      cf[d] = v;
+    } else {
+      const uint16_t h = f_to_bf16_rn(v);
+      chi[d] = h;
+      clo[d] = f_to_bf16_rn(v - bf16_to_f(h));
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) cn += __shfl_xor(cn, o);
+  if (lane == 0) cnorm_part[wave] = cn;
+  __syncthreads();
+  const float cnorm = cnorm_part[0] + cnorm_part[1] + cnorm_part[2] + cnorm_part[3];
+  const uint16_t* Xb = X + (int64_t)b * N * ld;
+
+  for (int r0 = wave * 32; r0 < N; r0 += 4 * 32) {
+    const int row = r0 + r < N ? r0 + r : N - 1;
+    const uint16_t* xr = Xb + (int64_t)row * ld;
+    float acc = 0.f;                                   // VALU: sum (x - c)^2; MFMA: ||x||^2
+    f32x16_t xc = {};                                  // MFMA: x . [c_hi, c_lo, 0, ...]
+    for (int d0 = 0; d0 < Dp; d0 += 16) {
+      const int d = d0 + 8 * hh;
+      u16x8_t w = *(const u16x8_t*)(xr + d);           // 8 dims of this lane's row (16-B load)
+      if (d0 + 16 > D) {                               // tail: dims past D contribute 0
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = d + j < D ? w[j] : (uint16_t)0;
+      }
+      if (VARIANT == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float y = bf16_to_f(w[j]) - cf[d + j];
+          acc = fmaf(y, y, acc);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = bf16_to_f(w[j]);
+          acc = fmaf(x, x, acc);
+        }
+        // B column n = r: c_hi for n = 0, c_lo for n = 1, 0 elsewhere (k = d .. d + 7)
+        u16x8_t cb = {};
+        if (r == 0) cb = *(const u16x8_t*)(chi + d);
+        if (r == 1) cb = *(const u16x8_t*)(clo + d);
+        xc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, w), __builtin_bit_cast(bf16x8_t, cb),
+                                                     xc, 0, 0, 0);
+      }
+    }
+    acc += __shfl_xor(acc, 32);                        // the row's other 8-dim half
+    if (VARIANT == 0) {
+      if (hh == 0 && r0 + r < N) qr[(int64_t)b * N + r0 + r] = acc;
+    } else {
+      // D[row][n] sits in lane n (+32 for rows 4..7 of each group of 8): lanes 0 / 32 hold x.c_hi,
+      // lanes 1 / 33 x.c_lo, for rows (i & 3) + 8 (i >> 2) + 4 hh.  Gather x.c of row r into lane r.
+      __shared__ float dot[4][32];
+      if (r < 2) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int rr = (i & 3) + 8 * (i >> 2) + 4 * hh;
+          if (r == 0) dot[wave][rr] = xc[i];
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+      if (r == 1) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int rr = (i & 3) + 8 * (i >> 2) + 4 * hh;
+          dot[wave][rr] += xc[i];
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+      if (hh == 0 && r0 + r < N) qr[(int64_t)b * N + r0 + r] = acc - 2.f * dot[wave][r] + cnorm;
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+}  // namespace svoc
+
+using namespace svoc;
+
+extern "C" int svoc_qr_probe(const uint16_t* X, const float* C, float* qr, int B, int N, int D, int ld, int variant,
+                             hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (ld % 8 != 0 || ld < ((D + 15) / 16) * 16) return -1;   // 16-B loads over whole 16-dim chunks
+  const int Dp = ((D + 15) / 16) * 16;
+  const size_t lds = variant == 0 ? (size_t)Dp * 4 : (size_t)Dp * 4;
+  if (lds > 64 * 1024) return -2;
+  if (variant == 0) hipLaunchKernelGGL(qr_probe_kernel<0>, dim3(B), dim3(256), lds, stream, X, C, qr, N, D, ld);
+  else hipLaunchKernelGGL(qr_probe_kernel<1>, dim3(B), dim3(256), lds, stream, X, C, qr, N, D, ld);
+  return (int)hipGetLastError();
+}
