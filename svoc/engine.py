@@ -62,7 +62,10 @@ class ConsensusEngine:
             self.ld = _round_up(D, 8)              # 16-B rows for global_load_lds
             odt = torch.float32
         else:
-            self.vdtype = {"int64": torch.int64, "int32": torch.int32}[storage or "int64"]
+            # constrained values are validated to [0, 1e6] on every update (contract.cairo:591-593), so
+            # int32 storage is lossless there (half the bytes of int64); unconstrained wsad stays int64
+            default = "int32" if cfg.constrained else "int64"
+            self.vdtype = {"int64": torch.int64, "int32": torch.int32}[storage or default]
             if self.vdtype == torch.int32 and not cfg.constrained:
                 raise ValueError("int32 wsad storage is for constrained configs (values in [0, 1e6])")
             self.ld = D
