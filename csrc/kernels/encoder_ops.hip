@@ -113,14 +113,18 @@ extern "C" int svoc_add_layernorm_bf16(const void* x, const void* y, const void*
 // contiguous global loads) leaves each lane with one query's scores for 64 keys (its partner
 // lane ^ 32 holds the other 64), so the softmax is lane-local plus one xor-32 exchange, and the
 // accumulator registers ARE the A operand of Z = P·V (pairs of registers -> bf16, k order
-// 16s + 8(j>>2) + 4h + (j&3)).  V is staged transposed in LDS (row pitch S/2+2 dwords: conflict-free
-// 8-byte reads by 32 lanes) so each B fragment is two ds_read_b64.  P is normalised before the PV
-// product (bf16 P, as flash attention).  At S = 128 the whole problem is 32 MFMAs per wave.
+// 16s + 8(j>>2) + 4h + (j&3)).  V is staged ROW-major in LDS (one 16-B store per 16-B global load;
+// 128-B rows, 16-B chunk c of row k at chunk c ^ 4((k >> 1) & 1)) and each B fragment is two gfx950
+// transposed reads (ds_read_b64_tr_b16: a 16-lane group reads 4 keys x 16 dims and every lane gets
+// its dim's 4 keys), conflict-free under that swizzle.  (The previous image was transposed on the
+// write side: 16 two-byte LDS stores per 16-B chunk, with bank conflicts.)  P is normalised before
+// the PV product (bf16 P, as flash attention).  At S = 128 the whole problem is 32 MFMAs per wave.
 // ---------------------------------------------------------------------------------------------
 namespace svoc {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short v4i16 __attribute__((ext_vector_type(4)));
 
 template <int NQB>  // S_max / 32: query blocks = waves = key blocks
 __global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __restrict__ qkv,
@@ -128,8 +132,9 @@ __global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __
                                                              const int* __restrict__ cu_seqlens,
                                                              int64_t rows_total, uint16_t* __restrict__ out,
                                                              int H, float scale_log2) {
-  constexpr int S = 32 * NQB, DH = 64, PITCH = S + 4;  // bf16 elements per Vt row
-  __shared__ uint16_t Vt[DH * PITCH];
+  constexpr int S = 32 * NQB, DH = 64;
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[S * DH];   // row-major V, swizzled 16-B chunks
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[S * DH];   // row-major K, same image
   __shared__ uint8_t km[S];
   const int bh = blockIdx.x, b = bh / H, h = bh % H;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
@@ -148,16 +153,14 @@ __global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __
   const uint16_t* Kb = Qb + H * DH;
   const uint16_t* Vb = Qb + 2 * H * DH;
 
-  // stage Vᵀ and the key mask
+  // stage K and V once per workgroup (row-major, swizzled; every query wave reads them from LDS)
   for (int c = tid; c < nkb * 32 * (DH / 8); c += 64 * NQB) {
-    const int key = c >> 3, e0 = (c & 7) * 8;
-    const uint4 v = *(const uint4*)(Vb + row(key) * ts + e0);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      Vt[(e0 + 2 * i) * PITCH + key] = (uint16_t)(w[i] & 0xffffu);
-      Vt[(e0 + 2 * i + 1) * PITCH + key] = (uint16_t)(w[i] >> 16);
-    }
+    const int key = c >> 3, ch = c & 7;
+    const int off = 128 * key + 16 * (ch ^ (((key >> 1) & 1) << 2));
+    const int64_t g = row(key) * ts + ch * 8;
+    const uint4 kv = *(const uint4*)(Kb + g), vv = *(const uint4*)(Vb + g);
+    *(uint4*)((unsigned char*)Ks + off) = kv;
+    *(uint4*)((unsigned char*)Vs + off) = vv;
   }
   for (int k = tid; k < S; k += 64 * NQB)
     km[k] = cu_seqlens ? (uint8_t)(k < L) : (kmask ? kmask[(int64_t)b * S + k] : (uint8_t)1);
@@ -165,26 +168,28 @@ __global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __
   // X = K·Qᵀ for this wave's 32 queries: rows = keys (registers), column = query (lane)
   const int q0 = wave * 32;
   const bool active = q0 < L;
+  bf16x8 qf[4];
+  if (active) {
+#pragma unroll
+    for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(Qb + row(q0 + r) * ts + ds * 16 + 8 * hh);
+  }
+  __syncthreads();  // K, V and km staged
+  if (!active) return;
   f32x16 x[NQB];
 #pragma unroll
   for (int kb = 0; kb < NQB; ++kb) x[kb] = f32x16{};
-  if (active) {
-    bf16x8 qf[4];
 #pragma unroll
-    for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(Qb + row(q0 + r) * ts + ds * 16 + 8 * hh);
+  for (int kb = 0; kb < NQB; ++kb) {
+    if (kb < nkb) {
+      const int key = kb * 32 + r;
 #pragma unroll
-    for (int kb = 0; kb < NQB; ++kb) {
-      if (kb < nkb) {
-#pragma unroll
-        for (int ds = 0; ds < 4; ++ds) {
-          const bf16x8 kf = *(const bf16x8*)(Kb + row(kb * 32 + r) * ts + ds * 16 + 8 * hh);
-          x[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], x[kb], 0, 0, 0);
-        }
+      for (int ds = 0; ds < 4; ++ds) {
+        const int ch = 2 * ds + hh;
+        const bf16x8 kf = *(const bf16x8*)((unsigned char*)Ks + 128 * key + 16 * (ch ^ (((key >> 1) & 1) << 2)));
+        x[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ds], x[kb], 0, 0, 0);
       }
     }
   }
-  __syncthreads();  // Vt and km staged
-  if (!active) return;
 
   // softmax over the keys of query q0 + r (this lane: key rows (i&3) + 8(i>>2) + 4hh of each block)
   float m = -__builtin_inff();
@@ -215,8 +220,11 @@ __global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __
   sum += __shfl_xor(sum, 32);
   const float inv = 1.f / sum;
 
-  // Z = P·V: A = P (accumulator registers, rows = keys), B = V from Vᵀ in LDS
+  // Z = P·V: A = P (accumulator registers, rows = keys), B = V by transposed LDS reads: lane
+  // (group g = lane >> 4, i = lane & 15) addresses key key0 + 8t + (i >> 2), dims 4 (i & 3) .. +3 of
+  // its group's 16-dim block; it receives its own dim's 4 keys
   f32x16 z[2] = {f32x16{}, f32x16{}};
+  const int tq = (lane & 15) >> 2, tp = lane & 3, tg = (lane >> 4) & 1;
 #pragma unroll
   for (int kb = 0; kb < NQB; ++kb) {
     if (kb >= nkb) continue;
@@ -228,14 +236,15 @@ __global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __
       const int key0 = kb * 32 + 16 * s + 4 * hh;
 #pragma unroll
       for (int eb = 0; eb < 2; ++eb) {
-        const uint16_t* vr = Vt + (eb * 32 + r) * PITCH + key0;
-        const uint2 lo = *(const uint2*)vr, hi = *(const uint2*)(vr + 8);
         bf16x8 vf;
-        const uint32_t w[4] = {lo.x, lo.y, hi.x, hi.y};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          vf[2 * j] = __builtin_bit_cast(__bf16, (uint16_t)(w[j] & 0xffffu));
-          vf[2 * j + 1] = __builtin_bit_cast(__bf16, (uint16_t)(w[j] >> 16));
+        for (int t = 0; t < 2; ++t) {
+          const int key = key0 + 8 * t + tq, ch = eb * 4 + 2 * tg + (tp >> 1);
+          const int off = 128 * key + 16 * (ch ^ (((key >> 1) & 1) << 2)) + 8 * (tp & 1);
+          const v4i16 w = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4i16*)((unsigned char*)Vs + off));
+#pragma unroll
+          for (int j = 0; j < 4; ++j) vf[4 * t + j] = __builtin_bit_cast(__bf16, (short)w[j]);
         }
         z[eb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, vf, z[eb], 0, 0, 0);
       }
