@@ -256,6 +256,8 @@ void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& 
     p.fallback = fallback.data_ptr<uint8_t>();
     const char* only = std::getenv("SVOC_EXACT_WSAD_ONLY");
     p.skip_fallback = only && only[0] == '1';
+    const char* md = std::getenv("SVOC_EXACT_WSAD_MIN_D");   // tests: route small instances through it too
+    p.wsad_min_d = md ? std::atoi(md) : 64;
   }
   auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
   const int rc = svoc_exact_round(&p, stream);

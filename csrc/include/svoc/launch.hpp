@@ -70,6 +70,7 @@ struct ExactParams {
   int32_t* stage;
   uint8_t* fallback;
   int skip_fallback;        // tests: leave the flagged instances alone (shows which rounds it took)
+  int wsad_min_d;           // fewest columns the column-parallel kernel takes (default 64: one lane per column)
 };
 
 }  // namespace svoc

@@ -27,7 +27,7 @@ def _wsad(B, N, D, f, seed, a=20.0):
 def _run(values, f, env=None, active=None):
     B, N, D = values.shape
     o = alloc_exact_out(B, N, D, values.device)
-    old = {k: os.environ.get(k) for k in ("SVOC_EXACT_I128", "SVOC_EXACT_WSAD_ONLY")}
+    old = {k: os.environ.get(k) for k in ("SVOC_EXACT_I128", "SVOC_EXACT_WSAD_ONLY", "SVOC_EXACT_WSAD_MIN_D")}
     try:
         for k in old:
             os.environ.pop(k, None)
@@ -54,13 +54,13 @@ def test_wsad_kernel_bit_exact(N, D, f, dtype):
     B = 16
     v = _wsad(B, N, D, f, seed=N * 1000 + D)
     vg = v.to(DEV, dtype)
-    fast = _run(vg, f, {"SVOC_EXACT_WSAD_ONLY": "1"})   # the column-parallel kernel alone
+    fast = _run(vg, f, {"SVOC_EXACT_WSAD_ONLY": "1", "SVOC_EXACT_WSAD_MIN_D": "1"})   # the column-parallel kernel alone
     ref = _run(v.to(DEV), f, {"SVOC_EXACT_I128": "1"})   # the i128 kernel alone
     took = fast["status"] == 0
     assert took.sum() >= B - 1, fast["status"]         # it takes (almost) every round of Beta data
     for k in OUTS:
         assert torch.equal(fast[k][took], ref[k][took]), k
-    comb = _run(vg, f)                                   # dispatcher: column-parallel + i128 fallback
+    comb = _run(vg, f, {"SVOC_EXACT_WSAD_MIN_D": "1"})   # dispatcher: column-parallel + i128 fallback
     for k in OUTS:
         assert torch.equal(comb[k], ref[k]), k
 
@@ -80,7 +80,7 @@ def test_wsad_kernel_matches_cpu_engine():
 def test_wsad_kernel_goldens(name):
     values, constrained, ms, gold = GOLDEN[name]
     v = torch.tensor([values] * 3, dtype=torch.int64, device=DEV)
-    o = _run(v, N_FAILING, {"SVOC_EXACT_WSAD_ONLY": "1"})
+    o = _run(v, N_FAILING, {"SVOC_EXACT_WSAD_ONLY": "1", "SVOC_EXACT_WSAD_MIN_D": "1"})
     assert o["status"].tolist() == [0, 0, 0]
     assert o["consensus"][2].tolist() == gold["consensus"]
     assert o["rel"][1].tolist() == [gold["rel1"], gold["rel2"]]

@@ -1,0 +1,35 @@
+#!/bin/bash
+# Every headline bench record on one MI355X -> profiles/results.jsonl (one source of truth for the
+# README / BASELINE tables: python tools/results_table.py), plus the c2 / c3 rocprofv3 kernel tables.
+set -u
+R=$(pwd)
+mkdir -p gpurun_out
+OUT=gpurun_out/results.jsonl
+: > $OUT
+run() {  # key, timeout, bench args...
+  local key=$1 t=$2; shift 2
+  echo "=== $key ($(date +%T))"
+  timeout -k 10 $t python bench.py "$@" > gpurun_out/res_$key.log 2>&1 || { tail -5 gpurun_out/res_$key.log; return 1; }
+  python - "$key" <<'PY' >> $OUT
+import json, sys
+line = [l for l in open(f"gpurun_out/res_{sys.argv[1]}.log").read().splitlines() if l.startswith("{")][-1]
+d = json.loads(line); d["key"] = sys.argv[1]; print(json.dumps(d))
+PY
+  tail -1 $OUT | cut -c1-160
+}
+run c3 300 --config c3 --steps 20 --warmup 3 &&
+run c2 300 --config c2 --steps 20 --warmup 3 &&
+run c5 300 --config c5 --steps 50 --warmup 3 &&
+run c4 300 --config c4 --steps 10 --warmup 2 &&
+run c2_exact 300 --config c2 --mode exact --steps 10 --warmup 2 &&
+run c2_exact_int64 300 --config c2 --mode exact --storage int64 --steps 10 --warmup 2 &&
+run c5_exact 300 --config-file configs/c5_exact_rounds.yaml --steps 20 --warmup 2 &&
+run wide512 300 --config-file configs/wide512.yaml --steps 10 --warmup 2 &&
+run c1 300 --config c1 --steps 50 --warmup 3 || exit 1
+for cfg in c3 c2; do
+  echo "=== rocprof $cfg ($(date +%T))"
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+      -d $R/gpurun_out/prof_$cfg -o run -- python3 $R/bench.py --config $cfg --steps 6 --warmup 1 --graph 0 \
+      > $R/gpurun_out/prof_$cfg.log 2>&1) || exit 1
+done
+echo "=== done"

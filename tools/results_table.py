@@ -1,0 +1,124 @@
+"""One source of truth for the headline numbers: `profiles/results.jsonl` (one `bench.py` record per
+line, written by tools/gpu_results.sh on one MI355X, tagged with "key") is rendered into the
+results tables of README.md and BASELINE.md between `<!-- results:<name>:begin -->` /
+`<!-- results:<name>:end -->` markers.  `--check` exits non-zero if a document disagrees with the
+records (tests/test_docs.py runs it).
+
+    python tools/results_table.py [--check]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RESULTS = os.path.join(ROOT, "profiles", "results.jsonl")
+
+# key -> (label, reference comparator from BASELINE.md §2)
+ROWS = [
+    ("c1", "c1: 4 oracles × 2 dims, one exact round, CPU (plumbing)", "2,518/s Python emulator (7×2)"),
+    ("c2", "c2: 64 × 1024, 10k batched instances, bf16", "≈93/s numpy fp64"),
+    ("c3", "c3: 256 × 4096 streaming, failing-oracle masking (headline)", "≈6/s numpy fp64"),
+    ("c4", "c4: BERT-base sentiment oracles → consensus", "—"),
+    ("c5", "c5: governance + reliability stream, 1M instances (7 × 6)", "≈127,900/s numpy fp64 (7×6)"),
+    ("c2_exact", "c2 shape, exact wsad (bit-identical to the contract), int32 storage", "0.61/s exact Python emulator"),
+    ("c2_exact_int64", "c2 shape, exact wsad, int64 storage", "0.61/s exact Python emulator"),
+    ("c5_exact", "c5 shape (7 × 6), exact wsad, 1M instances", "939/s exact Python emulator"),
+    ("wide512", "512 oracles × 2048 dims, 1024 instances (N > 256)", "—"),
+]
+
+
+def load(path=RESULTS):
+    recs = {}
+    if not os.path.exists(path):
+        return recs
+    with open(path, encoding="utf-8") as f:
+        for line in f:
+            line = line.strip()
+            if line:
+                r = json.loads(line)
+                recs[r["key"]] = r
+    return recs
+
+
+def fmt_rate(v: float) -> str:
+    if v >= 1e9:
+        return f"{v / 1e9:.2f} G"
+    if v >= 1e6:
+        return f"{v / 1e6:.2f} M"
+    if v >= 1e4:
+        return f"{v / 1e3:.1f} k"
+    return f"{v:,.0f}"
+
+
+def notes(r: dict) -> str:
+    c = r.get("config", {})
+    out = [f"{r['ms_per_step']:.3f} ms/step", f"batch {c.get('global_batch')}", r.get("dtype", "")]
+    if c.get("oracle_updates_per_s"):
+        out.append(f"{fmt_rate(c['oracle_updates_per_s'])} oracle updates/s")
+    if c.get("governance_actions_per_step"):
+        out.append(f"{c['governance_actions_per_step']} governance actions/step")
+    if c.get("comments_per_step"):
+        out.append(f"{c['comments_per_step']} comments/step")
+    return ", ".join(x for x in out if x)
+
+
+def render_baseline(recs) -> str:
+    lines = ["| config | reference number | MI355X 1 GPU (`bench.py`) | details | survey CPU comparator (§2) |",
+             "|---|---|---:|---|---|"]
+    for key, label, comp in ROWS:
+        r = recs.get(key)
+        if r is None:
+            continue
+        unit = "windows/s" if key == "c4" else "rounds/s"
+        lines.append(f"| {label} | none published | **{fmt_rate(r['value'])} {unit}** | {notes(r)} | {comp} |")
+    return "\n".join(lines)
+
+
+def render_readme(recs) -> str:
+    lines = ["| config | rounds/s (1× MI355X) | notes |", "|---|---:|---|"]
+    for key, label, _ in ROWS:
+        r = recs.get(key)
+        if r is None or key == "c1":
+            continue
+        unit = " windows/s" if key == "c4" else ""
+        lines.append(f"| {label} | **{fmt_rate(r['value'])}{unit}** | {notes(r)} |")
+    return "\n".join(lines)
+
+
+def splice(text: str, name: str, body: str) -> str:
+    pat = re.compile(rf"(<!-- results:{name}:begin -->).*?(<!-- results:{name}:end -->)", re.S)
+    if not pat.search(text):
+        raise SystemExit(f"markers for '{name}' not found")
+    return pat.sub(lambda m: m.group(1) + "\n" + body + "\n" + m.group(2), text)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--check", action="store_true")
+    a = ap.parse_args()
+    recs = load()
+    if not recs:
+        print("no profiles/results.jsonl", file=sys.stderr)
+        return 1
+    bad = 0
+    for doc, name, body in (("README.md", "readme", render_readme(recs)),
+                            ("BASELINE.md", "baseline", render_baseline(recs))):
+        path = os.path.join(ROOT, doc)
+        text = open(path, encoding="utf-8").read()
+        new = splice(text, name, body)
+        if a.check:
+            if new != text:
+                print(f"{doc}: results table out of date (python tools/results_table.py)", file=sys.stderr)
+                bad = 1
+        elif new != text:
+            open(path, "w", encoding="utf-8").write(new)
+            print(f"updated {doc}")
+    return bad
+
+
+if __name__ == "__main__":
+    sys.exit(main())
