@@ -347,9 +347,11 @@ using namespace svoc;
 // -2: not applicable (the caller runs the i128 kernel on every instance).
 extern "C" int svoc_exact_round_wsad(const ExactParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
-  // lane = column: below a wave's worth of columns most lanes idle, and the i128 kernel packs 8-32
-  // small instances per wave instead (7 x 6: 136 M vs 10 M rounds/s here)
-  if (!p->constrained || p->legacy || p->N < 4 || p->N > 256 || p->D < p->wsad_min_d) return -2;
+  // lane = column: with few columns most lanes idle, and for N <= 32 the i128 kernel packs 2-8
+  // instances per wave instead (profiles/r2_exact_crossover.json: 7 x 6 140 M vs 10 M rounds/s,
+  // 16 x 16 27 M vs 10 M; but 64 x 16 already 8.3 M vs 6.0 M for this kernel)
+  if (!p->constrained || p->legacy || p->N < 4 || p->N > 256) return -2;
+  if (p->N <= 32 && p->D < p->wsad_min_d) return -2;
   if (!p->stage || !p->fallback) return -2;
   if ((int64_t)p->N * p->D * (p->val32 ? 4 : 8) >= (1ll << 31)) return -2;   // 32-bit buffer offsets
   if (p->N <= 64) return launch_wsad<1>(*p, stream);
