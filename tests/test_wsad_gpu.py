@@ -146,3 +146,36 @@ def test_qr_probe_mfma_vs_valu_precision():
         err[v] = ((qr.double() - ref).abs() / ref).max().item()
     assert err[0] < 2e-5 and err[1] < 2e-3, err
     assert err[1] > err[0]
+
+
+@pytest.mark.parametrize("N,D,f", [(64, 1024, 8), (256, 512, 32)])
+def test_fast_bf16_agrees_with_exact_on_shared_grid(N, D, f):
+    """Fast (bf16 storage, fp32 math) vs exact (wsad) on data both represent exactly (x = j / 64, i.e.
+    wsad j * 15625): identical reliable masks, consensus within 1 wsad ulp, rel1 / rel2 within 32 wsad
+    ulps (the contract truncates every wsad_mul and its Newton sqrt; fp32 rounds).  Instances whose exact
+    quadratic risks tie across the rank cut are skipped (the tie rule then decides on values the two
+    modes round differently)."""
+    from helpers import run_fast
+    B = 32
+    x, _ = beta_oracles(B, N, D, f, seed=N + D, dtype=torch.float64)
+    j = torch.round(x[:, :, :D] * 64).clamp(0, 64)
+    vb = torch.zeros(B, N, (D + 7) // 8 * 8, dtype=torch.bfloat16)
+    vb[:, :, :D] = (j / 64).to(torch.bfloat16)
+    vw = (j * 15625).to(torch.int64).contiguous()
+    fa = run_fast(vb.to(DEV), D, f, True, 1.0)
+    ex = _run(vw.to(DEV, torch.int32), f)
+    torch.cuda.synchronize()
+    fa = {k: v.cpu() for k, v in fa.items()}
+    assert (ex["status"] == 0).all() and (fa["status"] == 0).all()
+    q = ex["qr"]
+    srt = torch.sort(q, dim=1).values
+    R = N - f
+    clean = srt[:, R - 1] != srt[:, R]          # no tie across the cut
+    assert clean.sum() >= B // 2
+    assert torch.equal(fa["reliable"][clean].bool(), ex["reliable"][clean].bool())
+    cons = (fa["consensus"][clean].double() * 1e6 - ex["consensus"][clean].double()).abs()
+    assert cons.max().item() <= 1.0 + 1e-6, cons.max()
+    # rel: the contract truncates every wsad product of its quadratic sums (D terms each), fp32 rounds;
+    # measured max 13 wsad ulps (1.3e-5) on 64 x 1024
+    rel = (fa["rel"][clean].double() * 1e6 - ex["rel"][clean].double()).abs()
+    assert rel.max().item() <= 32.0, rel.max()

@@ -26,6 +26,7 @@ ROWS = [
     ("c5", "c5: governance + reliability stream, 1M instances (7 × 6)", "≈127,900/s numpy fp64 (7×6)"),
     ("c2_exact", "c2 shape, exact wsad (bit-identical to the contract), int32 storage", "0.61/s exact Python emulator"),
     ("c2_exact_int64", "c2 shape, exact wsad, int64 storage", "0.61/s exact Python emulator"),
+    ("c3_exact", "c3 shape (256 × 4096), exact wsad, int32 storage", "≈6/s numpy fp64 (non-exact)"),
     ("c5_exact", "c5 shape (7 × 6), exact wsad, 1M instances", "939/s exact Python emulator"),
     ("wide512", "512 oracles × 2048 dims, 1024 instances (N > 256)", "—"),
 ]
