@@ -26,6 +26,7 @@
 // f - a + 1 <= H (H = 5 or 17); the dispatcher falls back to consensus_fast_reg.hip otherwise.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <utility>
 
@@ -729,12 +730,39 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   }
 }
 
-template <int NSEG, int H, bool CONS>
-static void launch_win_c(const FastParams& p, hipStream_t stream) {
-  constexpr int WAVES = 4;
+template <int NSEG, int WAVES, int H, bool CONS>
+static void launch_win_w(const FastParams& p, hipStream_t stream) {
   if (p.mode == 1) hipLaunchKernelGGL((consensus_fast_win_kernel<NSEG, WAVES, H, CONS, 1>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   else if (p.mode == 2) hipLaunchKernelGGL((consensus_fast_win_kernel<NSEG, WAVES, H, CONS, 2>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   else hipLaunchKernelGGL((consensus_fast_win_kernel<NSEG, WAVES, H, CONS, 0>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+}
+
+// Waves per workgroup (N > 128).  One workgroup per instance; 4 waves x 4 workgroups per CU (LDS
+// and the 128-VGPR cap) fill the 4 wave slots of every SIMD only from B = 4 x CUs instances on, and
+// c3's pipelined step launches ranges of 256-512.  8 waves (half the slabs per wave, 75 KiB of LDS,
+// 2 workgroups per CU) fill the SIMDs from 2 x CUs instances on and measured faster at every range
+// count, also at 1024 instances (c3: 4 waves 763 k / 771 k / 690 k rounds/s at 1 / 2 / 4 ranges,
+// 8 waves 784 k / 782 k / 803 k, 16 waves 757 k / 775 k / 728 k; profiles/r2_win_waves_ab.jsonl).
+// SVOC_WIN_WAVES=4|8|16 forces one.
+static int win_waves(const FastParams& p, int nseg) {
+  static const int forced = [] {
+    const char* e = getenv("SVOC_WIN_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  if (nseg != 4) return 4;
+  if (forced == 4 || forced == 8 || forced == 16) return forced;
+  constexpr int W8 = 8 * 16 * 2;   // columns per 8-wave slab
+  return p.D >= 2 * W8 ? 8 : 4;
+}
+
+template <int NSEG, int H, bool CONS>
+static void launch_win_c(const FastParams& p, hipStream_t stream) {
+  if constexpr (NSEG == 4) {
+    const int w = win_waves(p, NSEG);
+    if (w == 8) return launch_win_w<NSEG, 8, H, CONS>(p, stream);
+    if (w == 16) return launch_win_w<NSEG, 16, H, CONS>(p, stream);
+  }
+  launch_win_w<NSEG, 4, H, CONS>(p, stream);
 }
 
 template <int NSEG>
