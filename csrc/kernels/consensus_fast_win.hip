@@ -749,6 +749,7 @@ static int win_waves(const FastParams& p, int nseg) {
     const char* e = getenv("SVOC_WIN_WAVES");
     return e ? atoi(e) : 0;
   }();
+  if (nseg == 1) return forced == 2 || forced == 8 ? forced : 4;
   if (nseg != 4) return 4;
   if (forced == 4 || forced == 8 || forced == 16) return forced;
   constexpr int W8 = 8 * 16 * 2;   // columns per 8-wave slab
@@ -757,6 +758,11 @@ static int win_waves(const FastParams& p, int nseg) {
 
 template <int NSEG, int H, bool CONS>
 static void launch_win_c(const FastParams& p, hipStream_t stream) {
+  if constexpr (NSEG == 1) {
+    const int w = win_waves(p, NSEG);
+    if (w == 2) return launch_win_w<NSEG, 2, H, CONS>(p, stream);
+    if (w == 8) return launch_win_w<NSEG, 8, H, CONS>(p, stream);
+  }
   if constexpr (NSEG == 4) {
     const int w = win_waves(p, NSEG);
     if (w == 8) return launch_win_w<NSEG, 8, H, CONS>(p, stream);

@@ -10,7 +10,8 @@ def main(argv=None):
     ap.add_argument("--disable_startup_fetch", action="store_true", default=False)
     ap.add_argument("--dimension", type=int, default=DIMENSION)
     ap.add_argument("--live_mode", action="store_true", default=False)
-    ap.add_argument("--scraper", action="store_true", default=False, help="append synthetic comments on fetch")
+    ap.add_argument("--scraper", action="store_true", default=False, help="scrape (or synthesise) comments on fetch")
+    ap.add_argument("--scraper-source", default=None, help="URL or saved page for the scraper (svoc/models/scraper.py)")
     ap.add_argument("--rate", type=int, default=30 * 60, help="(kept for compatibility; no network)")
     ap.add_argument("--device", default="cpu")
     ap.add_argument("--mode", default="exact", choices=["exact", "fast"])
@@ -20,7 +21,7 @@ def main(argv=None):
     ap.add_argument("-c", "--command", action="append", default=[], help="run a command and exit")
     a = ap.parse_args(argv)
     cl = Client(device=a.device, mode=a.mode, db_path=a.db, encoder=a.encoder, dimension=a.dimension,
-                refresh_rate=a.refresh)
+                refresh_rate=a.refresh, scraper_source=a.scraper_source)
     cl.flags["scraper"] = a.scraper
     cl.flags["live_mode"] = a.live_mode
     if a.command:

@@ -3,8 +3,10 @@
 The reference UI sends text commands to ``web_interface.query`` (client/web_interface.py:133-303,
 help text :14-55).  Every command is kept; ``(S)`` commands that used to be Starknet RPC calls or
 transactions now call the in-process consensus engine (one contract instance, exact wsad mode by
-default, so the numbers are the contract's).  ``scraper on`` appends synthetic comments to the
-SQLite corpus (no network on the GPU boxes); ``live_mode on`` classifies the newest window.
+default, so the numbers are the contract's).  ``scraper on`` scrapes ``scraper_source`` (a URL or a
+saved page, svoc/models/scraper.py) into the SQLite corpus on every fetch, or appends synthetic
+comments when no source is set (no network on the GPU boxes); ``live_mode on`` classifies the newest
+window.
 
 Admin / oracle arguments accept an index or a ``0x...`` address; unlike the reference
 (client/contract.py:95-123, survey §2.8-10) addresses are compared as integers, so both work.
@@ -34,7 +36,7 @@ Commands :
     - auto_fetch on/off (default: off)
     - auto_commit on/off (default: off, ie. fetch => commit)
     - auto_resume on/off (default: off, ie. commit => resume)
-    - scraper on/off (default: off)       [synthetic comments appended to the corpus]
+    - scraper on/off (default: off)       [scrape --scraper-source (or synthetic comments) on fetch]
     - live_mode on/off (default: off)     [classify the newest window]
     - contract_declaration_address
     - contract_address
@@ -65,8 +67,10 @@ SIMULATION_REFRESH_RATE = 5.0                      # seconds between auto fetche
 class Client:
     def __init__(self, device: str = "cpu", mode: str = "exact", db_path: Optional[str] = None,
                  encoder: str = "tiny", dimension: int = DIMENSION, seed: int = 0,
-                 refresh_rate: float = SIMULATION_REFRESH_RATE, emit: Callable[[str], None] = print):
+                 refresh_rate: float = SIMULATION_REFRESH_RATE, emit: Callable[[str], None] = print,
+                 scraper_source: Optional[str] = None):
         self.device = device
+        self.scraper_source = scraper_source
         self.refresh_rate = float(refresh_rate)
         self.emit = emit                      # where the auto-fetch loop writes (the reference's console)
         self._lock = threading.RLock()        # one command at a time: the prompt and the auto-fetch loop
@@ -115,7 +119,11 @@ class Client:
     def fetch(self) -> str:
         """simulation_fetch (oracle_scheduler.py:155-161) + show_predictions (:136-153)."""
         if self.flags["scraper"]:
-            corpus.save_to_db(self.conn, corpus.synthetic_comments(30, seed=self.position + 1))
+            if self.scraper_source:
+                from .models.scraper import scrape_once
+                scrape_once(self.conn, self.scraper_source)
+            else:
+                corpus.save_to_db(self.conn, corpus.synthetic_comments(30, seed=self.position + 1))
         comments, stamps, self.position = corpus.read_window_from_db(self.conn, self.position)
         if self.flags["live_mode"]:
             n = self.conn.execute("SELECT COUNT(id) FROM comments").fetchone()[0]
