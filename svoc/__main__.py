@@ -19,7 +19,17 @@ def main(argv=None):
     ap.add_argument("--encoder", default="tiny", choices=["tiny", "base"])
     ap.add_argument("--refresh", type=float, default=5.0, help="auto_fetch period in seconds (client/common.py:11)")
     ap.add_argument("-c", "--command", action="append", default=[], help="run a command and exit")
+    ap.add_argument("--web", action="store_true", help="serve the browser UI instead (python -m svoc.web)")
+    ap.add_argument("--port", type=int, default=8080)
     a = ap.parse_args(argv)
+    if a.web:
+        from .web.app import main as web_main
+        args = ["--port", str(a.port), "--device", a.device, "--mode", a.mode, "--dimension", str(a.dimension),
+                "--refresh", str(a.refresh)]
+        args += ["--db", a.db] if a.db else []
+        args += ["--scraper-source", a.scraper_source] if a.scraper_source else []
+        args += ["--disable_startup_fetch"] if a.disable_startup_fetch else []
+        return web_main(args)
     cl = Client(device=a.device, mode=a.mode, db_path=a.db, encoder=a.encoder, dimension=a.dimension,
                 refresh_rate=a.refresh, scraper_source=a.scraper_source)
     cl.flags["scraper"] = a.scraper
