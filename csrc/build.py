@@ -61,7 +61,9 @@ def build(force: bool = False, jobs: int = 8, debug: bool = False, verbose: bool
     jobs_list = []
     for src in hip_srcs:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", *opt, *inc, "-c", src, "-o", obj]
+        # SVOC_HIPCC_FLAGS: extra kernel flags for A/B builds (e.g. -DSVOC_WIN_NT_STAGE=2)
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", *opt, *inc,
+               *os.environ.get("SVOC_HIPCC_FLAGS", "").split(), "-c", src, "-o", obj]
         jobs_list.append((src, obj, cmd))
     py_inc = sysconfig.get_paths()["include"]
     defs = ["-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", "-D_GLIBCXX_USE_CXX11_ABI=1", "-DTORCH_EXTENSION_NAME=_C"]

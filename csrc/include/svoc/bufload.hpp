@@ -21,6 +21,11 @@ SVOC_DEV __amdgpu_buffer_rsrc_t instance_rsrc(const void* base, uint32_t bytes) 
 SVOC_DEV uint32_t bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
 }
+// with a cache-policy operand (gfx950: 1 = sc0, 2 = nt, 16 = sc1)
+template <int AUX>
+SVOC_DEV uint32_t bload_p(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, AUX);
+}
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 SVOC_DEV void bstore(__amdgpu_buffer_rsrc_t r, uint32_t v, int voff, int soff) {

@@ -35,6 +35,13 @@
 #include "svoc/sortnet.hpp"
 #include "svoc/status.hpp"
 
+#ifndef SVOC_WIN_NT_STAGE
+#define SVOC_WIN_NT_STAGE 0
+#endif
+#ifndef SVOC_WIN_NT_REREAD
+#define SVOC_WIN_NT_REREAD 0
+#endif
+
 namespace svoc {
 
 // The reliable sums are trusted when sum_all(d^2) <= C * sum_R(d^2) and likewise for d^4, C =
@@ -145,8 +152,8 @@ SVOC_DEV void qr_moments_staged(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uin
   uint32_t wm[64];   // trees 2 and 3 from memory (indices i % 4 >= 2)
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
-    wm[2 + KEEP * m] = bload(rs, vo, (2 + KEEP * m) * rowb);
-    wm[3 + KEEP * m] = bload(rs, vo, (3 + KEEP * m) * rowb);
+    wm[2 + KEEP * m] = bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (2 + KEEP * m) * rowb);
+    wm[3 + KEEP * m] = bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (3 + KEEP * m) * rowb);
   }
   {
     uint32_t wv[64];
@@ -194,7 +201,7 @@ SVOC_DEV void qr_moments_staged_even(__amdgpu_buffer_rsrc_t rs, int vo, int rowb
   if constexpr (KEEP == 1) {
     uint32_t wv[64];
 #pragma unroll
-    for (int m = 0; m < 32; ++m) wv[2 * m + 1] = bload(rs, vo, (2 * m + 1) * rowb);
+    for (int m = 0; m < 32; ++m) wv[2 * m + 1] = bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (2 * m + 1) * rowb);
 #pragma unroll
     for (int m = 0; m < 32; ++m) wv[2 * m] = st[m * 64 + lane] ^ kp;
     if (MASKW) {
@@ -205,7 +212,7 @@ SVOC_DEV void qr_moments_staged_even(__amdgpu_buffer_rsrc_t rs, int vo, int rowb
   } else {
     uint32_t wm[64];   // tree 1 (odd rows) from memory, loads issued first
 #pragma unroll
-    for (int m = 0; m < 32; ++m) wm[2 * m + 1] = bload(rs, vo, (2 * m + 1) * rowb);
+    for (int m = 0; m < 32; ++m) wm[2 * m + 1] = bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (2 * m + 1) * rowb);
     {
       uint32_t wv[64];
 #pragma unroll
@@ -289,7 +296,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
       if (N == NPAD) {
         if (CONS) {
 #pragma unroll
-          for (int i = 0; i < 64; ++i) r[i] = as_k(bload(rs, vo, i * rowb) ^ kp);
+          for (int i = 0; i < 64; ++i) {
+            // rows staged in LDS are not read again: streaming policy for them, so the L2 keeps the
+            // rows the qr pass re-reads (SVOC_WIN_NT_STAGE, profiles/r2_win_nt_ab.txt)
+            const bool staged = STAGE && (NSEG == 4 ? (i & 3) < 2 : (i & 1) == 0);
+            r[i] = as_k((staged ? bload_p<SVOC_WIN_NT_STAGE>(rs, vo, i * rowb) : bload(rs, vo, i * rowb)) ^ kp);
+          }
           if constexpr (STAGE && NSEG == 4) {
 #pragma unroll
             for (int m = 0; m < 16; ++m) {
