@@ -129,8 +129,8 @@ def main():
         D_local = hi - lo
     cfg = ConsensusConfig(n_oracles=c["N"], dimension=D_local, n_failing_oracles=c["f"], constrained=True)
     mode = args.mode or c.get("mode", "fast")
-    if dshard and (mode != "fast" or args.config in ("c4", "c5")):
-        raise SystemExit("--dshard is for the fast column-sharded configs (c2, c3)")
+    if dshard and args.config in ("c4", "c5"):
+        raise SystemExit("--dshard is for the column-sharded configs (c2, c3, fast or exact)")
     eng = ConsensusEngine(cfg, batch=B, device=dev, mode=mode, storage=args.storage)
     eng.wave_hint = args.wave_hint
     dp = DataParallelConsensus(eng, rank=rank, world=world)

@@ -191,15 +191,18 @@ void exact_checks(const at::Tensor& values, const at::Tensor& c1, const at::Tens
 void exact_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t n_failing,
                      bool constrained, int64_t max_spread, at::Tensor c1, at::Tensor cons, at::Tensor skew,
                      at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable, at::Tensor status,
-                     bool legacy) {
+                     bool legacy, int64_t mode, int64_t rel_dim) {
   exact_checks(values, c1, cons, skew, kurt, rel, qr, reliable, status);
+  TORCH_CHECK(mode >= 0 && mode <= 2, "mode: 0 (whole round), 1 / 2 (D-sharded halves)");
   if (values.scalar_type() == at::kInt) {   // int32 wsad storage: the CPU engine works on int64
     exact_round_cpu(values.to(at::kLong), active, n_failing, constrained, max_spread, c1, cons, skew, kurt, rel, qr,
-                    reliable, status, legacy);
+                    reliable, status, legacy, mode, rel_dim);
     return;
   }
   ExactBatch eb{};
   eb.legacy = legacy;
+  eb.mode = (int)mode;
+  eb.rel_dim = rel_dim;
   eb.values = values.data_ptr<int64_t>();
   eb.B = values.size(0); eb.N = values.size(1); eb.D = values.size(2);
   eb.active = active_ptr(active, eb.B, values.device());
@@ -220,10 +223,13 @@ void exact_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& 
 void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t n_failing,
                      bool constrained, int64_t max_spread, at::Tensor c1, at::Tensor cons, at::Tensor skew,
                      at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable, at::Tensor status,
-                     bool legacy) {
+                     bool legacy, int64_t mode, int64_t rel_dim) {
   exact_checks(values, c1, cons, skew, kurt, rel, qr, reliable, status);
+  TORCH_CHECK(mode >= 0 && mode <= 2, "mode: 0 (whole round), 1 / 2 (D-sharded halves)");
   ExactParams p{};
   p.legacy = legacy ? 1 : 0;
+  p.mode = (int)mode;
+  p.rel_dim = (int)rel_dim;
   p.values = values.data_ptr();
   p.val32 = values.scalar_type() == at::kInt ? 1 : 0;
   p.B = (int)values.size(0); p.N = (int)values.size(1); p.D = (int)values.size(2);
@@ -249,7 +255,7 @@ void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& 
   // instances it flags; SVOC_EXACT_I128=1 forces the i128 kernel everywhere (tests, A/B)
   at::Tensor stage, fallback;
   const char* force = std::getenv("SVOC_EXACT_I128");
-  if (constrained && !legacy && p.N >= 4 && !(force && force[0] == '1')) {
+  if (constrained && !legacy && mode == 0 && p.N >= 4 && !(force && force[0] == '1')) {
     stage = at::empty({(int64_t)p.B, 4, (int64_t)p.D}, values.options().dtype(at::kInt));
     fallback = at::empty({(int64_t)p.B}, values.options().dtype(at::kByte));
     p.stage = stage.data_ptr<int32_t>();
@@ -276,7 +282,7 @@ TORCH_LIBRARY(svoc, m) {
   m.def(
       "exact_round(Tensor values, Tensor? active, int n_failing, bool constrained, int max_spread, "
       "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "
-      "Tensor(g!) reliable, Tensor(h!) status, bool legacy=False) -> ()");
+      "Tensor(g!) reliable, Tensor(h!) status, bool legacy=False, int mode=0, int rel_dim=0) -> ()");
   svoc::register_extra_defs(m);
 }
 

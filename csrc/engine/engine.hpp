@@ -37,11 +37,14 @@ struct ExactBatch {
   int64_t* c1;         // [B, D] or null
   int32_t* status;     // [B]
   bool legacy = false;  // obsolete contracts (contract_nd.cairo / contract_1d_constrained.cairo)
+  int mode = 0;         // D-sharded split (launch.hpp ExactParams::mode): 1 = c1 + qr partials, 2 = rest
+  int64_t rel_dim = 0;  // reliability dimension (global D), 0 = D
 };
 
 // legacy: reliability W - 2 sqrt(mean qr) without the /D (contract_nd.cairo:418,437) and no moments.
+// mode 1 / 2: D-sharded split (ExactBatch::mode); mode 2 reads o.c1 and o.qr (the all-reduced qr).
 int exact_round_one(const int64_t* X, int64_t N, int64_t D, int64_t n_failing, bool constrained,
-                    int64_t max_spread, ExactOut& o, bool legacy = false);
+                    int64_t max_spread, ExactOut& o, bool legacy = false, int mode = 0, int64_t rel_dim = 0);
 void exact_round_batch_cpu(const ExactBatch& b, int threads);
 
 // ---- fast (float compute, bf16/fp32 storage) ---------------------------------------------------

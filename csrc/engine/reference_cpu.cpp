@@ -53,22 +53,34 @@ i128 average_exact(const std::vector<i128>& v, int& st) {  // math.cairo:240-254
 }  // namespace
 
 int exact_round_one(const int64_t* X, int64_t N, int64_t D, int64_t n_failing, bool constrained,
-                    int64_t max_spread, ExactOut& o, bool legacy) {
+                    int64_t max_spread, ExactOut& o, bool legacy, int mode, int64_t rel_dim) {
   int st = ST_OK;
-  const int64_t rdim = legacy ? 1 : D;
+  const int64_t rdim = legacy ? 1 : (rel_dim > 0 ? rel_dim : D);
   std::vector<i128> col(N);
-  // ---- pass 1: essence (contract.cairo:455-459)
-  for (int64_t d = 0; d < D && st == ST_OK; ++d) {
-    for (int64_t i = 0; i < N; ++i) col[i] = X[i * D + d];
-    o.c1[d] = (int64_t)smooth_median_exact(col, st);
-  }
-  if (st) return st;
-  // quadratic risk (math.cairo:225-238)
   std::vector<i128> qr(N);
-  for (int64_t i = 0; i < N; ++i) {
-    i128 acc = 0;
-    for (int64_t d = 0; d < D; ++d) acc = add(acc, qdev(X[i * D + d], o.c1[d], st), st);
-    qr[i] = acc;
+  if (mode == 2) {   // D-sharded: c1 (this shard) and the all-reduced qr come in
+    for (int64_t i = 0; i < N; ++i) qr[i] = o.qr[i];
+  } else {
+    // ---- pass 1: essence (contract.cairo:455-459)
+    for (int64_t d = 0; d < D && st == ST_OK; ++d) {
+      for (int64_t i = 0; i < N; ++i) col[i] = X[i * D + d];
+      o.c1[d] = (int64_t)smooth_median_exact(col, st);
+    }
+    if (st) return st;
+    // quadratic risk (math.cairo:225-238)
+    for (int64_t i = 0; i < N; ++i) {
+      i128 acc = 0;
+      for (int64_t d = 0; d < D; ++d) acc = add(acc, qdev(X[i * D + d], o.c1[d], st), st);
+      qr[i] = acc;
+    }
+    if (mode == 1) {   // partials for the shard all-reduce (int64 sum)
+      if (st) return st;
+      for (int64_t i = 0; i < N; ++i) {
+        if (qr[i] >= kExactQrPartialMax || qr[i] <= -kExactQrPartialMax) return ST_OVERFLOW;
+        o.qr[i] = (int64_t)qr[i];
+      }
+      return ST_OK;
+    }
   }
   i128 mean_qr = average_exact(qr, st);
   i128 rel1 = constrained ? constrained_reliability(mean_qr, rdim, st)
@@ -152,10 +164,21 @@ void exact_round_batch_cpu(const ExactBatch& b, int threads) {
     const int64_t N = b.N, D = b.D;
     std::vector<int64_t> c1(D), cons(D), sk(D), ku(D), qr(N);
     std::vector<uint8_t> rel(N);
+    if (b.mode == 2) {
+      if (b.status[i] != ST_OK) return;   // a shard's pass 1 failed: the round reverts everywhere
+      std::memcpy(c1.data(), b.c1 + i * D, D * sizeof(int64_t));
+      std::memcpy(qr.data(), b.qr + i * N, N * sizeof(int64_t));
+    }
     ExactOut o{c1.data(), qr.data(), rel.data(), cons.data(), sk.data(), ku.data(), 0, 0};
-    int st = exact_round_one(b.values + i * N * D, N, D, b.n_failing, b.constrained, b.max_spread, o, b.legacy);
+    int st = exact_round_one(b.values + i * N * D, N, D, b.n_failing, b.constrained, b.max_spread, o, b.legacy,
+                             b.mode, b.rel_dim);
     b.status[i] = st;
     if (st != ST_OK) return;  // revert: outputs untouched
+    if (b.mode == 1) {
+      std::memcpy(b.qr + i * N, qr.data(), N * sizeof(int64_t));
+      if (b.c1) std::memcpy(b.c1 + i * D, c1.data(), D * sizeof(int64_t));
+      return;
+    }
     std::memcpy(b.consensus + i * D, cons.data(), D * sizeof(int64_t));
     std::memcpy(b.skew + i * D, sk.data(), D * sizeof(int64_t));
     std::memcpy(b.kurt + i * D, ku.data(), D * sizeof(int64_t));

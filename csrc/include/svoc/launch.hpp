@@ -71,7 +71,14 @@ struct ExactParams {
   uint8_t* fallback;
   int skip_fallback;        // tests: leave the flagged instances alone (shows which rounds it took)
   int wsad_min_d;           // fewest columns the column-parallel kernel takes (default 64: one lane per column)
+  // D-sharded rounds (svoc/parallel/dshard.py): 0 = whole round; 1 = pass 1 only -> c1 and the
+  // instance's qr PARTIALS (this shard's columns) into c1 / qr, status; 2 = from c1 and the all-reduced
+  // qr (inputs) on instances whose status is OK: rank mask, pass 2, moments, commit.  rel_dim: the
+  // reliability's dimension (the GLOBAL D; 0 = D).
+  int mode;
+  int rel_dim;
 };
+
 
 }  // namespace svoc
 

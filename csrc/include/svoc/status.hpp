@@ -27,4 +27,8 @@ enum Status : int {
   ST_NON_FINITE = 34,  // unconstrained float update with NaN / inf
 };
 
+// D-sharded exact rounds (split mode 1): bound on |qr partial|, so the int64 all-reduce of up to 32
+// shards' partials cannot wrap; a larger partial reverts the round with OVERFLOW.
+constexpr long long kExactQrPartialMax = 1ll << 58;
+
 }  // namespace svoc

@@ -146,37 +146,67 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
   int st = ST_OK;  // group-uniform by construction (every lane runs the same checked reductions)
 
   Rows<RPL> rows;
-  // ---- pass 1: c1 per column
-  for (int d = 0; d < D && st == ST_OK; ++d) {
+  i128 qr[RPL];
+  if (p.mode == 2) {
+    // D-sharded second half: this shard's c1 and the all-reduced qr come in; a shard whose first half
+    // failed has already set the (all-reduced) status
+    if (p.status[b] != ST_OK) return;
+    for (int d = gl; d < D; d += GS) c1[d] = p.c1[(int64_t)b * D + d];
 #pragma unroll
     for (int j = 0; j < RPL; ++j) {
       const int row = j * GS + gl;
-      rows.on[j] = row < N;
-      rows.x[j] = row < N ? X[(int64_t)row * D + d] : 0;
+      qr[j] = row < N ? (i128)p.qr[(int64_t)b * N + row] : 0;
     }
-    const i128 c = smooth_median_w<RPL, GS>(rows, g, N, N, cs, st);
-    if (gl == 0) c1[d] = (int64_t)c;
-  }
-  __syncthreads();
-  if (st != ST_OK) { if (gl == 0) p.status[b] = st; return; }
-  // quadratic risk per row (lane-local), then the checked mean
-  i128 qr[RPL];
-  int lst = ST_OK;
+    __syncthreads();
+  } else {
+    // ---- pass 1: c1 per column
+    for (int d = 0; d < D && st == ST_OK; ++d) {
 #pragma unroll
-  for (int j = 0; j < RPL; ++j) {
-    const int row = j * GS + gl;
-    i128 acc = 0;
-    if (row < N)
-      for (int d = 0; d < D; ++d) acc = add(acc, qdev(X[(int64_t)row * D + d], c1[d], lst), lst);
-    qr[j] = acc;
+      for (int j = 0; j < RPL; ++j) {
+        const int row = j * GS + gl;
+        rows.on[j] = row < N;
+        rows.x[j] = row < N ? X[(int64_t)row * D + d] : 0;
+      }
+      const i128 c = smooth_median_w<RPL, GS>(rows, g, N, N, cs, st);
+      if (gl == 0) c1[d] = (int64_t)c;
+    }
+    __syncthreads();
+    if (st != ST_OK) { if (gl == 0) p.status[b] = st; return; }
+    // quadratic risk per row (lane-local), then the checked mean
+    int lst = ST_OK;
+#pragma unroll
+    for (int j = 0; j < RPL; ++j) {
+      const int row = j * GS + gl;
+      i128 acc = 0;
+      if (row < N)
+        for (int d = 0; d < D; ++d) acc = add(acc, qdev(X[(int64_t)row * D + d], c1[d], lst), lst);
+      qr[j] = acc;
+    }
+    // any lane's overflow reverts (qr can only fail with OVERFLOW)
+    if (g.any_or(lst != ST_OK)) st = ST_OVERFLOW;
+    if (p.mode == 1) {   // D-sharded first half: c1 and the qr partials out, nothing else
+      bool big = false;
+#pragma unroll
+      for (int j = 0; j < RPL; ++j) big = big || qr[j] >= (i128)kExactQrPartialMax || qr[j] <= -(i128)kExactQrPartialMax;
+      if (g.any_or(big)) st = ST_OVERFLOW;
+      if (st == ST_OK) {
+        for (int d = gl; d < D; d += GS) p.c1[(int64_t)b * D + d] = c1[d];
+#pragma unroll
+        for (int j = 0; j < RPL; ++j) {
+          const int row = j * GS + gl;
+          if (row < N) p.qr[(int64_t)b * N + row] = (int64_t)qr[j];
+        }
+      }
+      if (gl == 0) p.status[b] = st;
+      return;
+    }
   }
-  // any lane's overflow reverts (qr can only fail with OVERFLOW)
-  if (g.any_or(lst != ST_OK)) st = ST_OVERFLOW;
   i128 sum_qr = 0;
 #pragma unroll
   for (int j = 0; j < RPL; ++j) sum_qr = add(sum_qr, g.sum(qr[j], st), st);
   const i128 mean_qr = idiv(sum_qr, (i128)N, st);
-  const int64_t rdim = p.legacy ? 1 : D;  // obsolete contracts: no /D (contract_nd.cairo:418)
+  // obsolete contracts: no /D (contract_nd.cairo:418); D-sharded rounds: the global D
+  const int64_t rdim = p.legacy ? 1 : (p.rel_dim > 0 ? p.rel_dim : D);
   const i128 rel1 = p.constrained ? constrained_reliability(mean_qr, rdim, st)
                                   : unconstrained_reliability(wsqrt(mean_qr, st), p.max_spread, st);
   if (st == ST_OK && !in_unit_interval(rel1)) st = ST_RELIABILITY_INTERVAL;
@@ -348,7 +378,7 @@ static int exact_round_i128(const ExactParams* p, hipStream_t stream) {
 extern "C" int svoc_exact_round(const ExactParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
   if (p->N < 1 || p->N > 1024 || p->D < 1) return -1;
-  if (p->stage && p->fallback) {
+  if (p->stage && p->fallback && p->mode == 0) {
     const int rc = svoc_exact_round_wsad(p, stream);
     if (rc != -2) {
       if (rc != 0 || p->skip_fallback) return rc;

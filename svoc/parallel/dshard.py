@@ -16,6 +16,13 @@ Per-instance atomicity across shards (survey §2.6; contract.cairo:588-603 rever
 zero-variance check of pass 2 sees only the local columns, so pass 2 writes into shadow outputs, the
 [B] status words are all-reduced (MAX: any shard's failure code wins, OK = 0), and only instances
 whose reduced status is OK commit -- on every rank, or on none.
+
+Exact (wsad) engines split the same way (the i128 kernel / CPU golden engine, modes 1 and 2): qr is
+a sum of per-column integer terms (each truncated on its own, math.cairo:225-238), so the int64
+all-reduce of the shards' partials IS the contract's qr and a successful sharded round is bit-identical
+to the unsharded one.  Differences, by construction: a shard's partial must stay below 2^58 (else the
+round reverts with OVERFLOW; the contract's i128 sum would only overflow near 2^127), and a reverted
+round reports the largest of the shards' codes, not the contract's first error in evaluation order.
 """
 from __future__ import annotations
 
@@ -36,6 +43,7 @@ class _Shadow:
 
     def __init__(self, e):
         self.qr = torch.zeros_like(e.qr)
+        self.c1 = torch.zeros_like(e.c1)
         self.consensus = torch.zeros_like(e.consensus)
         self.skew = torch.zeros_like(e.skew)
         self.kurt = torch.zeros_like(e.kurt)
@@ -45,25 +53,35 @@ class _Shadow:
 
 def run_round_sharded(engine, d_global: int, group=None, world: int = 1) -> None:
     """Consensus round for an engine holding a column shard of every instance."""
-    if engine.mode != "fast":
-        raise NotImplementedError("D-sharding is implemented for the fast (float) engine")
     e = engine
     sh = getattr(e, "_dshard_shadow", None)
     if sh is None:
         sh = e._dshard_shadow = _Shadow(e)
     e._ops.round_prologue(e.n_active, e.touched, e.N, True, e._active)
-    mx = float(e.cfg.unconstrained_max_spread)
     lg = e.cfg.legacy
-    w = e.work()                                     # window kernel: pass 1 -> pass 2 state
-    head = (e.values, e._active, e.D, e.cfg.n_failing_oracles, e.cfg.constrained, mx, e.c1)
-    # pass 1: local c1 + qr partials (into the shadow qr: the committed qr stays intact)
-    e._ops.fast_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status,
-                      e.wave_hint, 1, d_global, lg, w)
-    if world > 1:
-        dist.all_reduce(sh.qr, op=dist.ReduceOp.SUM, group=group)
-    # pass 2 from the global qr, into the shadow outputs; status = this shard's verdict
-    e._ops.fast_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status,
-                      e.wave_hint, 2, d_global, lg, w)
+    if e.mode == "fast":
+        mx = float(e.cfg.unconstrained_max_spread)
+        w = e.work()                                     # window kernel: pass 1 -> pass 2 state
+        head = (e.values, e._active, e.D, e.cfg.n_failing_oracles, e.cfg.constrained, mx, e.c1)
+        # pass 1: local c1 + qr partials (into the shadow qr: the committed qr stays intact)
+        e._ops.fast_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status,
+                          e.wave_hint, 1, d_global, lg, w)
+        if world > 1:
+            dist.all_reduce(sh.qr, op=dist.ReduceOp.SUM, group=group)
+        # pass 2 from the global qr, into the shadow outputs; status = this shard's verdict
+        e._ops.fast_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status,
+                          e.wave_hint, 2, d_global, lg, w)
+    else:
+        head = (e.values, e._active, e.cfg.n_failing_oracles, e.cfg.constrained, e.cfg.max_spread_wsad, sh.c1)
+        # first half: c1 + int64 qr partials; a shard that fails here (overflow) fails the round
+        e._ops.exact_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status, lg,
+                           1, d_global)
+        if world > 1:
+            dist.all_reduce(sh.qr, op=dist.ReduceOp.SUM, group=group)
+            dist.all_reduce(e.status, op=dist.ReduceOp.MAX, group=group)
+        # second half on the instances every shard passed (the kernel skips non-OK statuses)
+        e._ops.exact_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status, lg,
+                           2, d_global)
     if world > 1:
         dist.all_reduce(e.status, op=dist.ReduceOp.MAX, group=group)
     ok = (e._active != 0) & (e.status == int(Status.OK))
@@ -74,5 +92,7 @@ def run_round_sharded(engine, d_global: int, group=None, world: int = 1) -> None
     e.rel.copy_(torch.where(ok1, sh.rel, e.rel))
     e.qr.copy_(torch.where(ok1, sh.qr, e.qr))
     e.reliable.copy_(torch.where(ok1, sh.reliable, e.reliable))
+    if e.mode != "fast":
+        e.c1.copy_(torch.where(ok1, sh.c1, e.c1))
     e._ops.round_epilogue(e._active, e.status, e.rel, e.consensus_active, e.touched, e.metrics_fx)
     e.rounds += 1

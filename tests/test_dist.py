@@ -160,3 +160,62 @@ def test_dsharding_revert_is_atomic_across_shards():
     for inst in (1, 3):
         assert torch.equal(snaps[1]["cons"][inst], snaps[0]["cons"][inst])
         assert torch.equal(snaps[1]["qr"][inst], snaps[0]["qr"][inst])
+
+
+def _ds_exact_worker(rank, world, port, outdir, xs, cfgd):
+    _init(rank, world, port)
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    from svoc.parallel.dshard import run_round_sharded, shard_bounds
+    cfg = ConsensusConfig(**cfgd)
+    lo, hi = shard_bounds(cfg.dimension, rank, world)
+    e = ConsensusEngine(ConsensusConfig(**{**cfgd, "dimension": hi - lo}), xs[0].shape[0], device="cpu", mode="exact")
+    out = []
+    for x in xs:
+        e.values.copy_(x[:, :, lo:hi].to(e.values.dtype))
+        e.enabled.fill_(1); e.n_active.fill_(cfg.n_oracles); e.touched.fill_(1)
+        run_round_sharded(e, cfg.dimension, world=world)
+        out.append({k: getattr(e, k).clone() for k in ("consensus", "skew", "kurt", "rel", "qr", "reliable", "c1",
+                                                        "status", "consensus_active")})
+    torch.save(dict(out=out, lo=lo, hi=hi), os.path.join(outdir, f"dse{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("constrained,world", [(True, 2), (True, 3), (False, 2)])
+def test_dsharding_exact_bit_identical(constrained, world):
+    """Exact (wsad) engine, D-sharded: every output of every round equals the single-process exact engine
+    bit for bit (qr = the int64 sum of the shards' partials); a zero-variance column in one shard reverts
+    the instance on every shard with the single-process code, leaving the previous round's outputs."""
+    from helpers import beta_oracles
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    B, N, D, f = 4, 16, 11, 3
+    xs = []
+    for seed in (31, 32):
+        x, _ = beta_oracles(B, N, D, f, seed=seed, dtype=torch.float64)
+        xs.append((x[:, :, :D] * 1e6).to(torch.int64).contiguous())
+    xs[1][1, :, 1] = 500_000      # shard 0's column: zero variance -> that instance reverts
+    if not constrained:
+        xs = [x - 400_000 for x in xs]   # signed values (unconstrained domain)
+    cfgd = dict(n_oracles=N, dimension=D, n_failing_oracles=f, constrained=constrained,
+                unconstrained_max_spread=1.0)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ds_exact_worker, args=(world, _free_port(), d, xs, cfgd), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"dse{i}.pt"), weights_only=True) for i in range(world)]
+    ref = ConsensusEngine(ConsensusConfig(**cfgd), B, device="cpu", mode="exact")
+    snaps = []
+    for x in xs:
+        ref.values.copy_(x.to(ref.values.dtype))
+        ref.enabled.fill_(1); ref.n_active.fill_(N); ref.touched.fill_(1)
+        ref.run_round()
+        snaps.append({k: getattr(ref, k).clone() for k in ("consensus", "skew", "kurt", "rel", "qr", "reliable",
+                                                            "c1", "status", "consensus_active")})
+    assert snaps[0]["status"].tolist() == [0] * B
+    assert snaps[1]["status"][1].item() != 0 and snaps[1]["status"][[0, 2, 3]].tolist() == [0, 0, 0]
+    for s in r:
+        lo, hi = s["lo"], s["hi"]
+        for k, (o, ref_o) in enumerate(zip(s["out"], snaps)):
+            for name in ("rel", "qr", "reliable", "status", "consensus_active"):
+                assert torch.equal(o[name], ref_o[name]), (k, name)
+            for name in ("consensus", "skew", "kurt", "c1"):
+                assert torch.equal(o[name], ref_o[name][:, lo:hi]), (k, name)

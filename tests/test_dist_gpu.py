@@ -104,3 +104,43 @@ def test_rccl_backend_world1():
     with tempfile.TemporaryDirectory() as d:
         mp.spawn(_rccl_worker, args=(1, _free_port(), d), nprocs=1, join=True)
         assert torch.load(os.path.join(d, "rccl.pt"), weights_only=True).tolist() == [0, 1, 2, 3]
+
+
+def _ds_exact_worker(rank, world, port, outdir, x, cfgd):
+    _init(rank, world, port)
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    from svoc.parallel.dshard import run_round_sharded, shard_bounds
+    cfg = ConsensusConfig(**cfgd)
+    lo, hi = shard_bounds(cfg.dimension, rank, world)
+    e = ConsensusEngine(ConsensusConfig(**{**cfgd, "dimension": hi - lo}), x.shape[0], device="cuda", mode="exact")
+    e.values.copy_(x[:, :, lo:hi].to("cuda", e.values.dtype))
+    e.enabled.fill_(1); e.n_active.fill_(cfg.n_oracles); e.touched.fill_(1)
+    run_round_sharded(e, cfg.dimension, world=world)
+    torch.save({k: getattr(e, k).cpu() for k in ("consensus", "skew", "kurt", "rel", "qr", "reliable", "status")}
+               | dict(lo=lo, hi=hi), os.path.join(outdir, f"dse{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_dsharding_exact_two_ranks_on_one_gpu():
+    """Exact (wsad) D-sharding on the GPU i128 kernel's split modes: bit-identical to one whole round."""
+    from helpers import beta_oracles
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    B, N, D, f = 6, 64, 200, 8
+    x, _ = beta_oracles(B, N, D, f, seed=9, dtype=torch.float64)
+    x = (x[:, :, :D] * 1e6).to(torch.int64).contiguous()
+    cfgd = dict(n_oracles=N, dimension=D, n_failing_oracles=f, constrained=True)
+    ref = ConsensusEngine(ConsensusConfig(**cfgd), B, device="cuda", mode="exact")
+    ref.values.copy_(x.to("cuda", ref.values.dtype))
+    ref.enabled.fill_(1); ref.n_active.fill_(N); ref.touched.fill_(1)
+    ref.run_round()
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ds_exact_worker, args=(2, _free_port(), d, x, cfgd), nprocs=2, join=True)
+        r = [torch.load(os.path.join(d, f"dse{i}.pt"), weights_only=True) for i in range(2)]
+    assert (ref.status == 0).all()
+    for s in r:
+        for k in ("rel", "qr", "reliable", "status"):
+            assert torch.equal(s[k], getattr(ref, k).cpu()), k
+        for k in ("consensus", "skew", "kurt"):
+            assert torch.equal(s[k], getattr(ref, k).cpu()[:, s["lo"]:s["hi"]]), k

@@ -179,3 +179,38 @@ def test_fast_bf16_agrees_with_exact_on_shared_grid(N, D, f):
     # measured max 13 wsad ulps (1.3e-5) on 64 x 1024
     rel = (fa["rel"][clean].double() * 1e6 - ex["rel"][clean].double()).abs()
     assert rel.max().item() <= 32.0, rel.max()
+
+
+@pytest.mark.parametrize("N,D,f", [(16, 24, 3), (64, 300, 8), (256, 70, 32)])
+def test_exact_split_modes_match_whole_round(N, D, f):
+    """The i128 kernel's D-sharded halves (mode 1: c1 + qr partials; mode 2: from the summed qr), run on
+    two column slices on one GPU with the all-reduce done by hand, reproduce the whole round bit for bit."""
+    B = 8
+    v = _wsad(B, N, D, f, seed=N + 7 * D)
+    v[2, :, D // 4] = 123_456           # zero variance in slice 0 only: instance 2 reverts
+    vg = v.to(DEV)
+    whole = _run(vg, f)
+    cut = D // 2
+    parts = [vg[:, :, :cut].contiguous(), vg[:, :, cut:].contiguous()]
+    outs = [alloc_exact_out(B, N, x.shape[2], DEV) for x in parts]
+    op = svops.ops().exact_round
+    for x, o in zip(parts, outs):
+        op(x, None, f, True, 0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"], o["qr"], o["reliable"],
+           o["status"], False, 1, D)
+    qr = outs[0]["qr"] + outs[1]["qr"]
+    st = torch.maximum(outs[0]["status"], outs[1]["status"])
+    for x, o in zip(parts, outs):
+        o["qr"].copy_(qr)
+        o["status"].copy_(st)
+        op(x, None, f, True, 0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"], o["qr"], o["reliable"],
+           o["status"], False, 2, D)
+    st = torch.maximum(outs[0]["status"], outs[1]["status"]).cpu()
+    torch.cuda.synchronize()
+    assert torch.equal(st, whole["status"]) and st[2].item() != 0 and (st != 0).sum().item() == 1
+    ok = st == 0
+    for o in outs:
+        for k in ("rel", "qr", "reliable"):
+            assert torch.equal(o[k].cpu()[ok], whole[k][ok]), k
+    for k in ("c1", "consensus", "skew", "kurt"):
+        got = torch.cat([outs[0][k].cpu(), outs[1][k].cpu()], dim=1)
+        assert torch.equal(got[ok], whole[k][ok]), k
