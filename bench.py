@@ -111,7 +111,7 @@ def main():
             dist.init_process_group(args.backend or "nccl", device_id=dev)
         else:
             dist.init_process_group(args.backend or "gloo")
-    dshard = args.dshard and world > 1
+    dshard = args.dshard   # world 1: the split-kernel path without collectives (its overhead)
 
     from svoc.config import ConsensusConfig
     from svoc.engine import ConsensusEngine
@@ -207,7 +207,7 @@ def main():
     sync()
 
     graph = None
-    if args.graph and dev.type == "cuda" and not dshard:   # (no collectives inside a captured graph)
+    if args.graph and dev.type == "cuda" and not (dshard and world > 1):   # (no collectives in a graph)
         # the stream cycles with period `pool`: capture one period and replay it
         import math
         period = 1
