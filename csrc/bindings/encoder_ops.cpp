@@ -10,6 +10,10 @@
 
 extern "C" int svoc_add_layernorm_bf16(const void* x, const void* y, const void* w, const void* b, void* out,
                                        int64_t rows, int H, float eps, hipStream_t stream);
+extern "C" int svoc_embed_layernorm_bf16(const int64_t* ids, const int64_t* pos_ids, const void* tok, const void* pos,
+                                         const void* typ, const void* w, const void* b, void* out, int64_t rows, int H,
+                                         float eps, hipStream_t stream);
+extern "C" int svoc_segment_mean_bf16(const void* x, const int* cu, void* out, int64_t B, int H, hipStream_t stream);
 
 namespace svoc {
 namespace {
@@ -44,6 +48,69 @@ at::Tensor add_layernorm_hip(const at::Tensor& x, const at::Tensor& y, const at:
   return out;
 }
 
+// embeddings: LayerNorm(tok[ids] + pos[pos_ids] + typ[0]) (the sum in the weights' dtype, as the
+// PyTorch expression it replaces)
+at::Tensor embed_layernorm_ref(const at::Tensor& ids, const at::Tensor& pos_ids, const at::Tensor& tok,
+                               const at::Tensor& pos, const at::Tensor& typ, const at::Tensor& w, const at::Tensor& b,
+                               double eps) {
+  const int64_t H = tok.size(1);
+  auto e = tok.index_select(0, ids) + pos.index_select(0, pos_ids) + typ.reshape({-1, H}).select(0, 0);
+  return at::layer_norm(e, {H}, w, b, eps);
+}
+
+at::Tensor embed_layernorm_cpu(const at::Tensor& ids, const at::Tensor& pos_ids, const at::Tensor& tok,
+                               const at::Tensor& pos, const at::Tensor& typ, const at::Tensor& w, const at::Tensor& b,
+                               double eps) {
+  return embed_layernorm_ref(ids, pos_ids, tok, pos, typ, w, b, eps);
+}
+
+at::Tensor embed_layernorm_hip(const at::Tensor& ids, const at::Tensor& pos_ids, const at::Tensor& tok,
+                               const at::Tensor& pos, const at::Tensor& typ, const at::Tensor& w, const at::Tensor& b,
+                               double eps) {
+  TORCH_CHECK(ids.dim() == 1 && pos_ids.sizes() == ids.sizes(), "ids / pos_ids: [T]");
+  TORCH_CHECK(tok.dim() == 2 && pos.dim() == 2 && pos.size(1) == tok.size(1), "tok / pos tables: [V, H]");
+  const int64_t H = tok.size(1);
+  TORCH_CHECK(typ.numel() >= H && w.numel() == H && b.numel() == H, "typ / weight / bias: H elements");
+  const auto bf = at::kBFloat16;
+  const bool fast = tok.scalar_type() == bf && pos.scalar_type() == bf && typ.scalar_type() == bf &&
+                    w.scalar_type() == bf && b.scalar_type() == bf && hip_supported(H);
+  if (!fast) return embed_layernorm_ref(ids, pos_ids, tok, pos, typ, w, b, eps);
+  auto ic = ids.to(at::kLong).contiguous(), pc = pos_ids.to(at::kLong).contiguous();
+  auto tc = tok.contiguous(), qc = pos.contiguous(), yc = typ.contiguous(), wc = w.contiguous(), bc = b.contiguous();
+  auto out = at::empty({ids.size(0), H}, tc.options());
+  const int rc = svoc_embed_layernorm_bf16(ic.data_ptr<int64_t>(), pc.data_ptr<int64_t>(), tc.data_ptr(), qc.data_ptr(),
+                                           yc.data_ptr(), wc.data_ptr(), bc.data_ptr(), out.data_ptr(), ids.size(0),
+                                           (int)H, (float)eps, c10::hip::getCurrentHIPStream(tok.device().index()).stream());
+  TORCH_CHECK(rc == 0, "svoc_embed_layernorm_bf16 failed: ", rc);
+  return out;
+}
+
+// mean of x[t] over each segment [cu[b], cu[b+1]) (fp32 sums, empty segment -> 0)
+at::Tensor segment_mean_ref(const at::Tensor& x, const at::Tensor& cu) {
+  const int64_t B = cu.numel() - 1, H = x.size(1);
+  auto cul = cu.to(at::kLong);
+  auto lens = cul.slice(0, 1) - cul.slice(0, 0, B);
+  auto seg = at::repeat_interleave(at::arange(B, cul.options()), lens, c10::nullopt);
+  auto s = at::zeros({B, H}, x.options().dtype(at::kFloat)).index_add_(0, seg, x.to(at::kFloat));
+  return (s / lens.clamp_min(1).to(at::kFloat).unsqueeze(1)).to(x.scalar_type());
+}
+
+at::Tensor segment_mean_cpu(const at::Tensor& x, const at::Tensor& cu) { return segment_mean_ref(x, cu); }
+
+at::Tensor segment_mean_hip(const at::Tensor& x, const at::Tensor& cu) {
+  TORCH_CHECK(x.dim() == 2 && cu.dim() == 1 && cu.numel() >= 1, "x: [T, H], cu_seqlens: [B + 1]");
+  TORCH_CHECK(cu.scalar_type() == at::kInt && cu.is_contiguous() && cu.device() == x.device(),
+              "cu_seqlens: int32 on the device");
+  const int64_t B = cu.numel() - 1, H = x.size(1);
+  if (x.scalar_type() != at::kBFloat16 || H % 8 != 0 || H / 8 > 256) return segment_mean_ref(x, cu);
+  auto xc = x.contiguous();
+  auto out = at::empty({B, H}, xc.options());
+  const int rc = svoc_segment_mean_bf16(xc.data_ptr(), cu.data_ptr<int>(), out.data_ptr(), B, (int)H,
+                                        c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  TORCH_CHECK(rc == 0, "svoc_segment_mean_bf16 failed: ", rc);
+  return out;
+}
+
 }  // namespace
 
 void register_attention_defs(torch::Library& m);
@@ -52,14 +119,21 @@ void register_attention_hip(torch::Library& m);
 
 void register_encoder_defs(torch::Library& m) {
   m.def("add_layernorm(Tensor x, Tensor y, Tensor weight, Tensor bias, float eps) -> Tensor");
+  m.def("embed_layernorm(Tensor ids, Tensor pos_ids, Tensor tok, Tensor pos, Tensor typ, Tensor weight, Tensor bias, "
+        "float eps) -> Tensor");
+  m.def("segment_mean(Tensor x, Tensor cu_seqlens) -> Tensor");
   register_attention_defs(m);
 }
 void register_encoder_cpu(torch::Library& m) {
   m.impl("add_layernorm", &add_layernorm_cpu);
+  m.impl("embed_layernorm", &embed_layernorm_cpu);
+  m.impl("segment_mean", &segment_mean_cpu);
   register_attention_cpu(m);
 }
 void register_encoder_hip(torch::Library& m) {
   m.impl("add_layernorm", &add_layernorm_hip);
+  m.impl("embed_layernorm", &embed_layernorm_hip);
+  m.impl("segment_mean", &segment_mean_hip);
   register_attention_hip(m);
 }
 

@@ -83,6 +83,118 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(const uint16_t* __re
 
 using namespace svoc;
 
+namespace svoc {
+
+// embed_layernorm: out[t] = LayerNorm(tok[ids[t]] + pos[pos_ids[t]] + typ) * w + b (RoBERTa embeddings,
+// client/oracle_scheduler.py's classifier input), bf16 in/out.  The two adds round to bf16 as the
+// PyTorch expression they replace (bf16 tensors), the LayerNorm is fp32; one wave per token row as
+// add_layernorm.  Replaces an embedding gather, two elementwise adds and a LayerNorm (four passes).
+template <int EPL>
+__global__ __launch_bounds__(256) void embed_layernorm_kernel(const int64_t* __restrict__ ids,
+                                                              const int64_t* __restrict__ pos_ids,
+                                                              const uint16_t* __restrict__ tok,
+                                                              const uint16_t* __restrict__ pos,
+                                                              const uint16_t* __restrict__ typ,
+                                                              const uint16_t* __restrict__ w,
+                                                              const uint16_t* __restrict__ bias,
+                                                              uint16_t* __restrict__ out, int64_t rows, float eps) {
+  constexpr int H = 64 * EPL;
+  constexpr int V = EPL / 4;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const uint2* tr = (const uint2*)(tok + ids[row] * H);
+  const uint2* pr = (const uint2*)(pos + pos_ids[row] * H);
+  const uint2* yr = (const uint2*)typ;
+  float v[EPL];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int c = k * 64 + lane;
+    const uint2 a = tr[c], b = pr[c], t = yr[c];
+    const uint32_t aw[2] = {a.x, a.y}, bw[2] = {b.x, b.y}, tw[2] = {t.x, t.y};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int sh = 16 * h;
+        const float ab = bf2f(f2bf(bf2f((aw[j] >> sh) & 0xffffu) + bf2f((bw[j] >> sh) & 0xffffu)));
+        const float e = bf2f(f2bf(ab + bf2f((tw[j] >> sh) & 0xffffu)));
+        v[4 * k + 2 * j + h] = e;
+        s += e;
+      }
+    }
+  }
+  const float mean = wave_sum(s) * (1.f / H);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const float d = v[i] - mean;
+    q += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(q) * (1.f / H) + eps);
+  uint2* orow = (uint2*)(out + row * H);
+  const uint2* wr = (const uint2*)w;
+  const uint2* br = (const uint2*)bias;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int c = k * 64 + lane;
+    const uint2 gw = wr[c], gb = br[c];
+    const uint32_t ww[2] = {gw.x, gw.y}, bb[2] = {gb.x, gb.y};
+    uint32_t o[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const float lo = (v[4 * k + 2 * j] - mean) * rstd * bf2f(ww[j] & 0xffffu) + bf2f(bb[j] & 0xffffu);
+      const float hi = (v[4 * k + 2 * j + 1] - mean) * rstd * bf2f(ww[j] >> 16) + bf2f(bb[j] >> 16);
+      o[j] = (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+    }
+    orow[c] = make_uint2(o[0], o[1]);
+  }
+}
+
+// segment_mean: out[b] = mean of x[t] over t in [cu[b], cu[b+1]) (the masked mean pooling of the
+// classification head over the real tokens), fp32 sums in token order, bf16 out (empty segment: 0).
+// One workgroup per segment: thread (g, c) sums 8 columns (one 16-B load per row) of rows g, g + G, ...;
+// the G partial sums meet in LDS.  Replaces a scatter into the padded grid, an fp32 copy and a sum.
+__global__ __launch_bounds__(256) void segment_mean_kernel(const uint16_t* __restrict__ x, const int* __restrict__ cu,
+                                                           uint16_t* __restrict__ out, int H, int G) {
+  __shared__ float part[256 * 8];
+  const int b = blockIdx.x, chunks = H / 8;
+  const int tid = threadIdx.x, g = tid / chunks, c = tid % chunks;
+  const int lo = cu[b], hi = cu[b + 1];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (g < G) {
+    for (int t = lo + g; t < hi; t += G) {
+      const uint4 w = *(const uint4*)(x + (int64_t)t * H + 8 * c);
+      const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] += bf2f(ws[j] & 0xffffu);
+        acc[2 * j + 1] += bf2f(ws[j] >> 16);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) part[tid * 8 + j] = acc[j];
+  }
+  __syncthreads();
+  if (g == 0) {
+    const float inv = 1.f / (float)(hi - lo > 1 ? hi - lo : 1);
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float a0 = 0.f, a1 = 0.f;
+      for (int gg = 0; gg < G; ++gg) {
+        a0 += part[(gg * chunks + c) * 8 + 2 * j];
+        a1 += part[(gg * chunks + c) * 8 + 2 * j + 1];
+      }
+      o[j] = (uint32_t)f2bf(a0 * inv) | ((uint32_t)f2bf(a1 * inv) << 16);
+    }
+    *(uint4*)(out + (int64_t)b * H + 8 * c) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+}  // namespace svoc
+
 // Returns 0 on success, -1 if the hidden size is not supported (caller falls back to ATen).
 extern "C" int svoc_add_layernorm_bf16(const void* x, const void* y, const void* w, const void* b, void* out,
                                        int64_t rows, int H, float eps, hipStream_t stream) {
@@ -281,5 +393,37 @@ extern "C" int svoc_attention_short_bf16(const void* qkv, const void* kmask, con
     case 3: hipLaunchKernelGGL(attn_short_kernel<3>, grid, dim3(192), 0, stream, Q, M, cu_seqlens, R, O, H, scale_log2); break;
     default: hipLaunchKernelGGL(attn_short_kernel<4>, grid, dim3(256), 0, stream, Q, M, cu_seqlens, R, O, H, scale_log2); break;
   }
+  return (int)hipGetLastError();
+}
+
+extern "C" int svoc_embed_layernorm_bf16(const int64_t* ids, const int64_t* pos_ids, const void* tok, const void* pos,
+                                         const void* typ, const void* w, const void* b, void* out, int64_t rows, int H,
+                                         float eps, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  const auto* T = (const uint16_t*)tok;
+  const auto* P = (const uint16_t*)pos;
+  const auto* Y = (const uint16_t*)typ;
+  const auto* W = (const uint16_t*)w;
+  const auto* B = (const uint16_t*)b;
+  auto* O = (uint16_t*)out;
+  switch (H) {
+    case 256: hipLaunchKernelGGL(embed_layernorm_kernel<4>, grid, block, 0, stream, ids, pos_ids, T, P, Y, W, B, O, rows, eps); break;
+    case 512: hipLaunchKernelGGL(embed_layernorm_kernel<8>, grid, block, 0, stream, ids, pos_ids, T, P, Y, W, B, O, rows, eps); break;
+    case 768: hipLaunchKernelGGL(embed_layernorm_kernel<12>, grid, block, 0, stream, ids, pos_ids, T, P, Y, W, B, O, rows, eps); break;
+    case 1024: hipLaunchKernelGGL(embed_layernorm_kernel<16>, grid, block, 0, stream, ids, pos_ids, T, P, Y, W, B, O, rows, eps); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int svoc_segment_mean_bf16(const void* x, const int* cu, void* out, int64_t B, int H, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (H % 8 != 0 || H / 8 > 256 || B > 0x7fffffffll) return -1;
+  const int chunks = H / 8;
+  int G = 256 / chunks;
+  if (G > 8) G = 8;
+  hipLaunchKernelGGL(segment_mean_kernel, dim3((unsigned)B), dim3(chunks * G), 0, stream, (const uint16_t*)x, cu,
+                     (uint16_t*)out, H, G);
   return (int)hipGetLastError();
 }

@@ -160,15 +160,17 @@ class SentimentEncoder(nn.Module):
         return plan
 
     def _forward_packed(self, ids: torch.Tensor, p: PackPlan) -> torch.Tensor:
-        x = self.ln(self.tok(ids.reshape(-1)[p.idx]) + self.pos(p.pos) + self.typ.weight[0])   # [T, H]
+        from .. import ops as svops
+        o = svops.ops()
+        # embeddings + LayerNorm in one HIP kernel (gather, two adds, LN), [T, H]
+        x = o.embed_layernorm(ids.reshape(-1)[p.idx], p.pos, self.tok.weight, self.pos.weight, self.typ.weight,
+                              self.ln.weight, self.ln.bias, self.ln.eps)
         for layer in self.layers:
             x = layer.forward_packed(x, p)
         if self.cfg.pool == "cls":
             pooled = x[p.cu[:-1].long()]
-        else:   # masked mean: scatter back to the padded grid (unique indices: deterministic) and sum
-            xp = torch.zeros(p.B * p.S, x.shape[1], dtype=torch.float32, device=x.device)
-            xp[p.idx] = x.float()
-            pooled = (xp.view(p.B, p.S, -1).sum(1) / p.lens[:, None]).to(x.dtype)
+        else:   # masked mean over each sequence's real tokens (fp32 sums, one HIP kernel)
+            pooled = o.segment_mean(x, p.cu)
         h = torch.tanh(self.dense(pooled))
         return torch.sigmoid(self.head(h).float())
 

@@ -98,3 +98,38 @@ def test_encoder_packed_equals_padded():
         enc.packed = False
         b = enc(ids, mask)
     torch.testing.assert_close(a, b, rtol=0, atol=0.03)
+
+
+@pytest.mark.parametrize("H", [768, 256])
+def test_embed_layernorm_bf16(H):
+    """Fused embedding gather + adds + LayerNorm vs the same PyTorch expression (bf16 adds, fp32 LN)."""
+    V, P, T = 300, 130, 1000
+    g = torch.Generator(device="cuda").manual_seed(H)
+    tok = (0.02 * torch.randn(V, H, device="cuda", generator=g)).to(torch.bfloat16)
+    pos = (0.02 * torch.randn(P, H, device="cuda", generator=g)).to(torch.bfloat16)
+    typ = (0.02 * torch.randn(1, H, device="cuda", generator=g)).to(torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, device="cuda", generator=g)).to(torch.bfloat16)
+    b = (0.1 * torch.randn(H, device="cuda", generator=g)).to(torch.bfloat16)
+    ids = torch.randint(0, V, (T,), device="cuda", generator=g)
+    pid = torch.randint(0, P, (T,), device="cuda", generator=g)
+    out = svops.ops().embed_layernorm(ids, pid, tok, pos, typ, w, b, 1e-5)
+    e = (tok[ids] + pos[pid] + typ[0]).float()
+    ref = F.layer_norm(e, (H,), w.float(), b.float(), 1e-5)
+    torch.testing.assert_close(out.float(), ref, rtol=2e-2, atol=2e-2)
+    cpu = svops.ops().embed_layernorm(ids.cpu(), pid.cpu(), tok.cpu(), pos.cpu(), typ.cpu(), w.cpu(), b.cpu(), 1e-5)
+    torch.testing.assert_close(out.cpu().float(), cpu.float(), rtol=2e-2, atol=2e-2)
+
+
+def test_segment_mean_bf16():
+    """Masked mean pooling over packed segments (empty and 1-token segments included) vs fp32."""
+    lens = [5, 0, 1, 128, 77, 3]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device="cuda")
+    T, H = int(cu[-1]), 768
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randn(T, H, device="cuda", generator=g).to(torch.bfloat16)
+    out = svops.ops().segment_mean(x, cu)
+    ref = torch.stack([x[int(cu[i]):int(cu[i + 1])].float().sum(0) / max(lens[i], 1) for i in range(len(lens))])
+    torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2)
+    assert torch.equal(out[1].float(), torch.zeros(H, device="cuda"))
+    cpu = svops.ops().segment_mean(x.cpu(), cu.cpu())
+    torch.testing.assert_close(out.cpu().float(), cpu.float(), rtol=1e-2, atol=1e-2)
