@@ -239,7 +239,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 
 template <int NQB>  // S_max / 32: query blocks = waves = key blocks
-__global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __restrict__ qkv,
+__global__ __launch_bounds__(64 * NQB) __attribute__((amdgpu_waves_per_eu(4))) void attn_short_kernel(const uint16_t* __restrict__ qkv,
                                                              const uint8_t* __restrict__ kmask,
                                                              const int* __restrict__ cu_seqlens,
                                                              int64_t rows_total, uint16_t* __restrict__ out,
@@ -265,18 +265,20 @@ __global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __
   const uint16_t* Kb = Qb + H * DH;
   const uint16_t* Vb = Qb + 2 * H * DH;
 
-  // stage K and V once per workgroup (row-major, swizzled; every query wave reads them from LDS)
-  for (int c = tid; c < nkb * 32 * (DH / 8); c += 64 * NQB) {
-    const int key = c >> 3, ch = c & 7;
-    const int off = 128 * key + 16 * (ch ^ (((key >> 1) & 1) << 2));
-    const int64_t g = row(key) * ts + ch * 8;
-    const uint4 kv = *(const uint4*)(Kb + g), vv = *(const uint4*)(Vb + g);
-    *(uint4*)((unsigned char*)Ks + off) = kv;
-    *(uint4*)((unsigned char*)Vs + off) = vv;
+  // stage K and V once per workgroup (row-major, swizzled; every query wave reads them from LDS).
+  // Fixed trip count (S * 8 chunks over 64 * NQB threads = 4 per thread), all loads -- K, V and this
+  // wave's Q fragments -- issued before the first LDS store: one memory round trip per workgroup.
+  constexpr int ITER = S * (DH / 8) / (64 * NQB);
+  const int nchunks = nkb * 32 * (DH / 8);
+  uint4 kv[ITER], vv[ITER];
+#pragma unroll
+  for (int it = 0; it < ITER; ++it) {
+    int c = tid + it * 64 * NQB;
+    c = c < nchunks ? c : tid;   // past the sequence: re-read the thread's first chunk (cache hit), unused
+    const int64_t g = row(c >> 3) * ts + (c & 7) * 8;
+    kv[it] = *(const uint4*)(Kb + g);
+    vv[it] = *(const uint4*)(Vb + g);
   }
-  for (int k = tid; k < S; k += 64 * NQB)
-    km[k] = cu_seqlens ? (uint8_t)(k < L) : (kmask ? kmask[(int64_t)b * S + k] : (uint8_t)1);
-
   // X = K·Qᵀ for this wave's 32 queries: rows = keys (registers), column = query (lane)
   const int q0 = wave * 32;
   const bool active = q0 < L;
@@ -285,6 +287,18 @@ __global__ __launch_bounds__(64 * NQB) void attn_short_kernel(const uint16_t* __
 #pragma unroll
     for (int ds = 0; ds < 4; ++ds) qf[ds] = *(const bf16x8*)(Qb + row(q0 + r) * ts + ds * 16 + 8 * hh);
   }
+#pragma unroll
+  for (int it = 0; it < ITER; ++it) {
+    const int c = tid + it * 64 * NQB;
+    if (c < nchunks) {
+      const int key = c >> 3, ch = c & 7;
+      const int off = 128 * key + 16 * (ch ^ (((key >> 1) & 1) << 2));
+      *(uint4*)((unsigned char*)Ks + off) = kv[it];
+      *(uint4*)((unsigned char*)Vs + off) = vv[it];
+    }
+  }
+  for (int k = tid; k < S; k += 64 * NQB)
+    km[k] = cu_seqlens ? (uint8_t)(k < L) : (kmask ? kmask[(int64_t)b * S + k] : (uint8_t)1);
   __syncthreads();  // K, V and km staged
   if (!active) return;
   f32x16 x[NQB];
