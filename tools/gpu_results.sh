@@ -27,7 +27,7 @@ run c5_exact 300 --config-file configs/c5_exact_rounds.yaml --steps 20 --warmup 
 run c3_exact 300 --config-file configs/c3_exact_rounds.yaml --steps 10 --warmup 2 &&
 run wide512 300 --config-file configs/wide512.yaml --steps 10 --warmup 2 &&
 run c1 300 --config c1 --steps 50 --warmup 3 || exit 1
-for cfg in c3 c2; do
+for cfg in c3 c2 c4; do
   echo "=== rocprof $cfg ($(date +%T))"
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
       -d $R/gpurun_out/prof_$cfg -o run -- python3 $R/bench.py --config $cfg --steps 6 --warmup 1 --graph 0 \
