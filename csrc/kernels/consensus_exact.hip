@@ -378,7 +378,7 @@ static int exact_round_i128(const ExactParams* p, hipStream_t stream) {
 extern "C" int svoc_exact_round(const ExactParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
   if (p->N < 1 || p->N > 1024 || p->D < 1) return -1;
-  if (p->stage && p->fallback && p->mode == 0) {
+  if (p->stage && p->fallback) {
     const int rc = svoc_exact_round_wsad(p, stream);
     if (rc != -2) {
       if (rc != 0 || p->skip_fallback) return rc;

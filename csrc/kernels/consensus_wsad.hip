@@ -82,7 +82,10 @@ SVOC_DEV T group_sum(T v) {
   return v;
 }
 
-template <int NSEG, int WAVES, bool V32>
+// MODE (launch.hpp ExactParams::mode): 0 whole round; 1 D-sharded first half (c1 + qr partials out);
+// 2 D-sharded second half (c1 and the all-reduced qr in).  Instances it cannot take in mode 1 / 2 go
+// to the i128 kernel's same mode through p.fallback, as in mode 0.
+template <int NSEG, int WAVES, bool V32, int MODE>
 __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams p) {
   constexpr int P = 64 / NSEG;      // columns per wave
   constexpr int NPAD = 64 * NSEG;   // padded oracle rows
@@ -98,7 +101,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (p.active && !p.active[b]) {
+  if ((p.active && !p.active[b]) || (MODE == 2 && p.status[b] != ST_OK)) {   // mode 2: a shard failed
     if (tid == 0) p.fallback[b] = 0;
     return;
   }
@@ -124,7 +127,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
 
   // ------------------------------------------------------------ pass 1 (contract.cairo:455-463)
 #pragma nounroll
-  for (int s = 0; s < nslab; ++s) {
+  for (int s = 0; s < (MODE == 2 ? 0 : nslab); ++s) {
     const int col = s * W + wave * P + cw;
     const bool vc = col < D;
     const int vo = seg_off + (vc ? col : 0) * ESZ;
@@ -165,11 +168,31 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   __syncthreads();
   for (int t = tid; t < NPAD; t += NT) {
     uint64_t v = 0;
+    if (MODE == 2) {   // the all-reduced qr (int64; a negative total cannot come from this domain)
+      const int64_t q = t < N ? p.qr[(int64_t)b * N + t] : 0;
+      if (q < 0) flag = 1;
+      v = (uint64_t)q;
+    } else {
 #pragma unroll
-    for (int w = 0; w < WAVES; ++w) v += qr_part[w * NPAD + t];
+      for (int w = 0; w < WAVES; ++w) v += qr_part[w * NPAD + t];
+    }
     qr_lds[t] = v;
   }
+  if (MODE == 1 && badv) flag = 1;
   __syncthreads();
+  if (MODE == 1) {   // first half done: c1 and the qr partials out (partials < 2^58: D <= 2^38 columns)
+    if (flag) {
+      if (tid == 0) p.fallback[b] = 1;
+      return;
+    }
+    for (int c = tid; c < D; c += NT) p.c1[(int64_t)b * D + c] = stg[c];
+    for (int t = tid; t < N; t += NT) p.qr[(int64_t)b * N + t] = (int64_t)qr_lds[t];
+    if (tid == 0) {
+      p.status[b] = ST_OK;
+      p.fallback[b] = 0;
+    }
+    return;
+  }
 
   // ------------------------------------------------------------ rank mask (contract.cairo:345-363)
   const int f = p.n_failing;
@@ -199,12 +222,13 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       s_all = add(s_all, qv, st);
       if ((relmask[t >> 6] >> (t & 63)) & 1) s_rel = add(s_rel, qv, st);
     }
-    const i128 rel1 = constrained_reliability(idiv(s_all, (i128)N, st), D, st);
+    const int64_t rd = p.rel_dim > 0 ? p.rel_dim : D;   // D-sharded: the global dimension
+    const i128 rel1 = constrained_reliability(idiv(s_all, (i128)N, st), rd, st);
     if (!in_unit_interval(rel1)) st = ST_RELIABILITY_INTERVAL;
     if (f < 0 || R < 4) st = ST_TOO_FEW_RELIABLE;
     i128 rel2 = 0;
     if (st == ST_OK) {
-      rel2 = constrained_reliability(idiv(s_rel, (i128)R, st), D, st);
+      rel2 = constrained_reliability(idiv(s_rel, (i128)R, st), rd, st);
       if (!in_unit_interval(rel2)) st = ST_RELIABILITY_INTERVAL;
     }
     rels[0] = (int64_t)rel1;
@@ -248,7 +272,9 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       uint32_t r[64];
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
-        const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
+        uint32_t hw;
+        const uint32_t x = wload<V32>(rs, vo, i * rowb, hw);
+        if (MODE == 2) badv |= (vc && i < nv && (x > kWsadMax || hw != 0)) ? 1u : 0u;   // no pass 1 here
         const uint32_t mk = bit_mask(mm, i), low = bit_mask(ml, i);
         r[i] = ((x & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else -inf (low) / +inf
       }
@@ -305,7 +331,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       stg[3 * D + col] = (int32_t)ku;
     }
   }
-  if (bad) flag = 1;
+  if (bad || (MODE == 2 && badv)) flag = 1;
   __syncthreads();
   if (flag) {
     if (tid == 0) p.fallback[b] = 1;
@@ -315,7 +341,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   // ------------------------------------------------------------ commit (a successful round)
   const int64_t ob = (int64_t)b * D;
   for (int c = tid; c < D; c += NT) {
-    if (p.c1) p.c1[ob + c] = stg[c];
+    if (MODE == 0 && p.c1) p.c1[ob + c] = stg[c];   // (mode 2: c1 is the input, unchanged)
     p.consensus[ob + c] = stg[D + c];
     p.skew[ob + c] = stg[2 * D + c];
     p.kurt[ob + c] = stg[3 * D + c];
@@ -335,7 +361,9 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
 template <int NSEG>
 static int launch_wsad(const ExactParams& p, hipStream_t stream) {
   constexpr int WAVES = 4;
-  auto k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true> : consensus_wsad_kernel<NSEG, WAVES, false>;
+  auto k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 0> : consensus_wsad_kernel<NSEG, WAVES, false, 0>;
+  if (p.mode == 1) k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 1> : consensus_wsad_kernel<NSEG, WAVES, false, 1>;
+  if (p.mode == 2) k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 2> : consensus_wsad_kernel<NSEG, WAVES, false, 2>;
   hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   return (int)hipGetLastError();
 }

@@ -181,15 +181,36 @@ def test_fast_bf16_agrees_with_exact_on_shared_grid(N, D, f):
     assert rel.max().item() <= 32.0, rel.max()
 
 
+@pytest.mark.parametrize("path", ["dispatch", "i128", "wsad_only"])
 @pytest.mark.parametrize("N,D,f", [(16, 24, 3), (64, 300, 8), (256, 70, 32)])
-def test_exact_split_modes_match_whole_round(N, D, f):
-    """The i128 kernel's D-sharded halves (mode 1: c1 + qr partials; mode 2: from the summed qr), run on
-    two column slices on one GPU with the all-reduce done by hand, reproduce the whole round bit for bit."""
+def test_exact_split_modes_match_whole_round(N, D, f, path):
+    """The exact kernels' D-sharded halves (mode 1: c1 + qr partials; mode 2: from the summed qr), run on
+    two column slices on one GPU with the all-reduce done by hand, reproduce the whole round bit for bit:
+    through the dispatcher (column-parallel kernel + i128 fallback), the i128 kernel alone, and the
+    column-parallel kernel alone (which must then take every round: clean data)."""
     B = 8
     v = _wsad(B, N, D, f, seed=N + 7 * D)
-    v[2, :, D // 4] = 123_456           # zero variance in slice 0 only: instance 2 reverts
+    if path != "wsad_only":
+        v[2, :, D // 4] = 123_456       # zero variance in slice 0 only: instance 2 reverts
     vg = v.to(DEV)
     whole = _run(vg, f)
+    env = {"dispatch": {"SVOC_EXACT_WSAD_MIN_D": "1"}, "i128": {"SVOC_EXACT_I128": "1"},
+           "wsad_only": {"SVOC_EXACT_WSAD_ONLY": "1", "SVOC_EXACT_WSAD_MIN_D": "1"}}[path]
+    old_env = {k: os.environ.get(k) for k in ("SVOC_EXACT_I128", "SVOC_EXACT_WSAD_ONLY", "SVOC_EXACT_WSAD_MIN_D")}
+    for k in old_env:
+        os.environ.pop(k, None)
+    os.environ.update(env)
+    try:
+        _split_rounds(vg, whole, N, D, f, B, expect_revert=path != "wsad_only")
+    finally:
+        for k, val in old_env.items():
+            if val is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = val
+
+
+def _split_rounds(vg, whole, N, D, f, B, expect_revert):
     cut = D // 2
     parts = [vg[:, :, :cut].contiguous(), vg[:, :, cut:].contiguous()]
     outs = [alloc_exact_out(B, N, x.shape[2], DEV) for x in parts]
@@ -206,7 +227,8 @@ def test_exact_split_modes_match_whole_round(N, D, f):
            o["status"], False, 2, D)
     st = torch.maximum(outs[0]["status"], outs[1]["status"]).cpu()
     torch.cuda.synchronize()
-    assert torch.equal(st, whole["status"]) and st[2].item() != 0 and (st != 0).sum().item() == 1
+    assert torch.equal(st, whole["status"])
+    assert (st != 0).sum().item() == (1 if expect_revert else 0) and (not expect_revert or st[2].item() != 0)
     ok = st == 0
     for o in outs:
         for k in ("rel", "qr", "reliable"):
