@@ -149,16 +149,20 @@ __global__ __launch_bounds__(256) void consensus_fast_small_kernel(FastParams p)
     relbits |= rel ? (1u << i) : 0u;
     s_rel += rel ? qr[i] : 0.f;
   }
+  // divisors are launch-uniform: one reciprocal each instead of a full-precision division per use
+  // (the divisions were ~20% of this kernel's VALU instructions; profiles/r2_pmc_c5.md)
   const float rd = p.legacy ? 1.f : (float)(p.rel_dim > 0 ? p.rel_dim : D);
+  const float inv_nrd = 1.f / ((float)N * rd), inv_rrd = 1.f / ((float)R * rd);
+  const float inv_ms = 1.f / p.max_spread;
   int st = ST_OK;
   float rel1, rel2 = 0.f;
-  if (CONS) rel1 = 1.f - 2.f * sqrtf(s_all / (float)N / rd);
-  else rel1 = 1.f - fminf(p.max_spread, sqrtf(s_all / (float)N)) / p.max_spread;
+  if (CONS) rel1 = 1.f - 2.f * sqrtf(s_all * inv_nrd);
+  else rel1 = 1.f - fminf(p.max_spread, sqrtf(s_all * (1.f / (float)N))) * inv_ms;
   if (!(rel1 >= 0.f && rel1 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
   else if (R < 2) st = R <= 0 ? ST_USIZE_UNDERFLOW : ST_INDEX_OOB;
   else {
-    if (CONS) rel2 = 1.f - 2.f * sqrtf(s_rel / (float)R / rd);
-    else rel2 = 1.f - fminf(p.max_spread, sqrtf(s_rel / (float)R)) / p.max_spread;
+    if (CONS) rel2 = 1.f - 2.f * sqrtf(s_rel * inv_rrd);
+    else rel2 = 1.f - fminf(p.max_spread, sqrtf(s_rel * (1.f / (float)R))) * inv_ms;
     if (!(rel2 >= 0.f && rel2 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
     else if (R < 4 && !p.legacy) st = ST_TOO_FEW_RELIABLE;
   }
@@ -205,9 +209,9 @@ __global__ __launch_bounds__(256) void consensus_fast_small_kernel(FastParams p)
     medB = 0.5f * (bf16_hi(lo) + bf16_hi(hi));
   }
   // ---- moments (math.cairo:208-222, 320-398) from the shifted power sums
-  const float n = (float)R;
+  const float n = (float)R, inv_n = 1.f / n;
   const float k3 = n / ((n - 1.f) * (n - 2.f));
-  const float k4a = n * (n + 1.f) / (n - 1.f), k4b = 3.f * (n - 1.f) * (n - 1.f), k4c = (n - 2.f) * (n - 3.f);
+  const float k4a = n * (n + 1.f) / (n - 1.f), k4b = 3.f * (n - 1.f) * (n - 1.f), ik4c = 1.f / ((n - 2.f) * (n - 3.f));
   int zv = 0;
   float cons_o[2], sk_o[2], ku_o[2];
 #pragma unroll
@@ -215,16 +219,16 @@ __global__ __launch_bounds__(256) void consensus_fast_small_kernel(FastParams p)
     const bool v = h ? vB : vA;
     const float a1 = h ? s1.y : s1.x, a2 = h ? s2.y : s2.x, a3 = h ? s3.y : s3.x, a4 = h ? s4.y : s4.x;
     const float shh = h ? sh.y : sh.x, med = h ? medB : medA;
-    const float dl = a1 / n, e2 = a2 / n, e3 = a3 / n, e4 = a4 / n;
+    const float dl = a1 * inv_n, e2 = a2 * inv_n, e3 = a3 * inv_n, e4 = a4 * inv_n;
     const float mu2 = e2 - dl * dl;
     const float mu3 = e3 - 3.f * dl * e2 + 2.f * dl * dl * dl;
     const float mu4 = e4 - 4.f * dl * e3 + 6.f * dl * dl * e2 - 3.f * dl * dl * dl * dl;
     float sk = 0.f, ku = 0.f;
     if (mu2 > 0.f) {
       const float sd = sqrtf(mu2);
-      const float z3 = n * mu3 / (mu2 * sd), z4 = n * mu4 / (mu2 * mu2);
+      const float z3 = n * mu3 * __builtin_amdgcn_rcpf(mu2 * sd), z4 = n * mu4 * __builtin_amdgcn_rcpf(mu2 * mu2);
       sk = z3 * k3;
-      ku = (z4 * k4a - k4b) / k4c;
+      ku = (z4 * k4a - k4b) * ik4c;
     } else if (v) {
       zv = 1;
     }
