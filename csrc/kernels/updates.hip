@@ -174,6 +174,30 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
       const int64_t i = sub + (int64_t)k * L;
       if (i < nch) ((uint4*)dst)[i] = v[k];
     }
+  } else if (L == 1 && p.dtype == 0 && (row_bytes & 3) == 0 && row_bytes <= 16 && (((uintptr_t)p.upd) & 3) == 0 &&
+             (((uintptr_t)p.values) & 3) == 0 && (p.inst_stride & 1) == 0 && (p.ld & 1) == 0) {
+    // short bf16 rows (the deployed 7 x 6: 12 B): the row's words are loaded with the instance / oracle
+    // indices (their addresses do not depend on them), validated and stored from registers -- one
+    // memory round trip before the stores instead of three (profiles/r2_pmc_c5.md)
+    const int nw = (int)(row_bytes >> 2);
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = (in && k < nw) ? ((const uint32_t*)src)[k] : 0u;
+    bool ok = true, fin = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k >= nw) continue;
+      if (p.constrained) ok = ok && bf16_unit(w[k] & 0xffffu) && bf16_unit(w[k] >> 16);
+      else fin = fin && ((w[k] & 0x7f80u) != 0x7f80u) && ((w[k] & 0x7f800000u) != 0x7f800000u);
+    }
+    if (!in) return;
+    if (st == ST_OK && !ok) st = ST_INTERVAL_INPUT;
+    if (st == ST_OK && !fin) st = ST_NON_FINITE;
+    p.upd_status[u] = st;
+    if (st != ST_OK) return;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < nw) ((uint32_t*)dst)[k] = w[k];
   } else {
     bool ok = true, fin = true;
     if (in && st == ST_OK) {

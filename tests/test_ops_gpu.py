@@ -238,3 +238,32 @@ def test_unique_update_path_matches_general(D, constrained):
         outs.append((st.cpu(), e.values.cpu(), e.enabled.cpu(), e.n_active.cpu(), e.touched.cpu()))
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("constrained", [True, False])
+def test_apply_updates_unique_short_rows(constrained):
+    """The unique-update kernel's short-row path (7 x 6 bf16 rows, 12 B): distinct (instance, oracle)
+    pairs, an out-of-range oracle, an interval / non-finite value; equal to the CPU loop."""
+    B, N, D, ld = 40, 7, 6, 8
+    g = torch.Generator().manual_seed(5)
+    pairs = torch.randperm(B * N, generator=g)[:150]
+    inst, orc = pairs // N, pairs % N
+    orc[7] = N + 3                      # not an oracle
+    upd = torch.rand(150, D, generator=g).to(torch.bfloat16)
+    upd[11, 3] = 1.5 if constrained else float("nan")
+    res = []
+    for dev in ("cpu", DEV):
+        vals = torch.zeros(B, N, ld, dtype=torch.bfloat16, device=dev)
+        en = torch.zeros(B, N, dtype=torch.uint8, device=dev)
+        en[3] = 1                       # some oracles already enabled
+        na = en.sum(1, dtype=torch.int32)
+        tch = torch.zeros(B, dtype=torch.uint8, device=dev)
+        win = torch.full((B, N), -1, dtype=torch.int32, device=dev)
+        st = torch.empty(150, dtype=torch.int32, device=dev)
+        svops.ops().apply_updates(vals, en, na, tch, win, inst.to(dev), orc.to(dev), upd.to(dev), constrained, st,
+                                  True)
+        res.append([t.cpu() for t in (vals, en, na, tch, st)])
+    for a, b in zip(*res):
+        assert torch.equal(a.view(torch.uint8) if a.dtype == torch.bfloat16 else a,
+                           b.view(torch.uint8) if b.dtype == torch.bfloat16 else b)
+    assert res[1][4][7].item() != 0 and res[1][4][11].item() != 0
