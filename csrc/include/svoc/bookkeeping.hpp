@@ -31,9 +31,10 @@ SVOC_HD uint8_t book_active(const RoundBook& r, int64_t b) {
   return (r.n_active[b] == r.N && (!r.only_touched || r.touched[b])) ? 1 : 0;
 }
 
+// committed = ran and succeeded; every other status (fast-mode ZERO_VARIANCE included) reverted the
+// round, which leaves consensus_active as it was (contract.cairo:588-603: the whole tx reverts)
 SVOC_HD bool book_ok(const RoundBook& r, int64_t b) {
-  const int st = r.status[b];
-  return r.active[b] && (st == ST_OK || (r.fast && st == ST_ZERO_VARIANCE));
+  return r.active[b] && r.status[b] == ST_OK;
 }
 
 SVOC_HD unsigned long long book_rel2_fx(const RoundBook& r, int64_t b) {
