@@ -76,7 +76,7 @@ def main():
                          "-1 = the config's default")
     ap.add_argument("--mode", default=None, choices=["fast", "exact"],
                     help="override the config's engine mode (exact = bit-exact wsad int64 path)")
-    ap.add_argument("--storage", default=None, choices=["bf16", "int64", "int32"],
+    ap.add_argument("--storage", default=None, choices=["bf16", "fp32", "int64", "int32"],
                     help="engine value storage (exact mode: int64 default, int32 for constrained configs)")
     ap.add_argument("--dshard", action="store_true",
                     help="strong scaling: every rank holds a column slice of ALL instances (D-sharding, one "
@@ -267,7 +267,7 @@ def main():
             "metric": METRIC, "value": value, "unit": "consensus rounds/s", "n_gpus": world,
             "steps": steps_done, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "strong" if dshard else "weak", "vs_baseline": None,
-            "dtype": f"{eng.storage}-wsad" if mode == "exact" else c.get("dtype", "bf16"), "data": "synthetic",
+            "dtype": f"{eng.storage}-wsad" if mode == "exact" else ("fp32-storage" if eng.storage == "fp32" else c.get("dtype", "bf16")), "data": "synthetic",
             "config": {"model": c["model"], "global_batch": B * (1 if dshard else world), "seq_len": c["D"],
                        "parallelism": f"dshard{world}" if dshard else f"dp{world}", "engine_mode": mode, "n_oracles": c["N"], "dimension": c["D"],
                        "n_failing": c["f"], "updates_per_instance_per_step": U_per_inst,
@@ -276,7 +276,7 @@ def main():
         }
         if args.config in ("c2", "c3"):
             from svoc.utils.metrics import algorithmic_bytes_per_round
-            out["config"]["hbm_gbps_algorithmic"] = algorithmic_bytes_per_round(c["N"], c["D"]) * rounds / el / 1e9
+            out["config"]["hbm_gbps_algorithmic"] = algorithmic_bytes_per_round(c["N"], c["D"], eng.values.element_size()) * rounds / el / 1e9
         print(json.dumps(out))
         if args.log:
             from svoc.utils.metrics import JsonlLogger, engine_health, kernel_table

@@ -112,15 +112,26 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
                     at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim, bool legacy,
                     const c10::optional<at::Tensor>& work) {
   fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
-  TORCH_CHECK(values.scalar_type() == at::kBFloat16, "GPU fast path stores values in bf16");
+  TORCH_CHECK(values.scalar_type() == at::kBFloat16 || values.scalar_type() == at::kFloat,
+              "GPU fast path stores values in bf16 or fp32");
+  const bool f32 = values.scalar_type() == at::kFloat;
   const int64_t B = values.size(0), N = values.size(1), ld = values.size(2);
-  TORCH_CHECK(N >= 2 && N <= 1024, "GPU fast path supports 2 <= N <= 1024 oracles");
-  TORCH_CHECK(ld % 8 == 0, "row stride (ld) must be a multiple of 8 bf16 (16 B)");
-  TORCH_CHECK(((uintptr_t)values.data_ptr() & 15) == 0 && values.stride(0) % 8 == 0, "values must be 16-B aligned");
-  TORCH_CHECK(B < (1ll << 31) && D < (1 << 30), "size limits");
-  // the kernels address one instance with 32-bit buffer offsets (rows x ld x 2 B, workspace x 4 B)
-  TORCH_CHECK(N * ld * 2 < (1ll << 31) && fast_work_words(D) * 4 < (1ll << 31),
-              "instance too large for 32-bit buffer offsets (N * ld * 2 B and the workspace must stay < 2 GiB)");
+  if (f32) {
+    // reference-resolution storage: the column-parallel fp32 kernel (consensus_fast_f32.hip)
+    TORCH_CHECK(N >= 2 && N <= 256, "GPU fp32 fast path supports 2 <= N <= 256 oracles");
+    TORCH_CHECK(B < (1ll << 31) && D < (1 << 30), "size limits");
+    TORCH_CHECK(N * ld * 4 < (1ll << 31) && fast_work_words(D) * 4 < (1ll << 31),
+                "instance too large for 32-bit buffer offsets (N * ld * 4 B and the workspace must stay < 2 GiB)");
+  }
+  if (!f32) {
+    TORCH_CHECK(N >= 2 && N <= 1024, "GPU fast path supports 2 <= N <= 1024 oracles");
+    TORCH_CHECK(ld % 8 == 0, "row stride (ld) must be a multiple of 8 bf16 (16 B)");
+    TORCH_CHECK(((uintptr_t)values.data_ptr() & 15) == 0 && values.stride(0) % 8 == 0, "values must be 16-B aligned");
+    TORCH_CHECK(B < (1ll << 31) && D < (1 << 30), "size limits");
+    // the kernels address one instance with 32-bit buffer offsets (rows x ld x 2 B, workspace x 4 B)
+    TORCH_CHECK(N * ld * 2 < (1ll << 31) && fast_work_words(D) * 4 < (1ll << 31),
+                "instance too large for 32-bit buffer offsets (N * ld * 2 B and the workspace must stay < 2 GiB)");
+  }
   FastParams p{};
   p.values = values.data_ptr();
   p.active = active_ptr(active, B, values.device());
@@ -152,7 +163,7 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
     TORCH_CHECK(work->numel() >= fast_work_numel(B, D), "work: needs ", fast_work_numel(B, D),
                 " elements (svoc.ops.fast_work_numel)");
     p.work = (uint32_t*)work->data_ptr();
-  } else if (mode != 1 && !(mode == 0 && wave_hint == 0 && N <= 16 && D <= 128)) {
+  } else if (mode != 1 && (f32 || !(mode == 0 && wave_hint == 0 && N <= 16 && D <= 128))) {
     // a temporary one: every kernel but the small-instance one stages its pass-2 outputs there
     wtmp = at::empty({fast_work_numel(B, D)}, values.options().dtype(at::kInt));
     p.work = (uint32_t*)wtmp.data_ptr();
@@ -165,6 +176,11 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
   p.work_pairs = (int)fast_work_pairs(D);
   p.work_stride = words;
   auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
+  if (f32) {
+    const int rc = svoc_fast_round_f32(&p, stream);
+    TORCH_CHECK(rc == 0, "svoc_fast_round_f32 launch failed: ", rc);
+    return;
+  }
   const int rc = svoc_fast_round_bf16(&p, stream);
   TORCH_CHECK(rc == 0, "svoc_fast_round_bf16 launch failed: ", rc);
 }

@@ -85,6 +85,7 @@ struct ExactParams {
 extern "C" {
 typedef struct ihipStream_t* hipStream_t;
 int svoc_fast_round_bf16(const svoc::FastParams* p, hipStream_t stream);
+int svoc_fast_round_f32(const svoc::FastParams* p, hipStream_t stream);   // values fp32 [B, N, ld]
 int svoc_exact_round(const svoc::ExactParams* p, hipStream_t stream);
 }
 

@@ -1,0 +1,354 @@
+// Fast-mode consensus round over fp32 STORAGE (reference resolution): one workgroup per instance,
+// one lane per column.
+//
+// Why a separate kernel: the bf16 kernels (consensus_fast_win / _reg / _small) sort two 16-bit keys
+// per VGPR (v_pk_min_u16); bf16 quantises [0, 1] values to 2^-9..2^-8, three orders of magnitude
+// coarser than the contract's 1e-6 wsad grid (signed_decimal.cairo:82-83).  fp32 keeps 24 bits
+// (<= 6e-8 absolute on [0, 1]: every wsad value keeps its own rounding interval), so this path
+// selects the same oracles as the exact engine on data the fp32 grid separates
+// (tests/test_f32_gpu.py pins fast-fp32 against the exact wsad kernel).
+//
+// Semantics: contract/src/contract.cairo:442-503 (constrained) and :370-434 (unconstrained), in the
+// fast engine's real-unit form (csrc/engine/reference_cpu.cpp:fast_round_one, its CPU twin):
+//   pass 1: c1 = smooth median per column (ranks N/2 - 1, N/2; math.cairo:113-126), qr_i =
+//           sum_d (x_id - c1_d)^2 (math.cairo:225-238), rel1 from mean(qr) (contract.cairo:436-439);
+//   rank mask (qr asc, idx desc; sort.cairo:96-101) keeps N - f rows;
+//   pass 2: consensus = smooth median (constrained) / mean (unconstrained) of the reliable rows, rel2
+//           from their qr, population variance, sample-adjusted skewness / excess kurtosis
+//           (math.cairo:320-398).
+//
+// MI355X mapping (the column-parallel layout of consensus_wsad.hip with float math):
+//   * lane = column; NSEG = ceil(N / 64) lanes share a column for N > 64 (64 rows per lane);
+//     row offsets ride in SGPR soffsets of one buffer resource per instance (no address VGPRs);
+//   * fp32 -> order-preserving u32 key (sign-magnitude flip); median_group (sortnet.hpp) finds the
+//     two middle order statistics; rows >= N (and unreliable rows in pass 2) become 0 / ~0
+//     sentinels split so the middle pair lands on the real middle ranks -- no per-row masks in the
+//     network;
+//   * qr partials: a transposing butterfly over the wave's columns (DPP / ds_swizzle / permlane32),
+//     per-oracle sums in LDS, deterministic (no atomics);
+//   * pass 2 sums the reliable rows in fp64 while loading the keys (exact for <= 2^29 fp32 terms, so
+//     equal values give a mean equal to them and a zero variance exactly as the CPU twin's), then one
+//     re-read (L2-resident) for the fp64 central moments;
+//   * outputs are staged in the workspace and committed only when the round's status is OK
+//     (contract.cairo:588-603: a failed assert reverts the whole transaction).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "svoc/bufload.hpp"
+#include "svoc/launch.hpp"
+#include "svoc/sortnet.hpp"
+#include "svoc/status.hpp"
+
+namespace svoc {
+
+// fp32 bits <-> monotone u32 key (negative values: all bits flipped; positive: sign bit set)
+SVOC_DEV uint32_t f32_key(uint32_t u) { return u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u); }
+SVOC_DEV float key_f32(uint32_t k) {
+  return __builtin_bit_cast(float, k ^ ((uint32_t)((int32_t)~k >> 31) | 0x80000000u));
+}
+
+// Transposing butterfly over the wave's P columns: stage L exchanges with lane ^ (P >> L); the lane
+// ends with rows I + base(lane) summed over all P columns.
+template <int L, int I, int P>
+SVOC_DEV float qtree_f(const float (&q)[64], int lane) {
+  if constexpr (L == 0) {
+    return q[I];
+  } else {
+    constexpr int msk = P >> L;
+    const float lo_v = qtree_f<L - 1, I, P>(q, lane);
+    const float hi_v = qtree_f<L - 1, I + (64 >> L), P>(q, lane);
+    const bool up = (lane & msk) != 0;
+    const float send = up ? lo_v : hi_v;
+    const float keep = up ? hi_v : lo_v;
+    return keep + xor_lane<msk>(send);
+  }
+}
+template <int P, int... Is>
+SVOC_DEV void qtree_f_all(const float (&q)[64], int lane, float* acc, std::integer_sequence<int, Is...>) {
+  ((acc[Is] += qtree_f<__builtin_ctz(P), Is, P>(q, lane)), ...);
+}
+
+template <int NSEG, int P, class T>
+SVOC_DEV T seg_sum(T v) {
+#pragma unroll
+  for (int t = 1; t < NSEG; t <<= 1) v += __shfl_xor(v, t * P);
+  return v;
+}
+
+// MODE: 0 whole round; 1 pass 1 only (c1 + this shard's qr partials); 2 from the all-reduced qr
+// (D-sharding, svoc/parallel/dshard.py).
+template <int NSEG, int WAVES, bool CONS, int MODE>
+__global__ __launch_bounds__(WAVES * 64) void consensus_fast_f32_kernel(FastParams p) {
+  constexpr int P = 64 / NSEG;      // columns per wave
+  constexpr int NPAD = 64 * NSEG;   // padded oracle rows
+  constexpr int W = WAVES * P;      // columns per slab
+  constexpr int NT = WAVES * 64;
+  constexpr int KEEP = 64 / P;      // qr rows a lane holds after the butterfly
+  __shared__ float qr_part[WAVES * NPAD];
+  __shared__ float qr_lds[NPAD];
+  __shared__ uint64_t relmask[4], lowmask[4];
+  __shared__ float rels[2];
+  __shared__ int st_sh, zv_sh;
+
+  const int b = blockIdx.x;
+  if (p.active && !p.active[b]) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N = p.N, D = p.D;
+  if (p.n_failing > N) {   // reference_cpu.cpp fast_round_one: checked before anything is computed
+    if (tid == 0) p.status[b] = ST_USIZE_UNDERFLOW;
+    return;
+  }
+  if (tid == 0) zv_sh = 0;
+  const int seg = lane / P, cw = lane % P;
+  const int rowb = p.ld * 4;
+  const __amdgpu_buffer_rsrc_t rs =
+      instance_rsrc((const float*)p.values + (int64_t)b * p.inst_stride, (uint32_t)(N * rowb));
+  const int nslab = (D + W - 1) / W;
+  const int lo1 = (NPAD - N + 1) >> 1;   // pass-1 sentinel split (rows >= N): low keys first, then high
+  const int nv = N - seg * 64;           // this lane's rows < nv are real
+  const int nl = N + lo1 - seg * 64;
+  const int seg_off = seg * 64 * rowb;
+  const uint32_t pol = group_polarity<NSEG>(seg);
+
+  float acc[KEEP];
+#pragma unroll
+  for (int k = 0; k < KEEP; ++k) acc[k] = 0.f;
+
+  // ------------------------------------------------------------ pass 1 (contract.cairo:455-463)
+#pragma nounroll
+  for (int s = 0; s < (MODE == 2 ? 0 : nslab); ++s) {
+    const int col = s * W + wave * P + cw;
+    const bool vc = col < D;
+    const int vo = seg_off + (vc ? col : 0) * 4;
+    float c1;
+    {
+      uint32_t r[64];
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const uint32_t x = bload(rs, vo, i * rowb);
+        r[i] = (i < nv ? f32_key(x) : (i < nl ? 0u : ~0u)) ^ pol;
+      }
+      uint32_t lo, hi;
+      median_group<NSEG>(r, lo, hi);
+      c1 = 0.5f * (key_f32(lo) + key_f32(hi));
+    }
+    if (seg == 0 && vc) p.c1[(int64_t)b * D + col] = c1;
+    __builtin_amdgcn_sched_barrier(0);
+    // quadratic risk partials of this column (math.cairo:225-238), summed over the wave's columns
+    float q[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      const float y = __builtin_bit_cast(float, bload(rs, vo, i * rowb)) - c1;
+      q[i] = (vc && i < nv) ? y * y : 0.f;   // a select: columns past D may hold anything
+    }
+    qtree_f_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
+  }
+  {
+    int base = 0;
+#pragma unroll
+    for (int h = 32, msk = P / 2; msk >= 1; h >>= 1, msk >>= 1) base += (lane & msk) ? h : 0;
+#pragma unroll
+    for (int k = 0; k < KEEP; ++k) qr_part[wave * NPAD + seg * 64 + base + k] = acc[k];
+  }
+  __syncthreads();
+  for (int t = tid; t < NPAD; t += NT) {
+    float v = 0.f;
+    if (MODE == 2) {
+      v = t < N ? p.qr[(int64_t)b * N + t] : 0.f;
+    } else {
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) v += qr_part[w * NPAD + t];
+    }
+    qr_lds[t] = v;
+  }
+  __syncthreads();
+  if (MODE == 1) {   // D-sharding, first half: this shard's qr partials out (c1 already written)
+    for (int t = tid; t < N; t += NT) p.qr[(int64_t)b * N + t] = qr_lds[t];
+    if (tid == 0) p.status[b] = ST_OK;
+    return;
+  }
+
+  // ------------------------------------------------------------ rank mask (contract.cairo:345-363)
+  const int R = N - p.n_failing;
+  for (int base = 0; base < NPAD; base += NT) {
+    const int t = base + tid;
+    bool rel = false;
+    if (t < N) {
+      const float myq = qr_lds[t];
+      int rank = 0;
+      for (int j = 0; j < N; ++j) {
+        const float qj = qr_lds[j];
+        rank += (qj < myq || (qj == myq && j > t)) ? 1 : 0;   // (qr asc, idx desc)
+      }
+      rel = rank < R;
+    }
+    const uint64_t bal = __ballot(rel);
+    if (lane == 0 && (t >> 6) < 4) relmask[t >> 6] = bal;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    // reliabilities in fp64 over the fp32 qr, in the CPU twin's order (reference_cpu.cpp:224-243)
+    double s_all = 0.0, s_rel = 0.0;
+    for (int t = 0; t < N; ++t) {
+      s_all += (double)qr_lds[t];
+      if ((relmask[t >> 6] >> (t & 63)) & 1) s_rel += (double)qr_lds[t];
+    }
+    const double rd = p.legacy ? 1.0 : (double)(p.rel_dim > 0 ? p.rel_dim : D);
+    const double ms = (double)p.max_spread;
+    auto rel_of = [&](double mean_qr) -> float {
+      return CONS ? (float)(1.0 - 2.0 * sqrt(mean_qr / rd)) : (float)(1.0 - fmin(ms, sqrt(mean_qr)) / ms);
+    };
+    int st = ST_OK;
+    const float rel1 = rel_of(s_all / (double)N);
+    float rel2 = 0.f;
+    if (!(rel1 >= 0.f && rel1 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
+    else if (R < 2) st = R == 0 ? ST_USIZE_UNDERFLOW : ST_INDEX_OOB;
+    else {
+      rel2 = rel_of(s_rel / (double)R);
+      if (!(rel2 >= 0.f && rel2 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
+      else if (R < 4 && !p.legacy) st = ST_TOO_FEW_RELIABLE;
+    }
+    rels[0] = rel1;
+    rels[1] = rel2;
+    st_sh = st;
+    // pass-2 sentinel split: the first (NPAD - R + 1) / 2 non-reliable rows (row order) sort low
+    int need = (NPAD - R + 1) >> 1;
+    for (int w = 0; w < 4; ++w) {
+      uint64_t nr = w < NSEG ? ~relmask[w] : 0ull, lm = 0ull;
+      while (need > 0 && nr) {
+        const uint64_t bit = nr & (0ull - nr);
+        lm |= bit;
+        nr ^= bit;
+        --need;
+      }
+      lowmask[w] = lm;
+    }
+  }
+  __syncthreads();
+  if (st_sh != ST_OK) {
+    if (tid == 0) p.status[b] = st_sh;
+    return;   // revert: outputs untouched
+  }
+
+  // ------------------------------------------------------------ pass 2 (contract.cairo:476-500)
+  const int Dp = p.work_pairs, D2 = 2 * Dp;
+  const int STG = Dp * (2 * 17 + 8 + 2) * 4;   // launch.hpp: fast_work_stage_word
+  const __amdgpu_buffer_rsrc_t ws = instance_rsrc(p.work + (int64_t)b * p.work_stride, (uint32_t)(p.work_stride * 4));
+  const uint64_t mymask = relmask[seg];
+  const uint64_t mylow = lowmask[seg];
+  const double n = (double)R, inv_n = 1.0 / n;
+  const double k3 = n / ((n - 1.0) * (n - 2.0));
+  const double k4a = n * (n + 1.0) / (n - 1.0), k4b = 3.0 * (n - 1.0) * (n - 1.0), k4c = (n - 2.0) * (n - 3.0);
+  bool zv = false;
+#pragma nounroll
+  for (int s = 0; s < nslab; ++s) {
+    const int col = s * W + wave * P + cw;
+    const bool vc = col < D;
+    const int vo = seg_off + (vc ? col : 0) * 4;
+    uint64_t mm = mymask, ml = mylow;
+    asm volatile("" : "+v"(mm), "+v"(ml));   // keep the 64 row masks out of the slab loop's live set
+    double sx = 0.0;
+    float med = 0.f;
+    if constexpr (CONS) {
+      uint32_t r[64];
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const uint32_t x = bload(rs, vo, i * rowb);
+        const uint32_t mk = bit_mask(mm, i), low = bit_mask(ml, i);
+        sx += (double)__builtin_bit_cast(float, x & mk);   // masked rows add +0
+        r[i] = ((f32_key(x) & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else low (0) / high (~0)
+      }
+      uint32_t lo, hi;
+      median_group<NSEG>(r, lo, hi);
+      med = 0.5f * (key_f32(lo) + key_f32(hi));
+    } else {
+#pragma unroll 16
+      for (int i = 0; i < 64; ++i)
+        sx += (double)__builtin_bit_cast(float, bload(rs, vo, i * rowb) & bit_mask(mm, i));
+    }
+    sx = seg_sum<NSEG, P>(sx);
+    const double mu = sx / n;
+    __builtin_amdgcn_sched_barrier(0);
+    // central moments about the fp64 mean (one re-read of the column, L2-resident)
+    double s2 = 0.0, s3 = 0.0, s4 = 0.0;
+#pragma unroll 16
+    for (int i = 0; i < 64; ++i) {
+      const float x = __builtin_bit_cast(float, bload(rs, vo, i * rowb));
+      const double y = bit_mask(mm, i) ? (double)x - mu : 0.0;
+      const double y2 = y * y;
+      s2 += y2;
+      s3 = __builtin_fma(y2, y, s3);
+      s4 = __builtin_fma(y2, y2, s4);
+    }
+    s2 = seg_sum<NSEG, P>(s2);
+    s3 = seg_sum<NSEG, P>(s3);
+    s4 = seg_sum<NSEG, P>(s4);
+    if (seg == 0 && vc) {
+      const double var = s2 * inv_n;
+      float sk = 0.f, ku = 0.f;
+      if (!p.legacy) {
+        if (var <= 0.0) {
+          zv = true;
+        } else {
+          const double sd = sqrt(var);
+          const double z3 = s3 / (sd * sd * sd), z4 = s4 / (var * var);
+          sk = (float)(z3 * k3);
+          ku = (float)((z4 * k4a - k4b) / k4c);
+        }
+      }
+      stage_out(ws, STG, D2, 0, col, CONS ? med : (float)mu);
+      stage_out(ws, STG, D2, 1, col, sk);
+      stage_out(ws, STG, D2, 2, col, ku);
+    }
+  }
+  if (zv) zv_sh = 1;
+  __syncthreads();
+  // ------------------------------------------------------------ commit (a successful round only)
+  if (zv_sh) {
+    if (tid == 0) p.status[b] = ST_ZERO_VARIANCE;
+    return;
+  }
+  const int64_t ob = (int64_t)b * D;
+  commit_staged<NT>(ws, STG, D2, D, tid, p.consensus + ob, p.skew + ob, p.kurt + ob);
+  for (int t = tid; t < N; t += NT) {
+    p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
+    p.qr[(int64_t)b * N + t] = qr_lds[t];
+  }
+  if (tid == 0) {
+    p.rel[2 * (int64_t)b] = rels[0];
+    p.rel[2 * (int64_t)b + 1] = rels[1];
+    p.status[b] = ST_OK;
+  }
+}
+
+template <int NSEG, bool CONS>
+static int launch_f32_cons(const FastParams& p, hipStream_t stream) {
+  constexpr int WAVES = 4;
+  auto k = consensus_fast_f32_kernel<NSEG, WAVES, CONS, 0>;
+  if (p.mode == 1) k = consensus_fast_f32_kernel<NSEG, WAVES, CONS, 1>;
+  if (p.mode == 2) k = consensus_fast_f32_kernel<NSEG, WAVES, CONS, 2>;
+  hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+  return (int)hipGetLastError();
+}
+template <int NSEG>
+static int launch_f32(const FastParams& p, hipStream_t stream) {
+  return p.constrained ? launch_f32_cons<NSEG, true>(p, stream) : launch_f32_cons<NSEG, false>(p, stream);
+}
+
+}  // namespace svoc
+
+using namespace svoc;
+
+// -1: shape / workspace outside what the kernel supports (the binding checks these first).
+extern "C" int svoc_fast_round_f32(const FastParams* p, hipStream_t stream) {
+  if (p->B <= 0) return 0;
+  if (p->N < 2 || p->N > 256 || p->D > p->ld || p->mode < 0 || p->mode > 2) return -1;
+  if ((int64_t)p->N * p->ld * 4 >= (1ll << 31)) return -1;   // 32-bit buffer offsets
+  if (p->mode != 1 && (!p->work || p->work_pairs < fast_work_pairs(p->D) || p->work_stride < fast_work_words(p->D)))
+    return -1;   // pass 2 stages its outputs in the workspace
+  if (p->N <= 64) return launch_f32<1>(*p, stream);
+  if (p->N <= 128) return launch_f32<2>(*p, stream);
+  return launch_f32<4>(*p, stream);
+}

@@ -17,7 +17,8 @@ Two numeric modes share one semantics:
   (csrc/kernels/consensus_exact.hip) for the rest -- or the C++ CPU engine; updates are transactions
   (a reverted round rolls the update back, exactly like a reverted Starknet tx) and are replayed in
   order per instance.
-* ``fast``: bf16 storage / fp32 math through the fused HIP kernel (csrc/kernels/consensus_fast.hip).
+* ``fast``: fp32 math over bf16 storage (the fused kernels csrc/kernels/consensus_fast_*.hip) or fp32
+  storage (``storage="fp32"``: reference resolution, csrc/kernels/consensus_fast_f32.hip, N <= 256).
   Updates inside one step are coalesced (last writer wins) -- exact for the reference because a
   round is a pure function of the current values (survey §2.8-13); a reverted round keeps the stored
   values but leaves every consensus output untouched.
@@ -57,8 +58,8 @@ class ConsensusEngine:
         dev = self.device
         if mode == "fast":
             self.vdtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[storage or "bf16"]
-            if self.device.type == "cuda" and self.vdtype != torch.bfloat16:
-                raise ValueError("the GPU fast path stores oracle values in bf16")
+            if self.device.type == "cuda" and self.vdtype == torch.float32 and self.N > 256:
+                raise ValueError("the GPU fp32-storage fast path supports N <= 256 oracles")
             self.ld = _round_up(D, 8)              # 16-B rows for global_load_lds
             odt = torch.float32
         else:
@@ -209,8 +210,8 @@ class ConsensusEngine:
         instances, more than 32 failing oracles)."""
         if self.mode != "fast" or self.device.type != "cuda":
             return None
-        if not svops.fast_work_applies(self.N, self.D, self.cfg.n_failing_oracles):
-            return None
+        if self.vdtype == torch.bfloat16 and not svops.fast_work_applies(self.N, self.D, self.cfg.n_failing_oracles):
+            return None   # (the fp32 kernel always stages its pass-2 outputs there)
         if self._work is None:
             self._work = torch.empty(svops.fast_work_numel(self.B, self.D), dtype=torch.int32,
                                      device=self.device)

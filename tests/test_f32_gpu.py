@@ -1,0 +1,174 @@
+"""fp32-storage fast kernel (csrc/kernels/consensus_fast_f32.hip): reference-resolution fast mode.
+
+Checked against (1) the plain-PyTorch fp64/fp32 reference of the same round (svoc/ops/torch_ref.py),
+(2) its CPU twin (reference_cpu.cpp fast_round_one over fp32 storage), (3) the EXACT wsad engine on
+the same wsad data (reliable masks equal, consensus within one wsad ulp: SURVEY A.3), and (4) revert
+atomicity: a reverted round leaves every committed output bitwise unchanged (contract.cairo:588-603).
+"""
+import pytest
+import torch
+
+from helpers import alloc_fast_out, beta_oracles, fast_work, run_exact, run_fast
+from svoc import ops as svops
+from svoc.ops import torch_ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _f32(B, N, D, f, seed, a=20.0):
+    x, _ = beta_oracles(B, N, D, f, a=a, seed=seed, dtype=torch.float32)
+    return x
+
+
+SHAPES = [(4, 3, 0), (7, 6, 2), (16, 33, 3), (50, 300, 5), (64, 1024, 8), (65, 129, 9), (100, 260, 10),
+          (128, 512, 16), (200, 136, 20), (256, 600, 32), (33, 1, 4)]
+
+
+@pytest.mark.parametrize("N,D,f", SHAPES)
+@pytest.mark.parametrize("constrained", [True, False])
+def test_f32_kernel_vs_torch(N, D, f, constrained):
+    torch.manual_seed(N * 31 + D)
+    B = 12
+    x = _f32(B, N, D, f, seed=N + D)
+    if not constrained:
+        x = x * 4.0 - 1.5          # unconstrained: any finite values
+    o = run_fast(x.to(DEV), D, f, constrained, 3.0)
+    torch.cuda.synchronize()
+    ref = torch_ref.fast_round(x[:, :, :D].to(DEV), f, constrained, 3.0)
+    ok = o["status"] == 0
+    assert ok.all(), o["status"]
+    assert torch.equal(o["c1"], ref["c1"].float())        # medians of fp32 values: exact
+    torch.testing.assert_close(o["qr"], ref["qr"].float(), rtol=2e-5, atol=1e-6)
+    assert torch.equal(o["reliable"].bool(), ref["reliable"])
+    if constrained:
+        assert torch.equal(o["consensus"], ref["consensus"])
+    else:
+        torch.testing.assert_close(o["consensus"], ref["consensus"], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(o["rel"], ref["rel"], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(o["skew"], ref["skew"], rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(o["kurt"], ref["kurt"], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("N,D,f", [(7, 6, 2), (64, 257, 8), (256, 100, 32)])
+def test_f32_kernel_vs_cpu_twin(N, D, f):
+    B = 10
+    x = _f32(B, N, D, f, seed=7 * N + D)
+    g = run_fast(x.to(DEV), D, f, True)
+    c = run_fast(x, D, f, True)
+    torch.cuda.synchronize()
+    for k in ("status", "c1", "consensus", "reliable"):
+        assert torch.equal(g[k].cpu(), c[k]), k
+    for k in ("qr", "rel", "skew", "kurt"):
+        torch.testing.assert_close(g[k].cpu(), c[k], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("N,D,f", [(64, 1024, 8), (256, 512, 32), (100, 77, 10)])
+def test_f32_agrees_with_exact_at_reference_resolution(N, D, f):
+    """Same wsad data (1e-6 grid) through fast-fp32 and the exact engine: identical reliable masks,
+    consensus within one wsad ulp, rel1 / rel2 within a few ulps (the contract truncates each product),
+    moments within the fast-mode tolerance of SURVEY A.3.  Instances whose exact quadratic risks tie
+    across the rank cut would be decided by values the modes round differently: none here (checked)."""
+    B = 24
+    x, _ = beta_oracles(B, N, D, f, seed=N * 3 + D, dtype=torch.float64)
+    w = (x[:, :, :D] * 1e6).to(torch.int64).contiguous()
+    xf = torch.zeros(B, N, (D + 7) // 8 * 8, dtype=torch.float32)
+    xf[:, :, :D] = (w.double() / 1e6).float()
+    fa = run_fast(xf.to(DEV), D, f, True)
+    ex = run_exact(w.to(DEV, torch.int32), f, True)
+    torch.cuda.synchronize()
+    fa = {k: v.cpu() for k, v in fa.items()}
+    ex = {k: v.cpu() for k, v in ex.items()}
+    assert (ex["status"] == 0).all() and (fa["status"] == 0).all()
+    srt = torch.sort(ex["qr"], dim=1).values
+    assert (srt[:, N - f - 1] != srt[:, N - f]).all()
+    assert torch.equal(fa["reliable"].bool(), ex["reliable"].bool())
+    assert (fa["c1"].double() * 1e6 - ex["c1"].double()).abs().max().item() <= 1.0 + 1e-6
+    cons = (fa["consensus"].double() * 1e6 - ex["consensus"].double()).abs()
+    assert cons.max().item() <= 1.0 + 1e-6, cons.max()
+    rel = (fa["rel"].double() * 1e6 - ex["rel"].double()).abs()
+    assert rel.max().item() <= 32.0, rel.max()
+    # moments: the contract truncates z to 1e-6 before cubing it (math.cairo:320-363), fast mode does not
+    sk = (fa["skew"].double() - ex["skew"].double() / 1e6).abs()
+    ku = (fa["kurt"].double() - ex["kurt"].double() / 1e6).abs()
+    assert sk.max().item() < 2e-3 and ku.max().item() < 5e-3, (sk.max(), ku.max())
+
+
+def test_f32_reverts_leave_outputs_untouched():
+    """ZERO_VARIANCE, RELIABILITY_INTERVAL and TOO_FEW_RELIABLE on instances with committed outputs:
+    every output tensor stays bitwise unchanged, statuses equal the CPU twin's."""
+    B, N, D, f = 6, 64, 200, 8
+    x = _f32(B, N, D, f, seed=3)
+    xg = x.to(DEV)
+    o = run_fast(xg, D, f, True)
+    torch.cuda.synchronize()
+    assert (o["status"] == 0).all()
+    before = {k: v.clone() for k, v in o.items() if k not in ("status", "c1")}
+    y = x.clone()
+    y[1, :, 17] = 0.25                          # zero variance
+    y[2, : N // 2 + 1, :D] = 0.0                # rel1 < 0
+    y[2, N // 2 + 1:, :D] = 1.0
+    yg = y.to(DEV)
+    op = svops.ops().fast_round
+    op(yg, None, D, f, True, 1.0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"], o["qr"], o["reliable"],
+       o["status"], 0, 0, 0, False, fast_work(B, D, DEV))
+    cpu = run_fast(y, D, f, True)
+    torch.cuda.synchronize()
+    assert torch.equal(o["status"].cpu(), cpu["status"])
+    st = o["status"].cpu()
+    assert st[1].item() != 0 and st[2].item() != 0 and (st[[0, 3, 4, 5]] == 0).all()
+    bad = st != 0
+    for k, v in before.items():
+        assert torch.equal(o[k].cpu()[bad], v.cpu()[bad]), k
+    # too few reliable: f = N - 3
+    o2 = run_fast(xg, D, N - 3, True)
+    torch.cuda.synchronize()
+    assert (o2["status"].cpu() == run_fast(x, D, N - 3, True)["status"]).all()
+    assert (o2["status"] != 0).all() and (o2["consensus"] == 0).all()
+
+
+def test_f32_split_modes_match_whole_round():
+    """Mode 1 (c1 + qr partials) / mode 2 (from the summed qr) on two column slices == the whole round."""
+    B, N, D, f = 8, 100, 300, 10
+    x = _f32(B, N, D, f, seed=11)[:, :, :D].contiguous()
+    whole = run_fast(x.to(DEV), D, f, True)
+    cut = 152
+    parts = [x[:, :, :cut].contiguous().to(DEV), x[:, :, cut:].contiguous().to(DEV)]
+    outs = [alloc_fast_out(B, N, p.shape[2], DEV) for p in parts]
+    op = svops.ops().fast_round
+    for p, o in zip(parts, outs):
+        op(p, None, p.shape[2], f, True, 1.0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"], o["qr"],
+           o["reliable"], o["status"], 0, 1, D, False, None)
+    qr = outs[0]["qr"] + outs[1]["qr"]
+    for p, o in zip(parts, outs):
+        o["qr"].copy_(qr)
+        op(p, None, p.shape[2], f, True, 1.0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"], o["qr"],
+           o["reliable"], o["status"], 0, 2, D, False, fast_work(B, p.shape[2], DEV))
+    torch.cuda.synchronize()
+    for o in outs:
+        assert (o["status"] == 0).all()
+        assert torch.equal(o["reliable"], whole["reliable"])
+        torch.testing.assert_close(o["rel"], whole["rel"], rtol=1e-5, atol=1e-6)
+    for k in ("c1", "consensus"):
+        assert torch.equal(torch.cat([outs[0][k], outs[1][k]], 1), whole[k]), k
+
+
+def test_engine_fp32_storage_gpu():
+    """ConsensusEngine(storage="fp32") on the GPU: updates, rounds, getters; agrees with the CPU engine."""
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    cfg = ConsensusConfig(n_oracles=32, dimension=100, n_failing_oracles=4, constrained=True)
+    eg = ConsensusEngine(cfg, 16, device=DEV, mode="fast", storage="fp32")
+    ec = ConsensusEngine(cfg, 16, device="cpu", mode="fast", storage="fp32")
+    torch.manual_seed(0)
+    vals = torch.rand(16 * 32, 100)
+    inst = torch.arange(16).repeat_interleave(32)
+    orc = torch.arange(32).repeat(16)
+    for e in (eg, ec):
+        st = e.step(inst, orc, vals)
+        assert (st.cpu() == 0).all()
+    torch.cuda.synchronize()
+    assert eg.values.dtype == torch.float32 and bool(eg.consensus_active.all())
+    for k in ("status", "reliable", "consensus", "c1"):
+        assert torch.equal(getattr(eg, k).cpu(), getattr(ec, k)), k
+    torch.testing.assert_close(eg.rel.cpu(), ec.rel, rtol=1e-5, atol=1e-6)

@@ -1,0 +1,8 @@
+set -u
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_f32_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/f32_tests.log 2>&1
+rc=$?; tail -30 gpurun_out/f32_tests.log; [ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
+timeout -k 10 200 python bench.py --config c2 --storage fp32 --steps 20 --warmup 3 > gpurun_out/f32_c2.log 2>&1 || { tail gpurun_out/f32_c2.log; exit 1; }
+tail -1 gpurun_out/f32_c2.log
+timeout -k 10 200 python bench.py --config c3 --storage fp32 --steps 20 --warmup 3 > gpurun_out/f32_c3.log 2>&1 || { tail gpurun_out/f32_c3.log; exit 1; }
+tail -1 gpurun_out/f32_c3.log
