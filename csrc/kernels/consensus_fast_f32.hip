@@ -26,9 +26,9 @@
 //     network;
 //   * qr partials: a transposing butterfly over the wave's columns (DPP / ds_swizzle / permlane32),
 //     per-oracle sums in LDS, deterministic (no atomics);
-//   * pass 2 sums the reliable rows in fp64 while loading the keys (exact for <= 2^29 fp32 terms, so
-//     equal values give a mean equal to them and a zero variance exactly as the CPU twin's), then one
-//     re-read (L2-resident) for the fp64 central moments;
+//   * pass 2: power sums shifted by the pass-2 median (constrained) or the first reliable row
+//     (unconstrained) from one L2-resident re-read; a constant column gives y = 0 exactly, so zero
+//     variance is detected exactly as by the CPU twin; moments combined in fp64;
 //   * outputs are staged in the workspace and committed only when the round's status is OK
 //     (contract.cairo:588-603: a failed assert reverts the whole transaction).
 #include <hip/hip_runtime.h>
@@ -40,6 +40,10 @@
 #include "svoc/launch.hpp"
 #include "svoc/sortnet.hpp"
 #include "svoc/status.hpp"
+
+#ifndef SVOC_F32_WPE
+#define SVOC_F32_WPE 1   // waves per SIMD the register budget is capped for (4: <= 128 VGPRs)
+#endif
 
 namespace svoc {
 
@@ -70,6 +74,16 @@ SVOC_DEV void qtree_f_all(const float (&q)[64], int lane, float* acc, std::integ
   ((acc[Is] += qtree_f<__builtin_ctz(P), Is, P>(q, lane)), ...);
 }
 
+// The lane's 64 rows of one column, every load issued before any is consumed (64 in flight: the
+// compiler otherwise interleaves each load with its consumer and keeps ~4 outstanding).
+SVOC_DEV void load_col(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t (&x)[64]) {
+  asm volatile("" : "+s"(rowb));   // opaque: the 64 row soffsets are recomputed here (s_mul), not
+                                   // hoisted out of the slab loops into 64 live SGPRs (spilled to VGPRs)
+#pragma unroll
+  for (int i = 0; i < 64; ++i) x[i] = bload(rs, vo, i * rowb);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int NSEG, int P, class T>
 SVOC_DEV T seg_sum(T v) {
 #pragma unroll
@@ -80,7 +94,7 @@ SVOC_DEV T seg_sum(T v) {
 // MODE: 0 whole round; 1 pass 1 only (c1 + this shard's qr partials); 2 from the all-reduced qr
 // (D-sharding, svoc/parallel/dshard.py).
 template <int NSEG, int WAVES, bool CONS, int MODE>
-__global__ __launch_bounds__(WAVES * 64) void consensus_fast_f32_kernel(FastParams p) {
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC_F32_WPE))) void consensus_fast_f32_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;      // columns per wave
   constexpr int NPAD = 64 * NSEG;   // padded oracle rows
   constexpr int W = WAVES * P;      // columns per slab
@@ -122,13 +136,17 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_f32_kernel(FastPara
     const int col = s * W + wave * P + cw;
     const bool vc = col < D;
     const int vo = seg_off + (vc ? col : 0) * 4;
+    int nvl = nv, nll = nl;
+    asm volatile("" : "+v"(nvl), "+v"(nll));   // opaque per slab: stop LICM from hoisting 64 row masks
     float c1;
     {
       uint32_t r[64];
+      load_col(rs, vo, rowb, r);
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
-        const uint32_t x = bload(rs, vo, i * rowb);
-        r[i] = (i < nv ? f32_key(x) : (i < nl ? 0u : ~0u)) ^ pol;
+        // arithmetic masks, no per-row branches: real -> key, rows >= N -> 0 (first lo1) / ~0
+        const uint32_t mr = lt_mask(i, nvl), ml1 = lt_mask(i, nll);
+        r[i] = ((f32_key(r[i]) & mr) | (~mr & ~ml1)) ^ pol;
       }
       uint32_t lo, hi;
       median_group<NSEG>(r, lo, hi);
@@ -138,10 +156,15 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_f32_kernel(FastPara
     __builtin_amdgcn_sched_barrier(0);
     // quadratic risk partials of this column (math.cairo:225-238), summed over the wave's columns
     float q[64];
+    {
+      uint32_t xr[64];
+      load_col(rs, vo, rowb, xr);
+      const uint32_t vcm = vc ? 0xffffffffu : 0u;
 #pragma unroll
-    for (int i = 0; i < 64; ++i) {
-      const float y = __builtin_bit_cast(float, bload(rs, vo, i * rowb)) - c1;
-      q[i] = (vc && i < nv) ? y * y : 0.f;   // a select: columns past D may hold anything
+      for (int i = 0; i < 64; ++i) {
+        const float y = __builtin_bit_cast(float, xr[i]) - c1;
+        q[i] = fand(y * y, vcm & lt_mask(i, nvl));   // a mask, not a multiply: columns past D may hold anything
+      }
     }
     qtree_f_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
   }
@@ -237,6 +260,12 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_f32_kernel(FastPara
   const int STG = Dp * (2 * 17 + 8 + 2) * 4;   // launch.hpp: fast_work_stage_word
   const __amdgpu_buffer_rsrc_t ws = instance_rsrc(p.work + (int64_t)b * p.work_stride, (uint32_t)(p.work_stride * 4));
   const uint64_t mymask = relmask[seg];
+  int first_rel = 0;   // unconstrained: the power sums are shifted by the first reliable row
+  if (!CONS) {
+    for (int w = 0; w < NSEG; ++w)
+      if (relmask[w]) { first_rel = 64 * w + __builtin_ctzll(relmask[w]); break; }
+    first_rel = __builtin_amdgcn_readfirstlane(first_rel);
+  }
   const uint64_t mylow = lowmask[seg];
   const double n = (double)R, inv_n = 1.0 / n;
   const double k3 = n / ((n - 1.0) * (n - 2.0));
@@ -249,56 +278,62 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_fast_f32_kernel(FastPara
     const int vo = seg_off + (vc ? col : 0) * 4;
     uint64_t mm = mymask, ml = mylow;
     asm volatile("" : "+v"(mm), "+v"(ml));   // keep the 64 row masks out of the slab loop's live set
-    double sx = 0.0;
-    float med = 0.f;
+    // shift of the power sums: the pass-2 median (constrained) or the first reliable row's value --
+    // inside the reliable cluster, and equal to every value of a constant column (zero variance exact)
+    float sh;
     if constexpr (CONS) {
       uint32_t r[64];
+      load_col(rs, vo, rowb, r);
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
-        const uint32_t x = bload(rs, vo, i * rowb);
         const uint32_t mk = bit_mask(mm, i), low = bit_mask(ml, i);
-        sx += (double)__builtin_bit_cast(float, x & mk);   // masked rows add +0
-        r[i] = ((f32_key(x) & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else low (0) / high (~0)
+        r[i] = ((f32_key(r[i]) & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else low (0) / high (~0)
       }
       uint32_t lo, hi;
       median_group<NSEG>(r, lo, hi);
-      med = 0.5f * (key_f32(lo) + key_f32(hi));
+      sh = 0.5f * (key_f32(lo) + key_f32(hi));
     } else {
-#pragma unroll 16
-      for (int i = 0; i < 64; ++i)
-        sx += (double)__builtin_bit_cast(float, bload(rs, vo, i * rowb) & bit_mask(mm, i));
+      sh = __builtin_bit_cast(float, bload(rs, (vc ? col : 0) * 4, first_rel * rowb));
     }
-    sx = seg_sum<NSEG, P>(sx);
-    const double mu = sx / n;
+    uint64_t mm2 = mymask;
+    asm volatile("" : "+v"(mm2));   // a fresh copy: no row mask CSE'd across the sort (64 live VGPRs)
     __builtin_amdgcn_sched_barrier(0);
-    // central moments about the fp64 mean (one re-read of the column, L2-resident)
-    double s2 = 0.0, s3 = 0.0, s4 = 0.0;
-#pragma unroll 16
-    for (int i = 0; i < 64; ++i) {
-      const float x = __builtin_bit_cast(float, bload(rs, vo, i * rowb));
-      const double y = bit_mask(mm, i) ? (double)x - mu : 0.0;
-      const double y2 = y * y;
-      s2 += y2;
-      s3 = __builtin_fma(y2, y, s3);
-      s4 = __builtin_fma(y2, y2, s4);
+    // shifted power sums of the reliable rows (one re-read of the column, L2-resident); y = x - sh is
+    // 0 exactly for every row of a constant column, so its variance is exactly 0, as the CPU twin's
+    float s1f = 0.f, s2f = 0.f, s3f = 0.f, s4f = 0.f;
+    {
+      uint32_t xr[64];
+      load_col(rs, vo, rowb, xr);
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const float y = fand(__builtin_bit_cast(float, xr[i]) - sh, bit_mask(mm2, i));
+        const float y2 = y * y;
+        s1f += y;
+        s2f += y2;
+        s3f = __builtin_fmaf(y2, y, s3f);
+        s4f = __builtin_fmaf(y2, y2, s4f);
+      }
     }
-    s2 = seg_sum<NSEG, P>(s2);
-    s3 = seg_sum<NSEG, P>(s3);
-    s4 = seg_sum<NSEG, P>(s4);
+    const double s1 = seg_sum<NSEG, P>((double)s1f), s2 = seg_sum<NSEG, P>((double)s2f);
+    const double s3 = seg_sum<NSEG, P>((double)s3f), s4 = seg_sum<NSEG, P>((double)s4f);
+    // central moments from the shifted sums
+    const double dl = s1 * inv_n, e2 = s2 * inv_n, e3 = s3 * inv_n, e4 = s4 * inv_n;
+    const double mu2 = e2 - dl * dl;
+    const double mu3 = e3 - 3.0 * dl * e2 + 2.0 * dl * dl * dl;
+    const double mu4 = e4 - 4.0 * dl * e3 + 6.0 * dl * dl * e2 - 3.0 * dl * dl * dl * dl;
     if (seg == 0 && vc) {
-      const double var = s2 * inv_n;
       float sk = 0.f, ku = 0.f;
       if (!p.legacy) {
-        if (var <= 0.0) {
+        if (mu2 <= 0.0) {
           zv = true;
         } else {
-          const double sd = sqrt(var);
-          const double z3 = s3 / (sd * sd * sd), z4 = s4 / (var * var);
+          const double sd = sqrt(mu2);
+          const double z3 = n * mu3 / (mu2 * sd), z4 = n * mu4 / (mu2 * mu2);
           sk = (float)(z3 * k3);
           ku = (float)((z4 * k4a - k4b) / k4c);
         }
       }
-      stage_out(ws, STG, D2, 0, col, CONS ? med : (float)mu);
+      stage_out(ws, STG, D2, 0, col, CONS ? sh : (float)((double)sh + dl));
       stage_out(ws, STG, D2, 1, col, sk);
       stage_out(ws, STG, D2, 2, col, ku);
     }

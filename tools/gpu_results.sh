@@ -21,6 +21,8 @@ run c3 300 --config c3 --steps 20 --warmup 3 &&
 run c2 300 --config c2 --steps 20 --warmup 3 &&
 run c5 300 --config c5 --steps 50 --warmup 3 &&
 run c4 300 --config c4 --steps 10 --warmup 2 &&
+run c2_fp32 300 --config c2 --storage fp32 --steps 20 --warmup 3 &&
+run c3_fp32 300 --config c3 --storage fp32 --steps 20 --warmup 3 &&
 run c2_exact 300 --config c2 --mode exact --steps 10 --warmup 2 &&
 run c2_exact_int64 300 --config c2 --mode exact --storage int64 --steps 10 --warmup 2 &&
 run c5_exact 300 --config-file configs/c5_exact_rounds.yaml --steps 20 --warmup 2 &&

@@ -24,6 +24,8 @@ ROWS = [
     ("c3", "c3: 256 × 4096 streaming, failing-oracle masking (headline)", "≈6/s numpy fp64"),
     ("c4", "c4: BERT-base sentiment oracles → consensus", "—"),
     ("c5", "c5: governance + reliability stream, 1M instances (7 × 6)", "≈127,900/s numpy fp64 (7×6)"),
+    ("c2_fp32", "c2 shape, fast mode over fp32 storage (reference resolution)", "≈93/s numpy fp64"),
+    ("c3_fp32", "c3 shape, fast mode over fp32 storage (reference resolution)", "≈6/s numpy fp64"),
     ("c2_exact", "c2 shape, exact wsad (bit-identical to the contract), int32 storage", "0.61/s exact Python emulator"),
     ("c2_exact_int64", "c2 shape, exact wsad, int64 storage", "0.61/s exact Python emulator"),
     ("c3_exact", "c3 shape (256 × 4096), exact wsad, int32 storage", "≈6/s numpy fp64 (non-exact)"),
