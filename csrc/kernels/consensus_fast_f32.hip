@@ -80,7 +80,7 @@ SVOC_DEV void load_col(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t (&x
   // opaque: the 64 row soffsets are recomputed here (s_mul), not hoisted out of the slab loops into 64
   // live SGPRs (spilled to VGPRs), and a re-read stays a re-read (not CSE'd with an earlier load of the
   // same words, which would keep 64 more VGPRs live across the sort)
-  asm volatile("" : "+s"(rowb), "+v"(vo));
+  asm volatile("" : "+s"(rowb));
 #pragma unroll
   for (int i = 0; i < 64; ++i) x[i] = bload(rs, vo, i * rowb);
   __builtin_amdgcn_sched_barrier(0);
@@ -261,14 +261,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
   const int Dp = p.work_pairs, D2 = 2 * Dp;
   const int STG = Dp * (2 * 17 + 8 + 2) * 4;   // launch.hpp: fast_work_stage_word
   const __amdgpu_buffer_rsrc_t ws = instance_rsrc(p.work + (int64_t)b * p.work_stride, (uint32_t)(p.work_stride * 4));
-  uint64_t mymask = relmask[seg];
-  uint64_t mylow = lowmask[seg];
-  if constexpr (NSEG == 1) {   // workgroup-uniform: scalar registers
-    mymask = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(mymask >> 32)) << 32) |
-             __builtin_amdgcn_readfirstlane((uint32_t)mymask);
-    mylow = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(mylow >> 32)) << 32) |
-            __builtin_amdgcn_readfirstlane((uint32_t)mylow);
-  }
+  const uint64_t mymask = relmask[seg];
+  const uint64_t mylow = lowmask[seg];
   int first_rel = 0;   // unconstrained: the power sums are shifted by the first reliable row
   if (!CONS) {
     for (int w = 0; w < NSEG; ++w)
@@ -285,10 +279,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
     const bool vc = col < D;
     const int vo = seg_off + (vc ? col : 0) * 4;
     uint64_t mm = mymask, ml = mylow;
-    // opaque per slab: keep the 64 row masks out of the slab loop's live set (N <= 64: the masks are
-    // workgroup-uniform and stay in SGPRs, read by the VALU directly)
-    if constexpr (NSEG == 1) asm volatile("" : "+s"(mm), "+s"(ml));
-    else asm volatile("" : "+v"(mm), "+v"(ml));
+    asm volatile("" : "+v"(mm), "+v"(ml));   // keep the 64 row masks out of the slab loop's live set
     // shift of the power sums: the pass-2 median (constrained) or the first reliable row's value --
     // inside the reliable cluster, and equal to every value of a constant column (zero variance exact)
     float sh;
@@ -307,8 +298,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
       sh = __builtin_bit_cast(float, bload(rs, (vc ? col : 0) * 4, first_rel * rowb));
     }
     uint64_t mm2 = mymask;
-    if constexpr (NSEG == 1) asm volatile("" : "+s"(mm2));
-    else asm volatile("" : "+v"(mm2));   // a fresh copy: no row mask CSE'd across the sort (64 live VGPRs)
+    asm volatile("" : "+v"(mm2));   // a fresh copy: no row mask CSE'd across the sort (64 live VGPRs)
     __builtin_amdgcn_sched_barrier(0);
     // shifted power sums of the reliable rows (one re-read of the column, L2-resident); y = x - sh is
     // 0 exactly for every row of a constant column, so its variance is exactly 0, as the CPU twin's
