@@ -63,7 +63,7 @@ def test_data_parallel_gloo(world):
         assert r[k]["ids"].tolist() == [3 * k, 3 * k + 1, 3 * k + 2]
 
 
-def _ds_worker(rank, world, port, outdir, x, cfgd):
+def _ds_worker(rank, world, port, outdir, x, cfgd, storage="bf16"):
     _init(rank, world, port)
     from svoc.config import ConsensusConfig
     from svoc.engine import ConsensusEngine
@@ -71,7 +71,7 @@ def _ds_worker(rank, world, port, outdir, x, cfgd):
     cfg = ConsensusConfig(**cfgd)
     lo, hi = shard_bounds(cfg.dimension, rank, world)
     lcfg = ConsensusConfig(**{**cfgd, "dimension": hi - lo})
-    e = ConsensusEngine(lcfg, x.shape[0], device="cpu", mode="fast")
+    e = ConsensusEngine(lcfg, x.shape[0], device="cpu", mode="fast", storage=storage)
     e.values[:, :, : hi - lo] = x[:, :, lo:hi]
     e.enabled.fill_(1); e.n_active.fill_(cfg.n_oracles); e.touched.fill_(1)
     run_round_sharded(e, cfg.dimension, world=world)
@@ -81,16 +81,17 @@ def _ds_worker(rank, world, port, outdir, x, cfgd):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("constrained,world", [(True, 2), (False, 2), (True, 4)])
-def test_dsharding_matches_single_process(constrained, world):
+@pytest.mark.parametrize("constrained,world,storage", [(True, 2, "bf16"), (False, 2, "bf16"), (True, 4, "bf16"),
+                                                       (True, 2, "fp32"), (False, 3, "fp32")])
+def test_dsharding_matches_single_process(constrained, world, storage):
     from helpers import beta_oracles, run_fast
     B, N, D, f = 4, 32, 40, 4
-    x, _ = beta_oracles(B, N, D, f, seed=11)
+    x, _ = beta_oracles(B, N, D, f, seed=11, dtype=torch.bfloat16 if storage == "bf16" else torch.float32)
     x = x[:, :, :D].contiguous()
     ref = run_fast(x, D, f, constrained, 1.0)
     cfgd = dict(n_oracles=N, dimension=D, n_failing_oracles=f, constrained=constrained, unconstrained_max_spread=1.0)
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_ds_worker, args=(world, _free_port(), d, x, cfgd), nprocs=world, join=True)
+        mp.spawn(_ds_worker, args=(world, _free_port(), d, x, cfgd, storage), nprocs=world, join=True)
         r = [torch.load(os.path.join(d, f"ds{i}.pt"), weights_only=True) for i in range(world)]
     for s in r:
         assert torch.equal(s["st"], ref["status"])
