@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256) void upd_apply_kernel(UpdateParams p) {
 // unique (instance, oracle) pairs (e.g. a synthetic stream, one bootstrap batch per window): no
 // last-writer resolution needed, so validation and the row copy run in one pass over the updates
 // (one read of the update rows instead of two)
-template <int L>
+template <int L, int RB>
 __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
   const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
   const int sub = threadIdx.x & (L - 1);
@@ -137,12 +137,12 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
   const unsigned char* src = (const unsigned char*)p.upd + u * row_bytes;
   unsigned char* dst = (unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes;
   const bool vec = (row_bytes & 15) == 0 && (((uintptr_t)src) & 15) == 0 && (((uintptr_t)dst) & 15) == 0;
-  // bf16 rows of <= RB*L 16-B chunks (c3: 8 KiB rows, 8 chunks per lane): every chunk is loaded
-  // once into registers (all loads in flight together, non-temporal: the update batch is read
-  // once), validated there and stored from there, so the row is never re-read
-  constexpr int RB = 8;
+  // bf16 / fp32 rows of <= RB*L 16-B chunks (c3: 8 KiB bf16 rows, 8 chunks per lane; 16 KiB fp32
+  // rows, RB = 16): every chunk is loaded once into registers (all loads in flight together,
+  // non-temporal: the update batch is read once), validated there and stored from there, so the row
+  // is never re-read
   const int64_t nch = row_bytes / 16;
-  if (p.dtype == 0 && vec && nch <= (int64_t)RB * L) {  // uniform over the launch
+  if (p.dtype <= 1 && vec && nch <= (int64_t)RB * L) {  // uniform over the launch
     uint4 v[RB];
     bool ok = true, fin = true;
     const bool live = in && st == ST_OK;
@@ -158,8 +158,13 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
       const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        if (p.constrained) ok = ok && bf16_unit(w[j] & 0xffffu) && bf16_unit(w[j] >> 16);
-        else fin = fin && ((w[j] & 0x7f80u) != 0x7f80u) && ((w[j] & 0x7f800000u) != 0x7f800000u);
+        if (p.dtype == 1) {   // fp32: 0 <= x <= 1 (and -0.0) / finite
+          if (p.constrained) ok = ok && (w[j] <= 0x3f800000u || w[j] == 0x80000000u);
+          else fin = fin && ((w[j] & 0x7f800000u) != 0x7f800000u);
+        } else {
+          if (p.constrained) ok = ok && bf16_unit(w[j] & 0xffffu) && bf16_unit(w[j] >> 16);
+          else fin = fin && ((w[j] & 0x7f80u) != 0x7f80u) && ((w[j] & 0x7f800000u) != 0x7f800000u);
+        }
       }
     }
     ok = group_all<L>(ok);
@@ -253,7 +258,12 @@ template <int L>
 static int launch_updates(const UpdateParams& p, hipStream_t stream) {
   const int64_t blocks = ((int64_t)p.U * L + 255) / 256;
   if (p.unique) {
-    hipLaunchKernelGGL(upd_fused_unique_kernel<L>, dim3((unsigned)blocks), dim3(256), 0, stream, p);
+    // registers for the whole row: 8 16-B chunks per lane, 16 for rows past 8 * L chunks (fp32 c3)
+    const int64_t nch = (int64_t)p.D * p.elem_bytes / 16;
+    if (L == 64 && nch > 8 * L)
+      hipLaunchKernelGGL((upd_fused_unique_kernel<L, 16>), dim3((unsigned)blocks), dim3(256), 0, stream, p);
+    else
+      hipLaunchKernelGGL((upd_fused_unique_kernel<L, 8>), dim3((unsigned)blocks), dim3(256), 0, stream, p);
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(upd_validate_kernel<L>, dim3((unsigned)blocks), dim3(256), 0, stream, p);

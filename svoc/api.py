@@ -74,7 +74,7 @@ class OracleConsensus:
 
     def __init__(self, admins: Sequence[int], enable_oracle_replacement: bool, required_majority: int,
                  n_failing_oracles: int, constrained: bool, unconstrained_max_spread: int, dimension: int,
-                 oracles: Sequence[int], device="cpu", mode: str = "exact"):
+                 oracles: Sequence[int], device="cpu", mode: str = "exact", storage=None):
         ms = felt_to_i128(int(unconstrained_max_spread))
         cfg = ConsensusConfig(n_oracles=len(oracles), dimension=dimension, n_failing_oracles=n_failing_oracles,
                               constrained=bool(constrained), unconstrained_max_spread=ms / WSAD,
@@ -82,7 +82,7 @@ class OracleConsensus:
                               enable_oracle_replacement=bool(enable_oracle_replacement),
                               unconstrained_max_spread_wsad=ms)
         self._max_spread_wsad = ms
-        self._svc = ConsensusService(cfg, 1, list(admins), list(oracles), device=device, mode=mode)
+        self._svc = ConsensusService(cfg, 1, list(admins), list(oracles), device=device, mode=mode, storage=storage)
         self._b = 0
 
     @classmethod
@@ -203,7 +203,7 @@ class LegacyOracleConsensus(OracleConsensus):
                               unconstrained_max_spread_wsad=ms, variant=variant)
         cfg.validate()
         self._max_spread_wsad = ms
-        self._svc = ConsensusService(cfg, 1, list(admins), list(oracles), device=device, mode=mode)
+        self._svc = ConsensusService(cfg, 1, list(admins), list(oracles), device=device, mode=mode, storage=storage)
         self._b = 0
         self._scalar = variant == "1d_legacy"
 

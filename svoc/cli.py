@@ -101,8 +101,8 @@ class Client:
             from .engine import ConsensusEngine
             from .models.sentiment_oracle import SentimentOraclePipeline
             cfg = ConsensusConfig(n_oracles=N_ORACLES, dimension=6, n_failing_oracles=N_FAILING)
-            storage = "bf16" if self.device.startswith("cuda") else "fp32"
-            scratch = ConsensusEngine(cfg, 1, device=self.device, mode="fast", storage=storage)
+            # fp32 storage (reference resolution) on the CPU and on the GPU (consensus_fast_f32.hip)
+            scratch = ConsensusEngine(cfg, 1, device=self.device, mode="fast", storage="fp32")
             self._pipe = SentimentOraclePipeline(scratch, enc_cfg=self.enc_cfg, seed=self.seed)
         return self._pipe
 

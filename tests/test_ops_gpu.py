@@ -217,8 +217,10 @@ def test_unconstrained_updates_reject_non_finite_gpu():
         assert st.cpu().tolist() == [Status.OK, Status.NON_FINITE, Status.NON_FINITE, Status.OK]
 
 
-@pytest.mark.parametrize("D,constrained", [(6, True), (4096, True), (100, False)])
-def test_unique_update_path_matches_general(D, constrained):
+@pytest.mark.parametrize("D,constrained,storage", [(6, True, "bf16"), (4096, True, "bf16"), (100, False, "bf16"),
+                                                   (6, True, "fp32"), (2048, True, "fp32"), (4096, True, "fp32"),
+                                                   (4096, False, "fp32"), (100, False, "fp32")])
+def test_unique_update_path_matches_general(D, constrained, storage):
     """apply_updates(unique=True) (one fused pass) == the last-writer path on distinct pairs."""
     from svoc.config import ConsensusConfig
     from svoc.engine import ConsensusEngine
@@ -231,9 +233,11 @@ def test_unique_update_path_matches_general(D, constrained):
     vals = torch.rand(U, D, generator=g)
     vals[3, 0] = 1.5                 # interval error (constrained) / fine (unconstrained)
     vals[7, D - 1] = float("nan")    # rejected either way
+    vals[9, 0] = -0.0                # accepted (0 <= -0.0 <= 1)
+    vals[11, 1] = -1e-30             # interval error (constrained)
     outs = []
     for unique in (False, True):
-        e = ConsensusEngine(cfg, B, device=DEV, mode="fast")
+        e = ConsensusEngine(cfg, B, device=DEV, mode="fast", storage=storage)
         st = e.apply_updates(inst.to(DEV), orc.to(DEV), vals.to(DEV), unique=unique)
         outs.append((st.cpu(), e.values.cpu(), e.enabled.cpu(), e.n_active.cpu(), e.touched.cpu()))
     for a, b in zip(*outs):
