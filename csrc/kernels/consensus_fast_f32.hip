@@ -26,9 +26,11 @@
 //     network;
 //   * qr partials: a transposing butterfly over the wave's columns (DPP / ds_swizzle / permlane32),
 //     per-oracle sums in LDS, deterministic (no atomics);
-//   * pass 2: power sums shifted by the pass-2 median (constrained) or the first reliable row
-//     (unconstrained) from one L2-resident re-read; a constant column gives y = 0 exactly, so zero
-//     variance is detected exactly as by the CPU twin; moments combined in fp64;
+//   * pass 2 reads each column ONCE: the sort keys and, from the same registers, the reliable rows'
+//     power sums shifted by the pass-1 median plus their min / max key (a constant column -- zero
+//     variance -- is decided exactly, as by the CPU twin); a column whose mean sits far from c1
+//     relative to its spread is re-read once with the shift at its mean (cancellation guard);
+//     moments combined in fp64;
 //   * outputs are staged in the workspace and committed only when the round's status is OK
 //     (contract.cairo:588-603: a failed assert reverts the whole transaction).
 #include <hip/hip_runtime.h>
@@ -263,10 +265,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
   const __amdgpu_buffer_rsrc_t ws = instance_rsrc(p.work + (int64_t)b * p.work_stride, (uint32_t)(p.work_stride * 4));
   const uint64_t mymask = relmask[seg];
   const uint64_t mylow = lowmask[seg];
-  int first_rel = 0;   // unconstrained: the power sums are shifted by the first reliable row
-  if (!CONS) {
-    for (int w = 0; w < NSEG; ++w)
-      if (relmask[w]) { first_rel = 64 * w + __builtin_ctzll(relmask[w]); break; }
+  int first_rel = 0;   // N <= 64 unconstrained: the power sums are shifted by the first reliable row
+  if (!CONS && NSEG == 1) {
+    if (relmask[0]) first_rel = __builtin_ctzll(relmask[0]);
     first_rel = __builtin_amdgcn_readfirstlane(first_rel);
   }
   const double n = (double)R, inv_n = 1.0 / n;
@@ -280,44 +281,122 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
     const int vo = seg_off + (vc ? col : 0) * 4;
     uint64_t mm = mymask, ml = mylow;
     asm volatile("" : "+v"(mm), "+v"(ml));   // keep the 64 row masks out of the slab loop's live set
-    // shift of the power sums: the pass-2 median (constrained) or the first reliable row's value --
-    // inside the reliable cluster, and equal to every value of a constant column (zero variance exact)
-    float sh;
-    if constexpr (CONS) {
-      uint32_t r[64];
-      load_col(rs, vo, rowb, r);
+    float sh = 0.f;       // constrained: the pass-2 smooth median (the consensus)
+    bool constant;        // every reliable value equal (zero variance, decided exactly)
+    double shift, s1, s2, s3, s4;   // power sums of the reliable rows about `shift`
+    if constexpr (NSEG == 1) {
+      // N <= 64: median first, then one re-read for the moments (the one-read form below costs this
+      // instantiation ~250 VGPRs: the pruned 64-key network does not stream)
+      // shift of the power sums: the pass-2 median (constrained) or the first reliable row's value --
+      // inside the reliable cluster, and equal to every value of a constant column (zero variance exact)
+      if constexpr (CONS) {
+        uint32_t r[64];
+        load_col(rs, vo, rowb, r);
 #pragma unroll
-      for (int i = 0; i < 64; ++i) {
-        const uint32_t mk = bit_mask(mm, i), low = bit_mask(ml, i);
-        r[i] = ((f32_key(r[i]) & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else low (0) / high (~0)
+        for (int i = 0; i < 64; ++i) {
+          const uint32_t mk = bit_mask(mm, i), low = bit_mask(ml, i);
+          r[i] = ((f32_key(r[i]) & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else low (0) / high (~0)
+        }
+        uint32_t lo, hi;
+        median_group<NSEG>(r, lo, hi);
+        sh = 0.5f * (key_f32(lo) + key_f32(hi));
+      } else {
+        sh = __builtin_bit_cast(float, bload(rs, (vc ? col : 0) * 4, first_rel * rowb));
       }
-      uint32_t lo, hi;
-      median_group<NSEG>(r, lo, hi);
-      sh = 0.5f * (key_f32(lo) + key_f32(hi));
+      uint64_t mm2 = mymask;
+      asm volatile("" : "+v"(mm2));   // a fresh copy: no row mask CSE'd across the sort (64 live VGPRs)
+      __builtin_amdgcn_sched_barrier(0);
+      // shifted power sums of the reliable rows (one re-read of the column, L2-resident); y = x - sh is
+      // 0 exactly for every row of a constant column, so its variance is exactly 0, as the CPU twin's
+      float s1f = 0.f, s2f = 0.f, s3f = 0.f, s4f = 0.f;
+      {
+        uint32_t xr[64];
+        load_col(rs, vo, rowb, xr);
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          const float y = fand(__builtin_bit_cast(float, xr[i]) - sh, bit_mask(mm2, i));
+          const float y2 = y * y;
+          s1f += y;
+          s2f += y2;
+          s3f = __builtin_fmaf(y2, y, s3f);
+          s4f = __builtin_fmaf(y2, y2, s4f);
+        }
+      }
+      s1 = seg_sum<NSEG, P>((double)s1f); s2 = seg_sum<NSEG, P>((double)s2f);
+      s3 = seg_sum<NSEG, P>((double)s3f); s4 = seg_sum<NSEG, P>((double)s4f);
+      constant = false;
+      shift = (double)sh;
     } else {
-      sh = __builtin_bit_cast(float, bload(rs, (vc ? col : 0) * 4, first_rel * rowb));
-    }
-    uint64_t mm2 = mymask;
-    asm volatile("" : "+v"(mm2));   // a fresh copy: no row mask CSE'd across the sort (64 live VGPRs)
-    __builtin_amdgcn_sched_barrier(0);
-    // shifted power sums of the reliable rows (one re-read of the column, L2-resident); y = x - sh is
-    // 0 exactly for every row of a constant column, so its variance is exactly 0, as the CPU twin's
-    float s1f = 0.f, s2f = 0.f, s3f = 0.f, s4f = 0.f;
-    {
-      uint32_t xr[64];
-      load_col(rs, vo, rowb, xr);
+      // ONE read of the column: the sort keys of pass 2 and, from the same registers, the reliable rows'
+      // power sums shifted by the pass-1 median c1 (known here: written by pass 1 / the caller in mode 2)
+      // plus their min / max key (a constant column is decided exactly: zero variance, as the CPU twin)
+      const float c1c = vc ? p.c1[(int64_t)b * D + col] : 0.f;
+      float s1f = 0.f, s2f = 0.f, s3f = 0.f, s4f = 0.f;
+      uint32_t kmn = ~0u, kmx = 0u;
+      {
+        uint32_t r[64];
+        load_col(rs, vo, rowb, r);
 #pragma unroll
-      for (int i = 0; i < 64; ++i) {
-        const float y = fand(__builtin_bit_cast(float, xr[i]) - sh, bit_mask(mm2, i));
-        const float y2 = y * y;
-        s1f += y;
-        s2f += y2;
-        s3f = __builtin_fmaf(y2, y, s3f);
-        s4f = __builtin_fmaf(y2, y2, s4f);
+        for (int i = 0; i < 64; ++i) {
+          if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // stream the rows: raw value -> key in place
+          const uint32_t mk = bit_mask(mm, i);
+          const float y = fand(__builtin_bit_cast(float, r[i]) - c1c, mk);
+          const float y2 = y * y;
+          s1f += y;
+          s2f += y2;
+          s3f = __builtin_fmaf(y2, y, s3f);
+          s4f = __builtin_fmaf(y2, y2, s4f);
+          const uint32_t key = f32_key(r[i]);
+          kmn = min(kmn, key | ~mk);
+          kmx = max(kmx, key & mk);
+          if constexpr (CONS) {
+            const uint32_t low = bit_mask(ml, i);
+            r[i] = ((key & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else low (0) / high (~0)
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (CONS) {
+          uint32_t lo, hi;
+          median_group<NSEG>(r, lo, hi);
+          sh = 0.5f * (key_f32(lo) + key_f32(hi));
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 1; t < NSEG; t <<= 1) {
+        kmn = min(kmn, (uint32_t)__shfl_xor((int)kmn, t * P));
+        kmx = max(kmx, (uint32_t)__shfl_xor((int)kmx, t * P));
+      }
+      constant = kmn == kmx;
+      s1 = seg_sum<NSEG, P>((double)s1f); s2 = seg_sum<NSEG, P>((double)s2f);
+      s3 = seg_sum<NSEG, P>((double)s3f); s4 = seg_sum<NSEG, P>((double)s4f);
+      shift = (double)c1c;
+      // cancellation guard: when the reliable rows' mean sits far from c1 relative to their spread
+      // (mean offset^2 > 16 x variance), re-read the column once with the shift at the mean
+      {
+        const double dl = s1 * inv_n, mu2 = s2 * inv_n - dl * dl;
+        if (!constant && dl * dl > 16.0 * mu2) {
+          uint64_t mm2 = mymask;
+          asm volatile("" : "+v"(mm2));
+          const float sh2 = (float)((double)c1c + dl);
+          float t1 = 0.f, t2 = 0.f, t3 = 0.f, t4 = 0.f;
+          uint32_t xr[64];
+          load_col(rs, vo, rowb, xr);
+#pragma unroll
+          for (int i = 0; i < 64; ++i) {
+            const float y = fand(__builtin_bit_cast(float, xr[i]) - sh2, bit_mask(mm2, i));
+            const float y2 = y * y;
+            t1 += y;
+            t2 += y2;
+            t3 = __builtin_fmaf(y2, y, t3);
+            t4 = __builtin_fmaf(y2, y2, t4);
+          }
+          s1 = seg_sum<NSEG, P>((double)t1); s2 = seg_sum<NSEG, P>((double)t2);
+          s3 = seg_sum<NSEG, P>((double)t3); s4 = seg_sum<NSEG, P>((double)t4);
+          shift = (double)sh2;
+        }
       }
     }
-    const double s1 = seg_sum<NSEG, P>((double)s1f), s2 = seg_sum<NSEG, P>((double)s2f);
-    const double s3 = seg_sum<NSEG, P>((double)s3f), s4 = seg_sum<NSEG, P>((double)s4f);
     // central moments from the shifted sums
     const double dl = s1 * inv_n, e2 = s2 * inv_n, e3 = s3 * inv_n, e4 = s4 * inv_n;
     const double mu2 = e2 - dl * dl;
@@ -326,7 +405,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
     if (seg == 0 && vc) {
       float sk = 0.f, ku = 0.f;
       if (!p.legacy) {
-        if (mu2 <= 0.0) {
+        if (constant || mu2 <= 0.0) {
           zv = true;
         } else {
           const double sd = sqrt(mu2);
@@ -335,7 +414,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
           ku = (float)((z4 * k4a - k4b) / k4c);
         }
       }
-      stage_out(ws, STG, D2, 0, col, CONS ? sh : (float)((double)sh + dl));
+      stage_out(ws, STG, D2, 0, col, CONS ? sh : (float)(shift + dl));
       stage_out(ws, STG, D2, 1, col, sk);
       stage_out(ws, STG, D2, 2, col, ku);
     }
