@@ -94,6 +94,7 @@ SVOC_DEV uint32_t xor_lane_u32(uint32_t v) {
 template <int M>
 SVOC_DEV float xor_lane(float v) { return __builtin_bit_cast(float, xor_lane_u32<M>(__builtin_bit_cast(uint32_t, v))); }
 SVOC_DEV u16x2 shfl_k(u16x2 v, int src) { return as_k((uint32_t)__shfl((int)as_u32(v), src)); }
+SVOC_DEV uint32_t shfl_k(uint32_t v, int src) { return (uint32_t)__shfl((int)v, src); }
 
 // Full ascending bitonic sort of the 64 registers of one lane (each half independently).
 SVOC_DEV void sort64(u16x2 (&r)[64]) {
@@ -179,31 +180,34 @@ SVOC_DEV void merge64(K (&r)[64]) {
 }
 
 // Cross-lane flip: position i meets the partner's position 63-i; lower lane keeps the minima.
-SVOC_DEV void xlane_flip(u16x2 (&r)[64], int xmask, bool upper) {
+// (K: u16x2 = two bf16 columns per register, uint32_t = one 32-bit key)
+template <class K>
+SVOC_DEV void xlane_flip(K (&r)[64], int xmask, bool upper) {
 #pragma unroll
   for (int i = 0; i < 32; ++i) {
-    const u16x2 a = r[i], b = r[63 - i];
-    const u16x2 pa = shfl_xor_k(b, xmask);  // partner's r[63-i]
-    const u16x2 pb = shfl_xor_k(a, xmask);  // partner's r[i]
+    const K a = r[i], b = r[63 - i];
+    const K pa = shfl_xor_k(b, xmask);  // partner's r[63-i]
+    const K pb = shfl_xor_k(a, xmask);  // partner's r[i]
     r[i] = upper ? kmax(a, pa) : kmin(a, pa);
     r[63 - i] = upper ? kmax(b, pb) : kmin(b, pb);
   }
 }
 
 // Cross-lane half-cleaner: position i meets the partner's position i.
-SVOC_DEV void xlane_hc(u16x2 (&r)[64], int xmask, bool upper) {
+template <class K>
+SVOC_DEV void xlane_hc(K (&r)[64], int xmask, bool upper) {
 #pragma unroll
   for (int i = 0; i < 64; ++i) {
-    const u16x2 a = r[i];
-    const u16x2 p = shfl_xor_k(a, xmask);
+    const K a = r[i];
+    const K p = shfl_xor_k(a, xmask);
     r[i] = upper ? kmax(a, p) : kmin(a, p);
   }
 }
 
 // Sort 64*NSEG keys (x2 columns) spread over the NSEG lanes of a group. P = pairs per wave.
-template <int NSEG, int P>
-SVOC_DEV void sort_group(u16x2 (&r)[64], int seg) {
-  sort64_oem(r);
+template <int NSEG, int P, class K>
+SVOC_DEV void sort_group(K (&r)[64], int seg) {
+  sort_oem<64>(r);
 #pragma unroll
   for (int s = 2; s <= NSEG; s <<= 1) {
     xlane_flip(r, (s - 1) * P, (seg & (s >> 1)) != 0);
@@ -254,8 +258,8 @@ SVOC_DEV u16x2 group_select(const u16x2 (&r)[64], int rank, int lane) {
 // The two middle order statistics of the group's sorted 64*NSEG keys when the sentinel padding has
 // been split so that they sit at the fixed positions NPAD/2 - 1 and NPAD/2: no runtime register
 // indexing, at most one cross-lane read per value.
-template <int NSEG, int P>
-SVOC_DEV void middle_pair(const u16x2 (&r)[64], int seg, int lane, u16x2& lo, u16x2& hi) {
+template <int NSEG, int P, class K>
+SVOC_DEV void middle_pair(const K (&r)[64], int seg, int lane, K& lo, K& hi) {
   if constexpr (NSEG == 1) {
     lo = r[31];
     hi = r[32];
@@ -372,8 +376,8 @@ SVOC_DEV void median_group(K (&r)[64], K& lo, K& hi) {
 // per merge level a cross-lane flip, cross-lane half-cleaners and an in-lane merge), then the keys
 // at sorted positions NPAD/2 - 1 and NPAD/2 read from their owner lanes (middle_pair).  Keys in true
 // polarity (group_polarity<NSEG> = 0 for these widths).
-template <int NSEG, int P>
-SVOC_DEV void median_group_wide(u16x2 (&r)[64], int seg, int lane, u16x2& lo, u16x2& hi) {
+template <int NSEG, int P, class K>
+SVOC_DEV void median_group_wide(K (&r)[64], int seg, int lane, K& lo, K& hi) {
   static_assert(NSEG == 8 || NSEG == 16, "wide groups");
   sort_group<NSEG, P>(r, seg);
   middle_pair<NSEG, P>(r, seg, lane, lo, hi);

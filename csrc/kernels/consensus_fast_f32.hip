@@ -18,7 +18,7 @@
 //           (math.cairo:320-398).
 //
 // MI355X mapping (the column-parallel layout of consensus_wsad.hip with float math):
-//   * lane = column; NSEG = ceil(N / 64) lanes share a column for N > 64 (64 rows per lane);
+//   * lane = column; NSEG = ceil(N / 64) lanes share a column for N > 64 (64 rows per lane; N <= 1024);
 //     row offsets ride in SGPR soffsets of one buffer resource per instance (no address VGPRs);
 //   * fp32 -> order-preserving u32 key (sign-magnitude flip); median_group (sortnet.hpp) finds the
 //     two middle order statistics; rows >= N (and unreliable rows in pass 2) become 0 / ~0
@@ -88,6 +88,14 @@ SVOC_DEV void load_col(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t (&x
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// The two middle order statistics of the column group's 64*NSEG keys: median_group (NSEG <= 4,
+// keys XOR group_polarity) or the full cross-lane bitonic sort for N up to 512 / 1024 (NSEG 8 / 16).
+template <int NSEG, int P>
+SVOC_DEV void col_median(uint32_t (&r)[64], int lane, uint32_t& lo, uint32_t& hi) {
+  if constexpr (NSEG >= 8) median_group_wide<NSEG, P>(r, lane / P, lane, lo, hi);
+  else median_group<NSEG>(r, lo, hi);
+}
+
 template <int NSEG, int P, class T>
 SVOC_DEV T seg_sum(T v) {
 #pragma unroll
@@ -106,7 +114,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
   constexpr int KEEP = 64 / P;      // qr rows a lane holds after the butterfly
   __shared__ float qr_part[WAVES * NPAD];
   __shared__ float qr_lds[NPAD];
-  __shared__ uint64_t relmask[4], lowmask[4];
+  constexpr int NM = NSEG < 4 ? 4 : NSEG;   // 64-row mask words
+  __shared__ uint64_t relmask[NM], lowmask[NM];
   __shared__ float rels[2];
   __shared__ int st_sh, zv_sh;
 
@@ -153,7 +162,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
         r[i] = ((f32_key(r[i]) & mr) | (~mr & ~ml1)) ^ pol;
       }
       uint32_t lo, hi;
-      median_group<NSEG>(r, lo, hi);
+      col_median<NSEG, P>(r, lane, lo, hi);
       c1 = 0.5f * (key_f32(lo) + key_f32(hi));
     }
     if (seg == 0 && vc) p.c1[(int64_t)b * D + col] = c1;
@@ -212,7 +221,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
       rel = rank < R;
     }
     const uint64_t bal = __ballot(rel);
-    if (lane == 0 && (t >> 6) < 4) relmask[t >> 6] = bal;
+    if (lane == 0 && (t >> 6) < NM) relmask[t >> 6] = bal;
   }
   __syncthreads();
   if (tid == 0) {
@@ -242,7 +251,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
     st_sh = st;
     // pass-2 sentinel split: the first (NPAD - R + 1) / 2 non-reliable rows (row order) sort low
     int need = (NPAD - R + 1) >> 1;
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NM; ++w) {
       uint64_t nr = w < NSEG ? ~relmask[w] : 0ull, lm = 0ull;
       while (need > 0 && nr) {
         const uint64_t bit = nr & (0ull - nr);
@@ -298,7 +307,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
           r[i] = ((f32_key(r[i]) & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else low (0) / high (~0)
         }
         uint32_t lo, hi;
-        median_group<NSEG>(r, lo, hi);
+        col_median<NSEG, P>(r, lane, lo, hi);
         sh = 0.5f * (key_f32(lo) + key_f32(hi));
       } else {
         sh = __builtin_bit_cast(float, bload(rs, (vc ? col : 0) * 4, first_rel * rowb));
@@ -357,7 +366,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (CONS) {
           uint32_t lo, hi;
-          median_group<NSEG>(r, lo, hi);
+          col_median<NSEG, P>(r, lane, lo, hi);
           sh = 0.5f * (key_f32(lo) + key_f32(hi));
         }
       }
@@ -460,11 +469,13 @@ using namespace svoc;
 // -1: shape / workspace outside what the kernel supports (the binding checks these first).
 extern "C" int svoc_fast_round_f32(const FastParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
-  if (p->N < 2 || p->N > 256 || p->D > p->ld || p->mode < 0 || p->mode > 2) return -1;
+  if (p->N < 2 || p->N > 1024 || p->D > p->ld || p->mode < 0 || p->mode > 2) return -1;
   if ((int64_t)p->N * p->ld * 4 >= (1ll << 31)) return -1;   // 32-bit buffer offsets
   if (p->mode != 1 && (!p->work || p->work_pairs < fast_work_pairs(p->D) || p->work_stride < fast_work_words(p->D)))
     return -1;   // pass 2 stages its outputs in the workspace
   if (p->N <= 64) return launch_f32<1>(*p, stream);
   if (p->N <= 128) return launch_f32<2>(*p, stream);
-  return launch_f32<4>(*p, stream);
+  if (p->N <= 256) return launch_f32<4>(*p, stream);
+  if (p->N <= 512) return launch_f32<8>(*p, stream);
+  return launch_f32<16>(*p, stream);
 }

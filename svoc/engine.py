@@ -18,7 +18,7 @@ Two numeric modes share one semantics:
   (a reverted round rolls the update back, exactly like a reverted Starknet tx) and are replayed in
   order per instance.
 * ``fast``: fp32 math over bf16 storage (the fused kernels csrc/kernels/consensus_fast_*.hip) or fp32
-  storage (``storage="fp32"``: reference resolution, csrc/kernels/consensus_fast_f32.hip, N <= 256).
+  storage (``storage="fp32"``: reference resolution, csrc/kernels/consensus_fast_f32.hip).
   Updates inside one step are coalesced (last writer wins) -- exact for the reference because a
   round is a pure function of the current values (survey §2.8-13); a reverted round keeps the stored
   values but leaves every consensus output untouched.
@@ -58,8 +58,6 @@ class ConsensusEngine:
         dev = self.device
         if mode == "fast":
             self.vdtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[storage or "bf16"]
-            if self.device.type == "cuda" and self.vdtype == torch.float32 and self.N > 256:
-                raise ValueError("the GPU fp32-storage fast path supports N <= 256 oracles")
             self.ld = _round_up(D, 8)              # 16-B rows for global_load_lds
             odt = torch.float32
         else:

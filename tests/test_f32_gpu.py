@@ -22,7 +22,8 @@ def _f32(B, N, D, f, seed, a=20.0):
 
 
 SHAPES = [(4, 3, 0), (7, 6, 2), (16, 33, 3), (50, 300, 5), (64, 1024, 8), (65, 129, 9), (100, 260, 10),
-          (128, 512, 16), (200, 136, 20), (256, 600, 32), (33, 1, 4)]
+          (128, 512, 16), (200, 136, 20), (256, 600, 32), (33, 1, 4), (300, 70, 30), (512, 130, 64),
+          (1000, 40, 100), (1024, 256, 128)]
 
 
 @pytest.mark.parametrize("N,D,f", SHAPES)
@@ -66,7 +67,7 @@ def test_f32_kernel_vs_cpu_twin(N, D, f):
         torch.testing.assert_close(g[k].cpu(), c[k], rtol=1e-3, atol=5e-4)
 
 
-@pytest.mark.parametrize("N,D,f", [(64, 1024, 8), (256, 512, 32), (100, 77, 10)])
+@pytest.mark.parametrize("N,D,f", [(64, 1024, 8), (256, 512, 32), (100, 77, 10), (512, 96, 64)])
 def test_f32_agrees_with_exact_at_reference_resolution(N, D, f):
     """Same wsad data (1e-6 grid) through fast-fp32 and the exact engine: identical reliable masks,
     consensus within one wsad ulp, rel1 / rel2 within a few ulps (the contract truncates each product),
