@@ -28,6 +28,7 @@ run c2_exact_int64 300 --config c2 --mode exact --storage int64 --steps 10 --war
 run c5_exact 300 --config-file configs/c5_exact_rounds.yaml --steps 20 --warmup 2 &&
 run c3_exact 300 --config-file configs/c3_exact_rounds.yaml --steps 10 --warmup 2 &&
 run wide512 300 --config-file configs/wide512.yaml --steps 10 --warmup 2 &&
+run wide512_fp32 300 --config-file configs/wide512.yaml --storage fp32 --steps 10 --warmup 2 &&
 run c1 300 --config c1 --steps 50 --warmup 3 || exit 1
 for cfg in c3 c2 c4; do
   echo "=== rocprof $cfg ($(date +%T))"

@@ -31,6 +31,7 @@ ROWS = [
     ("c3_exact", "c3 shape (256 × 4096), exact wsad, int32 storage", "≈6/s numpy fp64 (non-exact)"),
     ("c5_exact", "c5 shape (7 × 6), exact wsad, 1M instances", "939/s exact Python emulator"),
     ("wide512", "512 oracles × 2048 dims, 1024 instances (N > 256)", "—"),
+    ("wide512_fp32", "512 × 2048, fast mode over fp32 storage", "—"),
 ]
 
 
