@@ -96,6 +96,12 @@ SVOC_DEV void col_median(uint32_t (&r)[64], int lane, uint32_t& lo, uint32_t& hi
   else median_group<NSEG>(r, lo, hi);
 }
 
+// 0, computed from v: a re-read whose offset adds after(v) cannot be issued before v exists.  Keeps the
+// re-read loads below the sort network that produces v (LLVM otherwise hoists them above it and holds
+// 64 more VGPRs across the network).  v is a median of real rows (never NaN) on every lane that
+// commits; elsewhere the +4 only shifts a discarded read.
+SVOC_DEV int after(float v) { return v != v ? 4 : 0; }
+
 template <int NSEG, int P, class T>
 SVOC_DEV T seg_sum(T v) {
 #pragma unroll
@@ -171,7 +177,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
     float q[64];
     {
       uint32_t xr[64];
-      load_col(rs, vo, rowb, xr);
+      load_col(rs, vo + after(c1), rowb, xr);
       const uint32_t vcm = vc ? 0xffffffffu : 0u;
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
@@ -320,7 +326,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
       float s1f = 0.f, s2f = 0.f, s3f = 0.f, s4f = 0.f;
       {
         uint32_t xr[64];
-        load_col(rs, vo, rowb, xr);
+        load_col(rs, vo + after(sh), rowb, xr);
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
           const float y = fand(__builtin_bit_cast(float, xr[i]) - sh, bit_mask(mm2, i));
