@@ -92,13 +92,16 @@ def test_corrupt_header_rejected_without_allocation(tmp_path):
         state.load(p)
 
 
-def test_fast_mode_roundtrip(tmp_path):
+@pytest.mark.parametrize("storage", ["bf16", "fp32"])
+def test_fast_mode_roundtrip(tmp_path, storage):
     cfg = ConsensusConfig(n_oracles=16, dimension=20, n_failing_oracles=2, n_admins=2)
-    a = ConsensusService(cfg, 4, ADMINS[:2], [100 + i for i in range(16)], device="cpu", mode="fast")
+    a = ConsensusService(cfg, 4, ADMINS[:2], [100 + i for i in range(16)], device="cpu", mode="fast",
+                         storage=storage)
     a.engine.randomize(0)
     a.engine.run_round()
     p = os.path.join(tmp_path, "f.svoc")
     state.save(a, p)
     b = state.load(p)
+    assert b.engine.storage == storage and b.engine.values.dtype == a.engine.values.dtype
     assert torch.equal(a.engine.values, b.engine.values)
     assert torch.equal(a.engine.consensus, b.engine.consensus)
