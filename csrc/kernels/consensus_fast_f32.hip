@@ -43,6 +43,9 @@
 #include "svoc/sortnet.hpp"
 #include "svoc/status.hpp"
 
+#ifndef SVOC_F32_KEEP_RAW
+#define SVOC_F32_KEEP_RAW 1   // N <= 64: the raw column kept in registers across the sort networks (no re-reads)
+#endif
 #ifndef SVOC_F32_WPE
 #define SVOC_F32_WPE 1   // waves per SIMD the register budget is capped for (4: <= 128 VGPRs)
 #endif
@@ -118,6 +121,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
   constexpr int W = WAVES * P;      // columns per slab
   constexpr int NT = WAVES * 64;
   constexpr int KEEP = 64 / P;      // qr rows a lane holds after the butterfly
+  constexpr bool KEEP_RAW = SVOC_F32_KEEP_RAW && NSEG == 1;   // pass 1 without the column re-read
   __shared__ float qr_part[WAVES * NPAD];
   __shared__ float qr_lds[NPAD];
   constexpr int NM = NSEG < 4 ? 4 : NSEG;   // 64-row mask words
@@ -158,27 +162,45 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
     int nvl = nv, nll = nl;
     asm volatile("" : "+v"(nvl), "+v"(nll));   // opaque per slab: stop LICM from hoisting 64 row masks
     float c1;
-    {
-      uint32_t r[64];
-      load_col(rs, vo, rowb, r);
+    float q[64];
+    const uint32_t vcm = vc ? 0xffffffffu : 0u;
+    if constexpr (KEEP_RAW) {
+      // the raw column stays in registers across the sort: no re-read for the quadratic risk
+      uint32_t xs[64], r[64];
+      load_col(rs, vo, rowb, xs);
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
-        // arithmetic masks, no per-row branches: real -> key, rows >= N -> 0 (first lo1) / ~0
         const uint32_t mr = lt_mask(i, nvl), ml1 = lt_mask(i, nll);
-        r[i] = ((f32_key(r[i]) & mr) | (~mr & ~ml1)) ^ pol;
+        r[i] = ((f32_key(xs[i]) & mr) | (~mr & ~ml1)) ^ pol;
       }
       uint32_t lo, hi;
       col_median<NSEG, P>(r, lane, lo, hi);
       c1 = 0.5f * (key_f32(lo) + key_f32(hi));
-    }
-    if (seg == 0 && vc) p.c1[(int64_t)b * D + col] = c1;
-    __builtin_amdgcn_sched_barrier(0);
-    // quadratic risk partials of this column (math.cairo:225-238), summed over the wave's columns
-    float q[64];
-    {
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const float y = __builtin_bit_cast(float, xs[i]) - c1;
+        q[i] = fand(y * y, vcm & lt_mask(i, nvl));
+      }
+      if (seg == 0 && vc) p.c1[(int64_t)b * D + col] = c1;
+    } else {
+      {
+        uint32_t r[64];
+        load_col(rs, vo, rowb, r);
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          // arithmetic masks, no per-row branches: real -> key, rows >= N -> 0 (first lo1) / ~0
+          const uint32_t mr = lt_mask(i, nvl), ml1 = lt_mask(i, nll);
+          r[i] = ((f32_key(r[i]) & mr) | (~mr & ~ml1)) ^ pol;
+        }
+        uint32_t lo, hi;
+        col_median<NSEG, P>(r, lane, lo, hi);
+        c1 = 0.5f * (key_f32(lo) + key_f32(hi));
+      }
+      if (seg == 0 && vc) p.c1[(int64_t)b * D + col] = c1;
+      __builtin_amdgcn_sched_barrier(0);
+      // quadratic risk partials of this column (math.cairo:225-238), summed over the wave's columns
       uint32_t xr[64];
       load_col(rs, vo + after(c1), rowb, xr);
-      const uint32_t vcm = vc ? 0xffffffffu : 0u;
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         const float y = __builtin_bit_cast(float, xr[i]) - c1;
@@ -304,27 +326,50 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
       // instantiation ~250 VGPRs: the pruned 64-key network does not stream)
       // shift of the power sums: the pass-2 median (constrained) or the first reliable row's value --
       // inside the reliable cluster, and equal to every value of a constant column (zero variance exact)
-      if constexpr (CONS) {
-        uint32_t r[64];
-        load_col(rs, vo, rowb, r);
+      float s1f = 0.f, s2f = 0.f, s3f = 0.f, s4f = 0.f;
+      if constexpr (CONS && KEEP_RAW) {
+        // the raw column stays in registers across the median network: no re-read for the moments
+        uint32_t xs[64], r[64];
+        load_col(rs, vo, rowb, xs);
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
           const uint32_t mk = bit_mask(mm, i), low = bit_mask(ml, i);
-          r[i] = ((f32_key(r[i]) & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else low (0) / high (~0)
+          r[i] = ((f32_key(xs[i]) & mk) | (~low & ~mk)) ^ pol;
         }
         uint32_t lo, hi;
         col_median<NSEG, P>(r, lane, lo, hi);
         sh = 0.5f * (key_f32(lo) + key_f32(hi));
+        uint64_t mm2 = mymask;
+        asm volatile("" : "+v"(mm2));
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          const float y = fand(__builtin_bit_cast(float, xs[i]) - sh, bit_mask(mm2, i));
+          const float y2 = y * y;
+          s1f += y;
+          s2f += y2;
+          s3f = __builtin_fmaf(y2, y, s3f);
+          s4f = __builtin_fmaf(y2, y2, s4f);
+        }
       } else {
-        sh = __builtin_bit_cast(float, bload(rs, (vc ? col : 0) * 4, first_rel * rowb));
-      }
-      uint64_t mm2 = mymask;
-      asm volatile("" : "+v"(mm2));   // a fresh copy: no row mask CSE'd across the sort (64 live VGPRs)
-      __builtin_amdgcn_sched_barrier(0);
-      // shifted power sums of the reliable rows (one re-read of the column, L2-resident); y = x - sh is
-      // 0 exactly for every row of a constant column, so its variance is exactly 0, as the CPU twin's
-      float s1f = 0.f, s2f = 0.f, s3f = 0.f, s4f = 0.f;
-      {
+        if constexpr (CONS) {
+          uint32_t r[64];
+          load_col(rs, vo, rowb, r);
+#pragma unroll
+          for (int i = 0; i < 64; ++i) {
+            const uint32_t mk = bit_mask(mm, i), low = bit_mask(ml, i);
+            r[i] = ((f32_key(r[i]) & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else low (0) / high (~0)
+          }
+          uint32_t lo, hi;
+          col_median<NSEG, P>(r, lane, lo, hi);
+          sh = 0.5f * (key_f32(lo) + key_f32(hi));
+        } else {
+          sh = __builtin_bit_cast(float, bload(rs, (vc ? col : 0) * 4, first_rel * rowb));
+        }
+        uint64_t mm2 = mymask;
+        asm volatile("" : "+v"(mm2));   // a fresh copy: no row mask CSE'd across the sort (64 live VGPRs)
+        __builtin_amdgcn_sched_barrier(0);
+        // shifted power sums of the reliable rows (one re-read of the column, L2-resident); y = x - sh is
+        // 0 exactly for every row of a constant column, so its variance is exactly 0, as the CPU twin's
         uint32_t xr[64];
         load_col(rs, vo + after(sh), rowb, xr);
 #pragma unroll
