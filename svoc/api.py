@@ -192,7 +192,8 @@ class LegacyOracleConsensus(OracleConsensus):
 
     def __init__(self, admins: Sequence[int], enable_oracle_replacement: bool, required_majority: int,
                  n_failing_oracles: int, constrained: bool, unconstrained_max_spread: int, dimension: int,
-                 oracles: Sequence[int], device="cpu", mode: str = "exact", variant: str = "nd_legacy"):
+                 oracles: Sequence[int], device="cpu", mode: str = "exact", variant: str = "nd_legacy",
+                 storage=None):
         if variant not in ("nd_legacy", "1d_legacy"):
             raise ValueError("variant must be 'nd_legacy' or '1d_legacy'")
         ms = int(unconstrained_max_spread)                     # i128 constructor argument
