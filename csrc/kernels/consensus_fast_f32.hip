@@ -46,6 +46,9 @@
 #ifndef SVOC_F32_KEEP_RAW
 #define SVOC_F32_KEEP_RAW 1   // N <= 64: the raw column kept in registers across the sort networks (no re-reads)
 #endif
+#ifndef SVOC_F32_RAW_NSEG
+#define SVOC_F32_RAW_NSEG 1   // widest lane group that keeps the raw column (NSEG 2 / 4: 179 VGPRs, 2 waves)
+#endif
 #ifndef SVOC_F32_WPE
 #define SVOC_F32_WPE 1   // waves per SIMD the register budget is capped for (4: <= 128 VGPRs)
 #endif
@@ -121,7 +124,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
   constexpr int W = WAVES * P;      // columns per slab
   constexpr int NT = WAVES * 64;
   constexpr int KEEP = 64 / P;      // qr rows a lane holds after the butterfly
-  constexpr bool KEEP_RAW = SVOC_F32_KEEP_RAW && NSEG == 1;   // pass 1 without the column re-read
+  constexpr bool KEEP_RAW = SVOC_F32_KEEP_RAW && NSEG <= SVOC_F32_RAW_NSEG;   // pass 1 without the column re-read
   __shared__ float qr_part[WAVES * NPAD];
   __shared__ float qr_lds[NPAD];
   constexpr int NM = NSEG < 4 ? 4 : NSEG;   // 64-row mask words
