@@ -106,3 +106,13 @@ def test_bench_gpus_world_mismatch_fails(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config-file", cfg, "--gpus", "2",
                         "--steps", "2", "--warmup", "0"], capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_bench_fp32_storage_cpu(tmp_path):
+    """bench.py --storage fp32: the fast engine over fp32 storage (CPU twin here), dtype reported."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config-file", _cpu_cfg(tmp_path),
+                        "--storage", "fp32", "--steps", "4", "--warmup", "1"], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["dtype"] == "fp32-storage" and out["value"] > 0 and out["config"]["ok_fraction"] == 1.0
