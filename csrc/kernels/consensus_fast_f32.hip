@@ -47,7 +47,7 @@
 #define SVOC_F32_KEEP_RAW 1   // N <= 64: the raw column kept in registers across the sort networks (no re-reads)
 #endif
 #ifndef SVOC_F32_RAW_NSEG
-#define SVOC_F32_RAW_NSEG 1   // widest lane group that keeps the raw column (NSEG 2 / 4: 179 VGPRs, 2 waves)
+#define SVOC_F32_RAW_NSEG 16   // lane groups that keep the raw column in pass 1 (all: fewer waves, still faster)
 #endif
 #ifndef SVOC_F32_WPE
 #define SVOC_F32_WPE 1   // waves per SIMD the register budget is capped for (4: <= 128 VGPRs)
