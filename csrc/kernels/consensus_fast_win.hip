@@ -41,6 +41,11 @@
 #ifndef SVOC_WIN_NT_REREAD
 #define SVOC_WIN_NT_REREAD 0
 #endif
+// SVOC_WIN_KEEP_RAW=1: the half of each slab that is not staged in LDS stays in 32 VGPRs across the
+// pass-1 window network (no qr re-read from memory), at 3 waves per SIMD instead of 4
+#ifndef SVOC_WIN_KEEP_RAW
+#define SVOC_WIN_KEEP_RAW 0
+#endif
 
 namespace svoc {
 
@@ -143,17 +148,22 @@ SVOC_DEV void qr_moments(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t m
 // i % 4 < 2, 32 rows) were written to the wave's LDS region as keys right after the pass-1 load; trees
 // 2 and 3 (32 rows) are re-read from memory, all 32 loads issued first so their latency overlaps the
 // LDS trees.  Same trees, same order of accumulation as qr_moments: bit-identical results.
-template <int P, bool MASKW>
+template <int P, bool MASKW, bool RAW = false>
 SVOC_DEV void qr_moments_staged(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, uint32_t kp,
                                 const uint32_t* st, int lane, const QrCtx& c, float* acc, f32x2& s1, f32x2& s2,
-                                f32x2& s3, f32x2& s4) {
+                                f32x2& s3, f32x2& s4, const uint32_t* kr = nullptr) {
   static_assert(P == 16, "staging layout: KEEP = 4 trees of 16 rows");
   constexpr int KEEP = 4, S = 4;
-  uint32_t wm[64];   // trees 2 and 3 from memory (indices i % 4 >= 2)
+  uint32_t wm[64];   // trees 2 and 3 from memory (indices i % 4 >= 2), or kept in registers (RAW)
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
-    wm[2 + KEEP * m] = bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (2 + KEEP * m) * rowb);
-    wm[3 + KEEP * m] = bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (3 + KEEP * m) * rowb);
+    if constexpr (RAW) {
+      wm[2 + KEEP * m] = kr[2 * m];
+      wm[3 + KEEP * m] = kr[2 * m + 1];
+    } else {
+      wm[2 + KEEP * m] = bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (2 + KEEP * m) * rowb);
+      wm[3 + KEEP * m] = bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (3 + KEEP * m) * rowb);
+    }
   }
   {
     uint32_t wv[64];
@@ -192,16 +202,17 @@ SVOC_DEV void qr_moments_staged(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uin
 // in-flight loads; the first butterfly half of the single tree when KEEP = 1) come from the wave's
 // LDS region, the odd rows are re-read from memory with all 32 loads issued before the LDS reads.
 // Same trees, same leaf order as qr_moments: bit-identical results.
-template <int P, bool MASKW>
+template <int P, bool MASKW, bool RAW = false>
 SVOC_DEV void qr_moments_staged_even(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, uint32_t kp,
                                      const uint32_t* st, int lane, const QrCtx& c, float* acc, f32x2& s1,
-                                     f32x2& s2, f32x2& s3, f32x2& s4) {
+                                     f32x2& s2, f32x2& s3, f32x2& s4, const uint32_t* kr = nullptr) {
   constexpr int KEEP = 64 / P, S = __builtin_ctz(P);
   static_assert(KEEP <= 2, "even-row staging: one or two trees");
   if constexpr (KEEP == 1) {
     uint32_t wv[64];
 #pragma unroll
-    for (int m = 0; m < 32; ++m) wv[2 * m + 1] = bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (2 * m + 1) * rowb);
+    for (int m = 0; m < 32; ++m)
+      wv[2 * m + 1] = RAW ? kr[m] : bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (2 * m + 1) * rowb);
 #pragma unroll
     for (int m = 0; m < 32; ++m) wv[2 * m] = st[m * 64 + lane] ^ kp;
     if (MASKW) {
@@ -210,9 +221,10 @@ SVOC_DEV void qr_moments_staged_even(__amdgpu_buffer_rsrc_t rs, int vo, int rowb
     }
     acc[0] += qr_tree<S, 0, P, false>(c, wv, s1, s2, s3, s4);
   } else {
-    uint32_t wm[64];   // tree 1 (odd rows) from memory, loads issued first
+    uint32_t wm[64];   // tree 1 (odd rows) from memory, loads issued first (or kept in registers: RAW)
 #pragma unroll
-    for (int m = 0; m < 32; ++m) wm[2 * m + 1] = bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (2 * m + 1) * rowb);
+    for (int m = 0; m < 32; ++m)
+      wm[2 * m + 1] = RAW ? kr[m] : bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (2 * m + 1) * rowb);
     {
       uint32_t wv[64];
 #pragma unroll
@@ -232,7 +244,7 @@ SVOC_DEV void qr_moments_staged_even(__amdgpu_buffer_rsrc_t rs, int vo, int rowb
 }
 
 template <int NSEG, int WAVES, int H, bool CONS, int MODE>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4))) void consensus_fast_win_kernel(FastParams p) {
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC_WIN_KEEP_RAW ? 3 : 4))) void consensus_fast_win_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // column pairs per wave (phase A)
   constexpr int NPAD = 64 * NSEG;
   constexpr int W = WAVES * P * 2;      // columns per workgroup step (phase A)
@@ -278,6 +290,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   float acc[KEEP];
 #pragma unroll
   for (int i = 0; i < KEEP; ++i) acc[i] = 0.f;
+  constexpr bool RAW = SVOC_WIN_KEEP_RAW && STAGE && (NSEG == 4 || NSEG == 1);
 
   // ------------------------------------------------------------ phase A: pass 1
   const int pass1_slabs = MODE == 2 ? 0 : nslab;
@@ -291,6 +304,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
     asm volatile("" : "+v"(nvl), "+v"(nll));
     float cA, cB;
     const uint32_t mW = vA ? (vB ? 0xffffffffu : 0x0000ffffu) : 0u;
+    uint32_t kr[RAW ? 32 : 1];   // the rows not staged in LDS, raw (RAW: no qr re-read)
     {
       u16x2 r[64];
       if (N == NPAD) {
@@ -307,10 +321,17 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
             for (int m = 0; m < 16; ++m) {
               stw[(2 * m) * 64 + lane] = as_u32(r[4 * m]);
               stw[(2 * m + 1) * 64 + lane] = as_u32(r[4 * m + 1]);
+              if constexpr (RAW) {
+                kr[2 * m] = as_u32(r[4 * m + 2]) ^ kp;
+                kr[2 * m + 1] = as_u32(r[4 * m + 3]) ^ kp;
+              }
             }
           } else if constexpr (STAGE) {
 #pragma unroll
-            for (int m = 0; m < 32; ++m) stw[m * 64 + lane] = as_u32(r[2 * m]);
+            for (int m = 0; m < 32; ++m) {
+              stw[m * 64 + lane] = as_u32(r[2 * m]);
+              if constexpr (RAW) kr[m] = as_u32(r[2 * m + 1]) ^ kp;
+            }
           }
         } else {
 #pragma unroll
@@ -361,11 +382,11 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
     f32x2 s1 = {0.f, 0.f}, s2 = s1, s3 = s1, s4 = s1;
     if (STAGE && N == NPAD) {
       if constexpr (STAGE && NSEG == 4) {
-        if ((s + 1) * W <= D) qr_moments_staged<P, false>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
-        else qr_moments_staged<P, true>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
+        if ((s + 1) * W <= D) qr_moments_staged<P, false, RAW>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4, kr);
+        else qr_moments_staged<P, true, RAW>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4, kr);
       } else if constexpr (STAGE) {
-        if ((s + 1) * W <= D) qr_moments_staged_even<P, false>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
-        else qr_moments_staged_even<P, true>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
+        if ((s + 1) * W <= D) qr_moments_staged_even<P, false, RAW>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4, kr);
+        else qr_moments_staged_even<P, true, RAW>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4, kr);
       }
     } else if ((s + 1) * W <= D) {
       if (N == NPAD) qr_moments<P, false, false>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
