@@ -53,6 +53,25 @@ SVOC_DEV uint32_t wload(__amdgpu_buffer_rsrc_t rs, int voff, int soff, uint32_t&
   }
 }
 
+// Low 32-bit words of the lane's 64 rows of one column (int32 values, or the low word of int64 values
+// whose high words pass 1 / the first pass-2 read validated), every load issued before any is
+// consumed.  Written inline, each re-read loop waited on its load before issuing the next (one load in
+// flight); the opaque stride keeps the 64 row soffsets from being hoisted into live SGPRs.
+SVOC_DEV void load_lo(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t (&x)[64]) {
+  asm volatile("" : "+s"(rowb));
+#pragma unroll
+  for (int i = 0; i < 64; ++i) x[i] = bload(rs, vo, i * rowb);
+  __builtin_amdgcn_sched_barrier(0);
+}
+// The re-read offset made to depend on v (empty asm, as the window kernel's vo2): the loads cannot be
+// issued before v exists.  Without it LLVM hoists every re-read above the sort network (nothing else
+// orders them) and holds 256 loaded words at once.
+template <class T>
+SVOC_DEV int after(int vo, T v) {
+  asm volatile("" : "+v"(vo) : "v"(v));
+  return vo;
+}
+
 // Transposing butterfly over the wave's P columns (the fast kernels' qr tree, exact u32 sums):
 // stage L exchanges with lane ^ (P >> L); the lane ends with rows I + base(lane) of all P columns.
 template <int L, int I, int P>
@@ -93,6 +112,9 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   constexpr int NT = WAVES * 64;
   constexpr int KEEP = 64 / P;      // qr rows a lane holds after the butterfly
   constexpr int ESZ = V32 ? 4 : 8;
+  // re-reads issued as 64-load batches ordered after the value they need (load_lo / after): +37% at
+  // 256 x 4096; the N <= 64 kernel keeps the inline loops (the batches cost it a wave per SIMD: -18%)
+  constexpr bool BATCH = NSEG >= 2;
   __shared__ uint64_t qr_part[WAVES * NPAD];
   __shared__ uint64_t qr_lds[NPAD];
   __shared__ uint64_t relmask[4], lowmask[4];
@@ -151,10 +173,19 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     // quadratic risk (math.cairo:225-238): this column's qdev of every row, summed over the columns
     uint32_t q[64];
     const double cd = (double)c1;
+    if constexpr (BATCH) {
+      load_lo(rs, after(vo, c1), rowb, q);
 #pragma unroll
-    for (int i = 0; i < 64; ++i) {
-      const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
-      q[i] = (vc && i < nv) ? (uint32_t)qdev_d((double)x, cd) : 0u;
+      for (int i = 0; i < 64; ++i) {
+        if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bound the fp64 temporaries in flight
+        q[i] = (vc && i < nv) ? (uint32_t)qdev_d((double)q[i], cd) : 0u;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
+        q[i] = (vc && i < nv) ? (uint32_t)qdev_d((double)x, cd) : 0u;
+      }
     }
     qtree_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
   }
@@ -270,13 +301,23 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     uint32_t cons;
     {
       uint32_t r[64];
+      if constexpr (BATCH && (MODE != 2 || V32)) {   // values validated in pass 1 (or 32-bit): one batch
+        load_lo(rs, vo, rowb, r);
 #pragma unroll
-      for (int i = 0; i < 64; ++i) {
-        uint32_t hw;
-        const uint32_t x = wload<V32>(rs, vo, i * rowb, hw);
-        if (MODE == 2) badv |= (vc && i < nv && (x > kWsadMax || hw != 0)) ? 1u : 0u;   // no pass 1 here
-        const uint32_t mk = bit_mask(mm, i), low = bit_mask(ml, i);
-        r[i] = ((x & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else -inf (low) / +inf
+        for (int i = 0; i < 64; ++i) {
+          if (MODE == 2) badv |= (vc && i < nv && r[i] > kWsadMax) ? 1u : 0u;   // no pass 1 here
+          const uint32_t mk = bit_mask(mm, i), low = bit_mask(ml, i);
+          r[i] = ((r[i] & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else -inf (low) / +inf
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          uint32_t hw;
+          const uint32_t x = wload<V32>(rs, vo, i * rowb, hw);
+          if (MODE == 2) badv |= (vc && i < nv && (x > kWsadMax || hw != 0)) ? 1u : 0u;   // no pass 1 here
+          const uint32_t mk = bit_mask(mm, i), low = bit_mask(ml, i);
+          r[i] = ((x & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else -inf (low) / +inf
+        }
       }
       uint32_t lo, hi;
       median_group<NSEG>(r, lo, hi);
@@ -286,17 +327,33 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     // the column is re-read per statistic (L2-hot) instead of held in 64 more VGPRs: the fp64 work
     // below needs the registers, and occupancy hides the re-read latency
     // mean (math.cairo:240-254): idiv(sum, R) of non-negative values
+    uint32_t xr[64];
     uint32_t sx = 0;
+    if constexpr (BATCH) {
+      load_lo(rs, after(vo, cons), rowb, xr);
+#pragma unroll
+      for (int i = 0; i < 64; ++i) sx += xr[i] & bit_mask(mm, i);
+    } else {
 #pragma unroll 16
-    for (int i = 0; i < 64; ++i) sx += wload<V32>(rs, vo, i * rowb, hw_) & bit_mask(mm, i);
+      for (int i = 0; i < 64; ++i) sx += wload<V32>(rs, vo, i * rowb, hw_) & bit_mask(mm, i);
+    }
     sx = group_sum<NSEG, P>(sx);
     const double mu = floor_div_d((double)sx, Rd, invR);
     // population variance (math.cairo:208-222): mean of qdev(x, mu) over the reliable rows
     uint32_t sv = 0;
+    if constexpr (BATCH) {
+      load_lo(rs, after(vo, mu), rowb, xr);
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
+        sv += bit_mask(mm, i) & (uint32_t)qdev_d((double)xr[i], mu);
+      }
+    } else {
 #pragma unroll 16
-    for (int i = 0; i < 64; ++i) {
-      const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
-      sv += bit_mask(mm, i) & (uint32_t)qdev_d((double)x, mu);
+      for (int i = 0; i < 64; ++i) {
+        const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
+        sv += bit_mask(mm, i) & (uint32_t)qdev_d((double)x, mu);
+      }
     }
     sv = group_sum<NSEG, P>(sv);
     const double var = floor_div_d((double)sv, Rd, invR);
@@ -307,15 +364,25 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     const double isd = 1.0 / sd;
     // z-score powers (math.cairo:320-363), reliable rows only (a masked row has z = 0: all powers 0)
     double s3 = 0.0, s4 = 0.0;
-#pragma unroll 8
-    for (int i = 0; i < 64; ++i) {
-      const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
-      const double dx = bit_mask(mm, i) ? (double)x - mu : 0.0;
+    // z-score powers of one row (a masked row has z = 0: all powers 0)
+    auto zpow = [&](uint32_t x, uint32_t mk) {
+      const double dx = mk ? (double)x - mu : 0.0;
       const double z = wdiv_d(dx, sd, isd);
       const double z2 = wmul_d(z, z);
       bad = bad || z2 >= 33554432.0;   // 2^25: keeps every product below wmul_d's 2^50 bound
       s3 += wmul_d(z2, z);
       s4 += wmul_d(z2, z2);
+    };
+    if constexpr (BATCH) {
+      load_lo(rs, after(vo, sd), rowb, xr);
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bound the fp64 temporaries in flight
+        zpow(xr[i], bit_mask(mm, i));
+      }
+    } else {
+#pragma unroll 8
+      for (int i = 0; i < 64; ++i) zpow(wload<V32>(rs, vo, i * rowb, hw_), bit_mask(mm, i));
     }
     s3 = group_sum<NSEG, P>(s3);
     s4 = group_sum<NSEG, P>(s4);
