@@ -34,6 +34,10 @@
 #include "svoc/wsad.hpp"
 #include "svoc/wsad_fast.hpp"
 
+#ifndef SVOC_WSAD_BATCH_QR
+#define SVOC_WSAD_BATCH_QR 1   // N <= 64 too: batched qr / mean re-reads (226 VGPRs, c2 exact +27%)
+#endif
+
 namespace svoc {
 
 constexpr uint32_t kWsadMax = 1000000u;
@@ -113,8 +117,10 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   constexpr int KEEP = 64 / P;      // qr rows a lane holds after the butterfly
   constexpr int ESZ = V32 ? 4 : 8;
   // re-reads issued as 64-load batches ordered after the value they need (load_lo / after): +37% at
-  // 256 x 4096; the N <= 64 kernel keeps the inline loops (the batches cost it a wave per SIMD: -18%)
+  // 256 x 4096; the N <= 64 kernel batches the qr and mean re-reads only (+27% at 64 x 1024): batching
+  // the fp64 variance / z-power re-reads too costs it a wave per SIMD (-18%)
   constexpr bool BATCH = NSEG >= 2;
+  constexpr bool BATCH1 = BATCH || SVOC_WSAD_BATCH_QR;   // the qr and mean re-reads only (no fp64 temporaries)
   __shared__ uint64_t qr_part[WAVES * NPAD];
   __shared__ uint64_t qr_lds[NPAD];
   __shared__ uint64_t relmask[4], lowmask[4];
@@ -173,7 +179,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     // quadratic risk (math.cairo:225-238): this column's qdev of every row, summed over the columns
     uint32_t q[64];
     const double cd = (double)c1;
-    if constexpr (BATCH) {
+    if constexpr (BATCH1) {
       load_lo(rs, after(vo, c1), rowb, q);
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
@@ -329,7 +335,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     // mean (math.cairo:240-254): idiv(sum, R) of non-negative values
     uint32_t xr[64];
     uint32_t sx = 0;
-    if constexpr (BATCH) {
+    if constexpr (BATCH1) {
       load_lo(rs, after(vo, cons), rowb, xr);
 #pragma unroll
       for (int i = 0; i < 64; ++i) sx += xr[i] & bit_mask(mm, i);
