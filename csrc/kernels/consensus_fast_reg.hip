@@ -16,12 +16,16 @@
 #include "svoc/sortnet.hpp"
 #include "svoc/status.hpp"
 
+#ifndef SVOC_REG_WIDE_BATCH
+#define SVOC_REG_WIDE_BATCH 0   // N > 256: batched qr re-read, 2 waves per SIMD
+#endif
+
 namespace svoc {
 
 // MODE 0: fused round; 1: pass 1 only (c1 + qr -> global); 2: rank + pass 2 from the global qr
 // (D-sharding: the caller all-reduces the qr partials in between).
 template <int NSEG, int WAVES, bool CONS, int MODE, bool RAW = false>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW ? 2 : 4))) void consensus_fast_reg_kernel(FastParams p) {
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((RAW || (SVOC_REG_WIDE_BATCH && NSEG >= 8)) ? 2 : 4))) void consensus_fast_reg_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // column pairs per wave
   constexpr int NPAD = 64 * NSEG;       // padded oracle rows
   constexpr int W = WAVES * P * 2;      // columns per workgroup step
@@ -118,7 +122,24 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW 
     __builtin_amdgcn_sched_barrier(0);
     float part[64];
     const f32x2 c2 = {vA ? cA : 0.f, vB ? cB : 0.f};
-    if (RAW || (s + 1) * W > D) {  // slab with columns past D (uniform): masked words
+    constexpr bool WB = SVOC_REG_WIDE_BATCH && NSEG >= 8 && !RAW;
+    if constexpr (WB) {
+      // wide groups: the re-read as one batch of 64 loads ordered after the network's result (empty
+      // asm); written inline it kept two loads in flight
+      uint32_t wv[64];
+      int vo2 = vo;
+      asm volatile("" : "+v"(vo2) : "v"(cA), "v"(cB));
+#pragma unroll
+      for (int i = 0; i < 64; ++i) wv[i] = bload(rs, vo2, i * rowb);
+      __builtin_amdgcn_sched_barrier(0);
+      const uint32_t mm = (s + 1) * W > D ? mW : 0xffffffffu;
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const f32x2 y = bf16x2_to_f32x2(wv[i] & mm) - c2;
+        const f32x2 q = y * y;
+        part[i] = q.x + q.y;
+      }
+    } else if (RAW || (s + 1) * W > D) {  // slab with columns past D (uniform): masked words
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         const uint32_t w = RAW ? wraw[i] : bload(rs, vo, i * rowb) & mW;  // else: L2/MALL-hot re-read
