@@ -34,7 +34,8 @@ struct FastParams {
   int work_fresh;           // the workspace holds no pass-1 state (mode 2 must not use the window kernel)
 };
 
-// Workspace per instance of the LDS-free fast kernels, in u32 words (Dp = fast_work_pairs(D)):
+// Workspace per instance of the LDS-free fast kernels, in u32 words (Dp = fast_work_pairs(D)).
+// bf16 kernels (column pairs):
 //   [17][2][Dp]  window keys (consensus_fast_win.hip; H = 17 upper bound)
 //   [4][Dp]      float2 all-row power sums
 //   [2 Dp]       cleanup column list
@@ -42,10 +43,24 @@ struct FastParams {
 //                copies them to the outputs only once its status is known to be OK, so a reverted
 //                round leaves every output untouched (contract.cairo:588-603: a failed assert
 //                reverts the whole transaction)
+// fp32 window kernel (consensus_fast_winf.hip, one column per lane, Dc = 2 Dp columns):
+//   [17][2][Dc] window keys, [4][Dc] power sums, [Dc] cleanup list, [3][Dc] staged outputs
+//   (at word kWinfStageCols * Dc)
 inline int64_t fast_work_pairs(int64_t D) { return ((D + 1) / 2 + 255) / 256 * 256; }
 inline int64_t fast_work_stage_word(int64_t D) { return fast_work_pairs(D) * (2 * 17 + 8 + 2); }
-inline int64_t fast_work_words(int64_t D) { return fast_work_pairs(D) * (2 * 17 + 8 + 2 + 6); }
+constexpr int kWinfStageCols = 2 * 17 + 4 + 1;
+inline int64_t fast_work_words(int64_t D) { return fast_work_pairs(D) * 2 * (kWinfStageCols + 3); }
 inline int64_t fast_work_numel(int64_t B, int64_t D) { return B * fast_work_words(D); }
+
+// Window half-width of the one-network kernels for (N, f): the smallest H in {5, 17} with a + 1 <= H
+// and f - a + 1 <= H (a = N/2 - R/2: the pass-2 middle pair sits f - a ranks above / a ranks below the
+// pass-1 one at most); 0 when neither fits.
+inline int fast_win_h(int N, int f) {
+  const int R = N - f, a = N / 2 - R / 2;
+  if (a + 1 <= 5 && f - a + 1 <= 5) return 5;
+  if (a + 1 <= 17 && f - a + 1 <= 17) return 17;
+  return 0;
+}
 
 struct ExactParams {
   const void* values;       // [B, N, D] wsad, int64 (or int32 when val32)
@@ -86,6 +101,7 @@ extern "C" {
 typedef struct ihipStream_t* hipStream_t;
 int svoc_fast_round_bf16(const svoc::FastParams* p, hipStream_t stream);
 int svoc_fast_round_f32(const svoc::FastParams* p, hipStream_t stream);   // values fp32 [B, N, ld]
+int svoc_fast_round_f32_win(const svoc::FastParams* p, hipStream_t stream);
 int svoc_exact_round(const svoc::ExactParams* p, hipStream_t stream);
 }
 

@@ -53,6 +53,12 @@ SVOC_DEV uint32_t key_to_bf16x2(u16x2 k) {
 SVOC_DEV u16x2 pos_to_key(uint32_t raw) { return as_k(raw ^ 0x80008000u); }
 SVOC_DEV uint32_t key_to_pos(u16x2 k) { return as_u32(k) ^ 0x80008000u; }
 
+// fp32 bits <-> monotone u32 key (negative values: all bits flipped; positive: sign bit set)
+SVOC_DEV uint32_t f32_key(uint32_t u) { return u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u); }
+SVOC_DEV float key_f32(uint32_t k) {
+  return __builtin_bit_cast(float, k ^ ((uint32_t)((int32_t)~k >> 31) | 0x80000000u));
+}
+
 SVOC_DEV float bf16_lo(uint32_t w) { return __builtin_bit_cast(float, w << 16); }
 SVOC_DEV float bf16_hi(uint32_t w) { return __builtin_bit_cast(float, w & 0xffff0000u); }
 SVOC_DEV float fand(float x, uint32_t m) { return __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, x) & m); }
@@ -393,51 +399,51 @@ SVOC_DEV void median_group_wide(K (&r)[64], int seg, int lane, K& lo, K& hi) {
 // on the way in (~0 when the upper lane is in the opposite polarity), `ox` / `oy` into the minima /
 // maxima on the way out (the output polarity of the lower / upper lane).  xhc_swap<XM> is
 // xhc_pol<XM>(r, ~0u, 0, 0).
-template <int XM>
-SVOC_DEV void xhc_pol(u16x2 (&r)[64], uint32_t iy, uint32_t ox, uint32_t oy) {
+template <int XM, class K>
+SVOC_DEV void xhc_pol(K (&r)[64], uint32_t iy, uint32_t ox, uint32_t oy) {
 #pragma unroll
   for (int k = 0; k < 32; ++k) {
     uint32_t x = as_u32(r[2 * k]), y = as_u32(r[2 * k + 1]);
     xswap<XM>(x, y);
     y ^= iy;
-    const u16x2 lo = kmin(as_k(x), as_k(y)), hi = kmax(as_k(x), as_k(y));
+    const K lo = kmin(key_from<K>(x), key_from<K>(y)), hi = kmax(key_from<K>(x), key_from<K>(y));
     x = as_u32(lo) ^ ox;
     y = as_u32(hi) ^ oy;
     xswap<XM>(x, y);
-    r[2 * k] = as_k(x);
-    r[2 * k + 1] = as_k(y);
+    r[2 * k] = key_from<K>(x);
+    r[2 * k + 1] = key_from<K>(y);
   }
 }
 
 // The top H = 2^k + 1 keys of a bitonic in-lane sequence of 64, ascending: out[0] is the H-th
 // largest, out[H-1] the maximum.  Max-only half-cleaners down to 2K = 2(H-1) keys, one split into
 // the top K (sorted by a half-cleaner cascade) and the rest (whose maximum is the H-th largest).
-template <int H>
-SVOC_DEV void bitonic_top(const u16x2 (&r)[64], u16x2 (&out)[H]) {
-  constexpr int K = H - 1;
-  static_assert(K >= 2 && K <= 32 && (K & (K - 1)) == 0, "H = 2^k + 1, at most 33");
-  u16x2 t[64];
+template <int H, class K>
+SVOC_DEV void bitonic_top(const K (&r)[64], K (&out)[H]) {
+  constexpr int KT = H - 1;
+  static_assert(KT >= 2 && KT <= 32 && (KT & (KT - 1)) == 0, "H = 2^k + 1, at most 33");
+  K t[64];
 #pragma unroll
   for (int i = 0; i < 64; ++i) t[i] = r[i];
 #pragma unroll
-  for (int n = 64; n > 2 * K; n >>= 1) {
+  for (int n = 64; n > 2 * KT; n >>= 1) {
 #pragma unroll
     for (int i = 0; i < n / 2; ++i) t[i] = kmax(t[i], t[i + n / 2]);
   }
-  u16x2 mx = kmin(t[0], t[K]);
+  K mx = kmin(t[0], t[KT]);
 #pragma unroll
-  for (int i = 0; i < K; ++i) {
-    const u16x2 a = t[i], b = t[i + K];
+  for (int i = 0; i < KT; ++i) {
+    const K a = t[i], b = t[i + KT];
     if (i) mx = kmax(mx, kmin(a, b));
     t[i] = kmax(a, b);
   }
 #pragma unroll
-  for (int j = K / 2; j > 0; j >>= 1) {
+  for (int j = KT / 2; j > 0; j >>= 1) {
 #pragma unroll
-    for (int i = 0; i < K; ++i) {
+    for (int i = 0; i < KT; ++i) {
       const int l = i ^ j;
       if (l > i) {
-        const u16x2 a = t[i], b = t[l];
+        const K a = t[i], b = t[l];
         t[i] = kmin(a, b);
         t[l] = kmax(a, b);
       }
@@ -445,7 +451,7 @@ SVOC_DEV void bitonic_top(const u16x2 (&r)[64], u16x2 (&out)[H]) {
   }
   out[0] = mx;
 #pragma unroll
-  for (int i = 0; i < K; ++i) out[i + 1] = t[i];
+  for (int i = 0; i < KT; ++i) out[i + 1] = t[i];
 }
 
 // Sorted-position window around the middle of the group's 64*NSEG keys (r holds keys XOR
@@ -455,10 +461,10 @@ SVOC_DEV void bitonic_top(const u16x2 (&r)[64], u16x2 (&out)[H]) {
 // NSEG 1: both parts in the lane (w holds w0 then w1, 2H keys).  NSEG 2: part 0 in seg 0, part 1 in
 // seg 1.  NSEG 4: part 0 in seg 1, part 1 in seg 2 (segs 0 and 3 compute discarded keys).  lo / hi
 // (the middle pair, positions c - 1 and c, true keys) are returned in every lane of the group.
-template <int NSEG, int P, int H>
-SVOC_DEV void window_group(u16x2 (&r)[64], int seg, int lane, u16x2 (&w)[NSEG == 1 ? 2 * H : H], u16x2& lo,
-                           u16x2& hi) {
-  sort64_oem(r);
+// (K: u16x2 = two bf16 columns per register, uint32_t = one fp32 column: consensus_fast_winf.hip)
+template <int NSEG, int P, int H, class K>
+SVOC_DEV void window_group(K (&r)[64], int seg, int lane, K (&w)[NSEG == 1 ? 2 * H : H], K& lo, K& hi) {
+  sort_oem<64>(r);
   if constexpr (NSEG == 1) {
 #pragma unroll
     for (int m = 0; m < H; ++m) {

@@ -55,12 +55,6 @@
 
 namespace svoc {
 
-// fp32 bits <-> monotone u32 key (negative values: all bits flipped; positive: sign bit set)
-SVOC_DEV uint32_t f32_key(uint32_t u) { return u ^ ((uint32_t)((int32_t)u >> 31) | 0x80000000u); }
-SVOC_DEV float key_f32(uint32_t k) {
-  return __builtin_bit_cast(float, k ^ ((uint32_t)((int32_t)~k >> 31) | 0x80000000u));
-}
-
 // Transposing butterfly over the wave's P columns: stage L exchanges with lane ^ (P >> L); the lane
 // ends with rows I + base(lane) summed over all P columns.
 template <int L, int I, int P>
@@ -527,6 +521,12 @@ extern "C" int svoc_fast_round_f32(const FastParams* p, hipStream_t stream) {
   if ((int64_t)p->N * p->ld * 4 >= (1ll << 31)) return -1;   // 32-bit buffer offsets
   if (p->mode != 1 && (!p->work || p->work_pairs < fast_work_pairs(p->D) || p->work_stride < fast_work_words(p->D)))
     return -1;   // pass 2 stages its outputs in the workspace
+  // default: the one-network window kernel (consensus_fast_winf.hip) where it applies; wave_hint -7
+  // forces this two-network kernel (tests cross-check the two)
+  if (p->wave_hint != -7) {
+    const int rc = svoc_fast_round_f32_win(p, stream);
+    if (rc != -2) return rc;
+  }
   if (p->N <= 64) return launch_f32<1>(*p, stream);
   if (p->N <= 128) return launch_f32<2>(*p, stream);
   if (p->N <= 256) return launch_f32<4>(*p, stream);

@@ -533,9 +533,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
       const int pr = pair < npairs ? pair : npairs - 1;
       bool cA = pair < npairs, cB = pair < npairs && 2 * pair + 1 < D;
       if (inwin) {
-        const uint32_t lo = bload(ws, pr * 4, 0), hi = ~bload(ws, (Dp + pr) * 4, 0);
-        cA = cA && ((lo ^ hi) & 0xffffu) == 0;
-        cB = cB && ((lo ^ hi) >> 16) == 0;
+        // compared as values: a run of +0.0 and -0.0 is constant, but its keys differ
+        const uint32_t lo = key_to_pos(as_k(bload(ws, pr * 4, 0))), hi = key_to_pos(~as_k(bload(ws, (Dp + pr) * 4, 0)));
+        cA = cA && bf16_lo(lo) == bf16_lo(hi);
+        cB = cB && bf16_hi(lo) == bf16_hi(hi);
       }
       if (__ballot(cA || cB)) {   // rare: compare the reliable rows with the first one
         const uint32_t w0 = bload(rs, pr * 4, fr * rowb);
@@ -811,14 +812,6 @@ static void launch_win(const FastParams& p, int H, hipStream_t stream) {
   else launch_win_c<NSEG, 17, true>(p, stream);
 }
 
-// Window half-width for (N, f): the smallest H in {5, 17} with a + 1 <= H and f - a + 1 <= H.
-static int win_h(int N, int f) {
-  const int R = N - f, a = N / 2 - R / 2;
-  if (a + 1 <= 5 && f - a + 1 <= 5) return 5;
-  if (a + 1 <= 17 && f - a + 1 <= 17) return 17;
-  return 0;
-}
-
 }  // namespace svoc
 
 using namespace svoc;
@@ -829,7 +822,7 @@ extern "C" int svoc_fast_round_bf16_win(const FastParams* p, hipStream_t stream)
   if (!p->work || p->N < 2 || p->N > 256 || p->ld % 8 != 0 || p->D > p->ld) return -2;
   if (p->mode == 2 && p->work_fresh) return -2;   // pass 1 ran elsewhere: no windows to read
   if (p->n_failing < 0 || p->n_failing > 32 || p->n_failing > p->N - 2) return -2;
-  const int H = win_h(p->N, p->n_failing);
+  const int H = fast_win_h(p->N, p->n_failing);
   if (H == 0) return -2;
   if (p->work_pairs < fast_work_pairs(p->D) || p->work_pairs % 256 != 0 || p->work_stride < fast_work_words(p->D))
     return -1;

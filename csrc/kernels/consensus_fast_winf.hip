@@ -1,0 +1,763 @@
+// Fused two-pass robust consensus over fp32 STORAGE (reference resolution), "window" variant: ONE
+// sorting network and ONE read of the instance per round.
+//
+// Semantics: contract/src/contract.cairo:442-503 (constrained) / :370-434 (unconstrained), in the fast
+// engine's real-unit form (csrc/engine/reference_cpu.cpp fast_round_one, the CPU twin).  Same algorithm
+// as the bf16 window kernel (consensus_fast_win.hip:1-26), on 32-bit keys, one column per lane:
+//   pass 1 (phase A): per column, the 64*NSEG rows of a lane group (NSEG = ceil(N / 64) lanes x 64
+//     rows) go through the in-register median network extended to keep H keys on either side of the
+//     median (window_group, sortnet.hpp) -> c1 (math.cairo:113-126) and the window, written to the
+//     workspace; the qr loop (math.cairo:225-238) also accumulates the all-row power sums of
+//     d = x - c1 (packed over row pairs: v_pk_fma_f32);
+//   rank mask: sort by (qr asc, idx desc) (sort.cairo:96-101), the first R = N - f are reliable
+//     (contract.cairo:345-363);
+//   pass 2 (phase B, one lane per column): only the f removed rows are read.  The pass-2 smooth median
+//     over the R reliable rows (contract.cairo:476-480) is an order statistic of the FULL column shifted
+//     by at most f ranks, so it is read off the window by ranking the sorted removed keys against it;
+//     the reliable rows' power sums are the all-row sums minus the removed rows' (fp64 combination),
+//     with an exact two-pass recomputation for columns where that difference would cancel.
+// Versus consensus_fast_f32.hip (the two-network kernel): no second 64*NSEG-key network and no second
+// read of the instance.  HBM per round: the pass-1 read, half of it re-read for the qr pass (the other
+// half staged in LDS, constrained), the window round trip and the f removed rows.
+// Valid for f <= 32 with a + 1 <= H and f - a + 1 <= H (a = N/2 - R/2, H = 5 or 17); the dispatcher
+// falls back to consensus_fast_f32.hip otherwise.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <utility>
+
+#include "svoc/bufload.hpp"
+#include "svoc/launch.hpp"
+#include "svoc/sortnet.hpp"
+#include "svoc/status.hpp"
+
+namespace svoc {
+
+// Constrained keys: values validated to [0, 1] (sign bit clear, or -0.0: key 0, just below +0.0) ->
+// key = bits ^ 0x80000000, one XOR each way.  General keys: f32_key / key_f32.
+template <bool CONS>
+SVOC_DEV uint32_t fkey(uint32_t raw) {
+  if constexpr (CONS) return raw ^ 0x80000000u;
+  else return f32_key(raw);
+}
+template <bool CONS>
+SVOC_DEV float fkey_val(uint32_t k) {
+  if constexpr (CONS) return __builtin_bit_cast(float, k ^ 0x80000000u);
+  else return key_f32(k);
+}
+SVOC_DEV float u2f(uint32_t w) { return __builtin_bit_cast(float, w); }
+SVOC_DEV uint32_t f2u(float v) { return __builtin_bit_cast(uint32_t, v); }
+
+// wt < zt ? wt : ~0
+SVOC_DEV uint32_t winf_cand(uint32_t wt, uint32_t zt) {
+  const uint32_t d = __builtin_elementwise_sub_sat(zt, wt);
+  return wt | (__builtin_elementwise_min(d, 1u) - 1u);
+}
+
+// Skewness / sample-adjusted excess kurtosis (math.cairo:320-363) of n values from power sums of
+// d = x - shift, combined in fp64; false for zero variance (the contract's sqrt(0) -> div-by-zero).
+SVOC_DEV bool moments_from_sums_d(double n, double t1, double t2, double t3, double t4, double& dl, float& sk,
+                                  float& ku) {
+  dl = t1 / n;
+  const double e2 = t2 / n, e3 = t3 / n, e4 = t4 / n;
+  const double mu2 = e2 - dl * dl;
+  const double mu3 = e3 - 3.0 * dl * e2 + 2.0 * dl * dl * dl;
+  const double mu4 = e4 - 4.0 * dl * e3 + 6.0 * dl * dl * e2 - 3.0 * dl * dl * dl * dl;
+  sk = 0.f;
+  ku = 0.f;
+  if (!(mu2 > 0.0)) return false;
+  const double k3 = n / ((n - 1.0) * (n - 2.0));
+  const double k4a = n * (n + 1.0) / (n - 1.0), k4b = 3.0 * (n - 1.0) * (n - 1.0), k4c = (n - 2.0) * (n - 3.0);
+  const double sd = sqrt(mu2);
+  sk = (float)(n * mu3 / (mu2 * sd) * k3);
+  ku = (float)((n * mu4 / (mu2 * mu2) * k4a - k4b) / k4c);
+  return true;
+}
+
+// The lane's rows {I0 + STEP * m}, every load issued before any is consumed.  The row stride is made
+// opaque here, so the SGPR row offsets are recomputed per batch (s_mul) instead of being hoisted out of
+// the slab loop into 64 live SGPRs -- spilled to VGPR lanes, and then the compiler serialises every
+// load behind its v_readlane and its consumer (one load in flight).
+template <int I0, int STEP, int CNT>
+SVOC_DEV void load_rows(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t (&x)[64]) {
+  asm volatile("" : "+s"(rowb));
+#pragma unroll
+  for (int m = 0; m < CNT; ++m) x[I0 + STEP * m] = bload(rs, vo, (I0 + STEP * m) * rowb);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// qr partials of the lane's 64 rows (one column) reduced across the wave's P columns by the
+// transposing butterfly (stage L exchanges with lane ^ (P >> L) and halves the row set), evaluated
+// depth-first.  The two leaves of a level-1 node (rows I and I + 32) are formed as one packed pair, so
+// the power sums of d = x - c1 accumulate on v_pk_add / v_pk_fma (two rows per instruction).
+// MASKROWS: rows >= N (read as 0 past the buffer end) are masked out of the power sums.
+struct QrCtxF {
+  int nvl, lane;
+  float c;
+};
+template <int L, int I, int P, bool MASKROWS>
+SVOC_DEV float qrf_tree(const QrCtxF& c, const uint32_t (&wv)[64], f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
+  static_assert(L >= 1, "level-1 nodes are the packed leaves");
+  constexpr int msk = P >> L;
+  float lo_v, hi_v;
+  if constexpr (L == 1) {
+    f32x2 y = f32x2{u2f(wv[I]), u2f(wv[I + 32])} - f32x2{c.c, c.c};
+    f32x2 q = y * y;
+    lo_v = q.x;
+    hi_v = q.y;
+    if (MASKROWS) {
+      const uint32_t m0 = lt_mask(I, c.nvl), m1 = lt_mask(I + 32, c.nvl);
+      const float y0 = y.x, y1 = y.y, q0 = q.x, q1 = q.y;
+      y = f32x2{fand(y0, m0), fand(y1, m1)};
+      q = f32x2{fand(q0, m0), fand(q1, m1)};
+    }
+    s1 += y;
+    s2 += q;
+    s3 = __builtin_elementwise_fma(q, y, s3);
+    s4 = __builtin_elementwise_fma(q, q, s4);
+  } else {
+    lo_v = qrf_tree<L - 1, I, P, MASKROWS>(c, wv, s1, s2, s3, s4);
+    hi_v = qrf_tree<L - 1, I + (64 >> L), P, MASKROWS>(c, wv, s1, s2, s3, s4);
+  }
+  const bool up = (c.lane & msk) != 0;
+  const float send = up ? lo_v : hi_v;
+  const float keep = up ? hi_v : lo_v;
+  return keep + xor_lane<msk>(send);
+}
+// One butterfly tree (final slot I): its 64/KEEP rows are loaded together, then reduced depth-first; an
+// empty asm closes the tree so the next tree's loads are not hoisted into it.
+template <int P, int I, bool MASKW, bool MASKROWS>
+SVOC_DEV void qrf_tree_slot(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, const QrCtxF& c, float* acc,
+                            f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
+  constexpr int KEEP = 64 / P;
+  uint32_t wv[64];
+  load_rows<I, KEEP, 64 / KEEP>(rs, vo, rowb, wv);
+  if (MASKW) {
+#pragma unroll
+    for (int m = 0; m < 64 / KEEP; ++m) wv[I + KEEP * m] &= mW;
+  }
+  constexpr int S = __builtin_ctz(P);
+  acc[I] += qrf_tree<S, I, P, MASKROWS>(c, wv, s1, s2, s3, s4);
+  asm volatile("" : "+v"(acc[I]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
+}
+template <int P, bool MASKW, bool MASKROWS, int... Is>
+SVOC_DEV void qrf_seq(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, const QrCtxF& c, float* acc,
+                      f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4, std::integer_sequence<int, Is...>) {
+  (qrf_tree_slot<P, Is, MASKW, MASKROWS>(rs, vo, rowb, mW, c, acc, s1, s2, s3, s4), ...);
+}
+template <int P, bool MASKW, bool MASKROWS>
+SVOC_DEV void qrf_moments(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, const QrCtxF& c, float* acc,
+                          f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
+  qrf_seq<P, MASKW, MASKROWS>(rs, vo, rowb, mW, c, acc, s1, s2, s3, s4, std::make_integer_sequence<int, 64 / P>{});
+}
+
+// qr pass with half of the slab staged in LDS (N = NPAD = 256, constrained): trees 0 and 1 (rows
+// i % 4 < 2) come from the wave's LDS region (raw bits, written straight from the pass-1 load registers),
+// trees 2 and 3 are re-read with all 32 loads issued first so their latency overlaps the LDS trees.
+template <int P, bool MASKW>
+SVOC_DEV void qrf_moments_staged(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, uint32_t kp,
+                                 const uint32_t* st, int lane, const QrCtxF& c, float* acc, f32x2& s1, f32x2& s2,
+                                 f32x2& s3, f32x2& s4) {
+  static_assert(P == 16, "staging layout: KEEP = 4 trees of 16 rows");
+  constexpr int KEEP = 4, S = 4;
+  uint32_t wm[64];
+  {
+    asm volatile("" : "+s"(rowb));
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      wm[2 + KEEP * m] = bload(rs, vo, (2 + KEEP * m) * rowb);
+      wm[3 + KEEP * m] = bload(rs, vo, (3 + KEEP * m) * rowb);
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    uint32_t wv[64];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      wv[t + KEEP * m] = st[(2 * m + t) * 64 + lane];
+      if (MASKW) wv[t + KEEP * m] &= mW;
+    }
+    if (t == 0) acc[0] += qrf_tree<S, 0, P, false>(c, wv, s1, s2, s3, s4);
+    else acc[1] += qrf_tree<S, 1, P, false>(c, wv, s1, s2, s3, s4);
+    asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
+  }
+  if (MASKW) {
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      wm[2 + KEEP * m] &= mW;
+      wm[3 + KEEP * m] &= mW;
+    }
+  }
+  acc[2] += qrf_tree<S, 2, P, false>(c, wm, s1, s2, s3, s4);
+  asm volatile("" : "+v"(acc[2]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
+  acc[3] += qrf_tree<S, 3, P, false>(c, wm, s1, s2, s3, s4);
+}
+
+// qr pass with the even rows staged in LDS for N <= 128 (NSEG 1 and 2, constrained): the odd rows are
+// re-read with all 32 loads issued before the LDS reads.
+template <int P, bool MASKW>
+SVOC_DEV void qrf_moments_staged_even(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, uint32_t kp,
+                                      const uint32_t* st, int lane, const QrCtxF& c, float* acc, f32x2& s1,
+                                      f32x2& s2, f32x2& s3, f32x2& s4) {
+  constexpr int KEEP = 64 / P, S = __builtin_ctz(P);
+  static_assert(KEEP <= 2, "even-row staging: one or two trees");
+  if constexpr (KEEP == 1) {
+    uint32_t wv[64];
+    load_rows<1, 2, 32>(rs, vo, rowb, wv);
+#pragma unroll
+    for (int m = 0; m < 32; ++m) wv[2 * m] = st[m * 64 + lane];
+    if (MASKW) {
+#pragma unroll
+      for (int i = 0; i < 64; ++i) wv[i] &= mW;
+    }
+    acc[0] += qrf_tree<S, 0, P, false>(c, wv, s1, s2, s3, s4);
+  } else {
+    uint32_t wm[64];
+    load_rows<1, 2, 32>(rs, vo, rowb, wm);
+    {
+      uint32_t wv[64];
+#pragma unroll
+      for (int m = 0; m < 32; ++m) {
+        wv[2 * m] = st[m * 64 + lane];
+        if (MASKW) wv[2 * m] &= mW;
+      }
+      acc[0] += qrf_tree<S, 0, P, false>(c, wv, s1, s2, s3, s4);
+      asm volatile("" : "+v"(acc[0]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
+    }
+    if (MASKW) {
+#pragma unroll
+      for (int m = 0; m < 32; ++m) wm[2 * m + 1] &= mW;
+    }
+    acc[1] += qrf_tree<S, 1, P, false>(c, wm, s1, s2, s3, s4);
+  }
+}
+
+template <int NSEG, int WAVES, int H, bool CONS, int MODE>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4))) void consensus_fast_winf_kernel(FastParams p) {
+  constexpr int P = 64 / NSEG;          // columns per wave (phase A)
+  constexpr int NPAD = 64 * NSEG;
+  constexpr int W = WAVES * P;          // columns per workgroup step (phase A)
+  constexpr int NT = WAVES * 64;
+  constexpr int KEEP = 64 / P;
+  // constrained: half of each slab (32 rows x 64 lanes, keys) staged per wave for the qr pass
+  constexpr bool STAGE = CONS && MODE != 2;
+  __shared__ uint32_t stage[STAGE ? WAVES * 32 * 64 : 1];
+  __shared__ float qr_part[WAVES * NPAD];
+  __shared__ float qr_lds[NPAD];
+  __shared__ uint64_t relmask[4];
+  __shared__ int urow[32];      // removed rows, index order
+  __shared__ float misc_f[2];
+  __shared__ int misc_i[3];     // status, zero-variance flag, cleanup list length
+
+  const int b = blockIdx.x;
+  if (p.active && !p.active[b]) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 32) urow[tid] = 0;  // f < 32: unused slots still name a valid row
+  if (tid == 0) misc_i[2] = 0;
+  const int seg = lane / P, cw = lane % P;
+  const int N = p.N, D = p.D;
+  const int rowb = p.ld * 4;
+  const float* inst = (const float*)p.values + (int64_t)b * p.inst_stride;
+  const __amdgpu_buffer_rsrc_t rs = instance_rsrc(inst, (uint32_t)(N * rowb));
+  const int nslab = (D + W - 1) / W;
+  const int Dc = 2 * p.work_pairs;      // workspace columns (launch.hpp: fast_work_words)
+  // this instance's workspace: [H][2][Dc] window keys, at byte MOM the [4][Dc] all-row power sums, at
+  // LST the [Dc] cleanup column list, at STG the [3][Dc] staged pass-2 outputs (unconstrained)
+  const __amdgpu_buffer_rsrc_t ws = instance_rsrc(p.work + (int64_t)b * p.work_stride, (uint32_t)(p.work_stride * 4));
+  const int MOM = 2 * H * Dc * 4;
+  const int LST = MOM + 4 * Dc * 4;
+  const int STG = Dc * kWinfStageCols * 4;
+  const int lo1 = (NPAD - N + 1) >> 1;
+  const int nv = N - seg * 64;
+  const int nl = N + lo1 - seg * 64;
+  const int seg_off = seg * 64 * rowb;
+  const uint32_t pol = group_polarity<NSEG>(seg);
+  const uint32_t kp = 0x80000000u ^ pol;   // constrained key = raw ^ kp
+  uint32_t* const stw = stage + (STAGE ? wave * 32 * 64 : 0);
+
+  float acc[KEEP];
+#pragma unroll
+  for (int i = 0; i < KEEP; ++i) acc[i] = 0.f;
+
+  // ------------------------------------------------------------ phase A: pass 1 (contract.cairo:455-463)
+  const int pass1_slabs = MODE == 2 ? 0 : nslab;
+#pragma nounroll
+  for (int s = 0; s < pass1_slabs; ++s) {
+    const int col = s * W + wave * P + cw;
+    const bool vc = col < D;
+    const int vo = seg_off + (vc ? col * 4 : 0);
+    int nvl = nv, nll = nl;
+    asm volatile("" : "+v"(nvl), "+v"(nll));
+    float c1v;
+    const uint32_t mW = vc ? 0xffffffffu : 0u;
+    {
+      uint32_t r[64];
+      // (no sched_barrier after these loads -- it costs ~40 spilled VGPRs; the opaque stride keeps the
+      // 64 row offsets out of the slab loop's SGPR live set)
+      int rowb1 = rowb;
+      asm volatile("" : "+s"(rowb1));
+      if (N == NPAD) {
+        if (CONS) {
+#pragma unroll
+          for (int i = 0; i < 64; ++i) r[i] = bload(rs, vo, i * rowb1);
+          // the staged rows go to LDS raw, straight from the load registers
+          if constexpr (STAGE && NSEG == 4) {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+              stw[(2 * m) * 64 + lane] = r[4 * m];
+              stw[(2 * m + 1) * 64 + lane] = r[4 * m + 1];
+            }
+          } else if constexpr (STAGE) {
+#pragma unroll
+            for (int m = 0; m < 32; ++m) stw[m * 64 + lane] = r[2 * m];
+          }
+#pragma unroll
+          for (int i = 0; i < 64; ++i) r[i] ^= kp;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 64; ++i) r[i] = fkey<CONS>(bload(rs, vo, i * rowb1)) ^ pol;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          // real rows -> key; rows >= N -> 0 (the first lo1) / ~0 sentinels, so the middle of the
+          // padded sort is the middle of the real rows
+          const uint32_t hi_m = ~lt_mask(i, nll);
+          r[i] = ((fkey<CONS>(bload(rs, vo, i * rowb1)) & (lt_mask(i, nvl) | hi_m)) | hi_m) ^ pol;
+        }
+      }
+      uint32_t klo, khi;
+      if constexpr (CONS) {
+        uint32_t wk[NSEG == 1 ? 2 * H : H];
+        window_group<NSEG, P, H>(r, seg, lane, wk, klo, khi);
+        if constexpr (NSEG == 1) {
+#pragma unroll
+          for (int m = 0; m < H; ++m) {
+            bstore(ws, wk[m], col * 4, 2 * m * Dc * 4);
+            bstore(ws, wk[H + m], (Dc + col) * 4, 2 * m * Dc * 4);
+          }
+        } else {
+          constexpr int slo = NSEG == 2 ? 0 : 1;
+          if (seg == slo || seg == slo + 1) {
+            const int part = seg - slo;
+#pragma unroll
+            for (int m = 0; m < H; ++m) bstore(ws, wk[m], (part * Dc + col) * 4, 2 * m * Dc * 4);
+          }
+        }
+      } else {
+        median_group<NSEG>(r, klo, khi);
+      }
+      c1v = 0.5f * (fkey_val<CONS>(klo) + fkey_val<CONS>(khi));
+    }
+    if (seg == 0 && vc) p.c1[(int64_t)b * D + col] = c1v;
+    __builtin_amdgcn_sched_barrier(0);
+    // the re-read's offset depends on the network's result (empty asm): otherwise the loads are hoisted
+    // above the network and both 64-register arrays are live at once (spills)
+    int vo2 = vo;
+    asm volatile("" : "+v"(vo2) : "v"(c1v));
+    const QrCtxF qc{nvl, lane, vc ? c1v : 0.f};
+    f32x2 s1 = {0.f, 0.f}, s2 = s1, s3 = s1, s4 = s1;
+    if (STAGE && N == NPAD) {
+      if constexpr (STAGE && NSEG == 4) {
+        if ((s + 1) * W <= D) qrf_moments_staged<P, false>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
+        else qrf_moments_staged<P, true>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
+      } else if constexpr (STAGE) {
+        if ((s + 1) * W <= D) qrf_moments_staged_even<P, false>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
+        else qrf_moments_staged_even<P, true>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
+      }
+    } else if ((s + 1) * W <= D) {
+      if (N == NPAD) qrf_moments<P, false, false>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
+      else qrf_moments<P, false, true>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
+    } else {
+      if (N == NPAD) qrf_moments<P, true, false>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
+      else qrf_moments<P, true, true>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
+    }
+    float t1 = s1.x + s1.y, t2 = s2.x + s2.y, t3 = s3.x + s3.y, t4 = s4.x + s4.y;
+    if constexpr (NSEG == 4) {
+      t1 += xor_lane<16>(t1); t2 += xor_lane<16>(t2); t3 += xor_lane<16>(t3); t4 += xor_lane<16>(t4);
+    }
+    if constexpr (NSEG >= 2) {
+      t1 += xor_lane<32>(t1); t2 += xor_lane<32>(t2); t3 += xor_lane<32>(t3); t4 += xor_lane<32>(t4);
+    }
+    if (seg == 0) {
+      bstore(ws, f2u(t1), col * 4, MOM);
+      bstore(ws, f2u(t2), col * 4, MOM + Dc * 4);
+      bstore(ws, f2u(t3), col * 4, MOM + 2 * Dc * 4);
+      bstore(ws, f2u(t4), col * 4, MOM + 3 * Dc * 4);
+    }
+  }
+
+  // ------------------------------------------------------------ qr reduction
+  {
+    int base = 0;
+#pragma unroll
+    for (int h = 32, msk = P / 2; msk >= 1; h >>= 1, msk >>= 1) base += (lane & msk) ? h : 0;
+#pragma unroll
+    for (int i = 0; i < KEEP; ++i) qr_part[wave * NPAD + seg * 64 + base + i] = acc[i];
+  }
+  __syncthreads();
+  for (int t = tid; t < NPAD; t += NT) {
+    float q = 0.f;
+    if (MODE == 2) {
+      q = t < N ? p.qr[(int64_t)b * N + t] : 0.f;
+    } else {
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) q += qr_part[w * NPAD + t];
+    }
+    qr_lds[t] = q;
+  }
+  __syncthreads();
+  if (MODE == 1) {
+    for (int t = tid; t < N; t += NT) p.qr[(int64_t)b * N + t] = qr_lds[t];
+    if (tid == 0) p.status[b] = ST_OK;
+    return;
+  }
+
+  // ------------------------------------------------------------ rank mask (contract.cairo:345-363)
+  const int f = p.n_failing;
+  const int R = N - f;
+  for (int base = 0; base < NPAD; base += NT) {
+    const int t = base + tid;
+    bool rel = false;
+    if (t < N) {
+      const float myq = qr_lds[t];
+      int rank = 0;
+      const int n4 = N & ~3;
+      for (int j = 0; j < n4; j += 4) {
+        const float4 q4 = *(const float4*)(qr_lds + j);
+        rank += (q4.x < myq || (q4.x == myq && j > t)) ? 1 : 0;
+        rank += (q4.y < myq || (q4.y == myq && j + 1 > t)) ? 1 : 0;
+        rank += (q4.z < myq || (q4.z == myq && j + 2 > t)) ? 1 : 0;
+        rank += (q4.w < myq || (q4.w == myq && j + 3 > t)) ? 1 : 0;
+      }
+      for (int j = n4; j < N; ++j) {
+        const float qj = qr_lds[j];
+        rank += (qj < myq || (qj == myq && j > t)) ? 1 : 0;
+      }
+      rel = rank < R;
+    }
+    const uint64_t bal = __ballot(rel);
+    if (lane == 0 && (t >> 6) < 4) relmask[t >> 6] = bal;
+  }
+  __syncthreads();
+  // removed rows in index order (pass 2 reads only these)
+  for (int t = tid; t < N; t += NT) {
+    const int w = t >> 6;
+    const uint64_t nr = ~relmask[w];
+    if ((nr >> (t & 63)) & 1) {
+      int cnt = __popcll(nr & ((1ull << (t & 63)) - 1));
+      for (int v = 0; v < w; ++v) cnt += __popcll(~relmask[v]);
+      if (cnt < 32) urow[cnt] = t;
+    }
+  }
+  if (tid < 64) {
+    // reliabilities (contract.cairo:365-368,436-439) from fp64 sums of the fp32 qr
+    double s_all = 0.0, s_rel = 0.0;
+    for (int t = tid; t < N; t += 64) {
+      const double q = (double)qr_lds[t];
+      s_all += q;
+      s_rel += ((relmask[t >> 6] >> (t & 63)) & 1) ? q : 0.0;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      s_all += __shfl_xor(s_all, o);
+      s_rel += __shfl_xor(s_rel, o);
+    }
+    if (tid == 0) {
+      int st = ST_OK;
+      const double rd = p.legacy ? 1.0 : (double)(p.rel_dim > 0 ? p.rel_dim : D);
+      const double ms = (double)p.max_spread;
+      auto rel_of = [&](double mean_qr) -> float {
+        return CONS ? (float)(1.0 - 2.0 * sqrt(mean_qr / rd)) : (float)(1.0 - fmin(ms, sqrt(mean_qr)) / ms);
+      };
+      const float rel1 = rel_of(s_all / (double)N);
+      float rel2 = 0.f;
+      if (!(rel1 >= 0.f && rel1 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
+      else if (R < 2) st = R <= 0 ? ST_USIZE_UNDERFLOW : ST_INDEX_OOB;
+      else {
+        rel2 = rel_of(s_rel / (double)R);
+        if (!(rel2 >= 0.f && rel2 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
+        else if (R < 4 && !p.legacy) st = ST_TOO_FEW_RELIABLE;
+      }
+      misc_f[0] = rel1;
+      misc_f[1] = rel2;
+      misc_i[0] = st;
+      misc_i[1] = 0;
+    }
+  }
+  __syncthreads();
+  if (misc_i[0] != ST_OK) {
+    if (tid == 0) p.status[b] = misc_i[0];
+    return;
+  }
+
+  // ------------------------------------------------------------ zero-variance pre-check (constrained)
+  // A reliable column of zero variance reverts the round (math.cairo:322,331; contract.cairo:588-603).
+  // The R equal values would form a sorted run covering positions [f, N - f - 1]; when f + H <= N/2 that
+  // run contains the whole window, so only columns whose window is constant qualify and only those are
+  // compared against the reliable rows (as consensus_fast_win.hip).  Decided before any output is written.
+  if (CONS && !p.legacy) {
+    const bool inwin = f + H <= N / 2;
+    int fr = 0;   // first reliable row
+    for (int w = 0; w < 4; ++w)
+      if (relmask[w]) { fr = 64 * w + __builtin_ctzll(relmask[w]); break; }
+    bool zv = false;
+#pragma nounroll
+    for (int base = wave * 64; base < D; base += WAVES * 64) {
+      const int col = base + lane;
+      const int pc = col < D ? col : D - 1;
+      bool cand = col < D;
+      if (inwin) {
+        // compared as values: a run of +0.0 and -0.0 is constant, but its keys differ
+        const uint32_t lo = bload(ws, pc * 4, 0), hi = ~bload(ws, (Dc + pc) * 4, 0);
+        cand = cand && fkey_val<true>(lo) == fkey_val<true>(hi);
+      }
+      if (__ballot(cand)) {   // rare: compare the reliable rows with the first one
+        const float r0 = u2f(bload(rs, pc * 4, fr * rowb));
+        for (int i = fr + 1; i < N; ++i) {
+          if (!((relmask[i >> 6] >> (i & 63)) & 1)) continue;   // uniform
+          cand = cand && u2f(bload(rs, pc * 4, i * rowb)) == r0;
+        }
+        zv = zv || cand;
+      }
+    }
+    if (zv) misc_i[1] = 1;
+    __syncthreads();
+    if (misc_i[1]) {
+      if (tid == 0) p.status[b] = ST_ZERO_VARIANCE;
+      return;
+    }
+  }
+  if (CONS) {
+    for (int t = tid; t < N; t += NT) {
+      p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
+      p.qr[(int64_t)b * N + t] = qr_lds[t];
+    }
+  }
+
+  // ------------------------------------------------------------ phase B: pass 2 (contract.cairo:476-500)
+  // one lane per column: the removed keys are sorted once and ranked against the window
+  const double n = (double)R;
+  const int sh = H - 1 - (N / 2 - R / 2);   // -inf sentinels in front of the removed keys
+  const int64_t ob = (int64_t)b * D;
+  bool zv = false;
+#pragma nounroll
+  for (int base = wave * 64; base < D; base += WAVES * 64) {
+    const int col = base + lane;
+    const int pc = col < D ? col : D - 1;
+    const int vo = pc * 4;
+    const float c1c = p.c1[ob + pc];
+    // opaque per-iteration copies: otherwise LICM hoists the 2H slot offsets / masks out of the loop
+    int shl = sh, fl = f;
+    asm volatile("" : "+s"(shl), "+s"(fl));
+    constexpr int NS = CONS ? 2 * H : 32;
+    const int s0 = CONS ? shl : 0;
+    const uint64_t realm = ((fl >= 64 ? ~0ull : (1ull << fl) - 1)) << s0;
+    const uint64_t lowm = (1ull << s0) - 1;
+    uint32_t uw[NS];
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      const int row = t - s0;
+      const bool real = (realm >> t) & 1;
+      uw[t] = 0u;
+      if (CONS || real) uw[t] = bload(rs, vo, __builtin_amdgcn_readfirstlane(urow[real ? row : 0]) * rowb);
+    }
+    // removed rows' power sums of d = x - c1
+    float u1 = 0.f, u2 = 0.f, u3 = 0.f, u4 = 0.f;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) {
+      if ((realm >> t) & 1) {   // uniform
+        const float y = u2f(uw[t]) - c1c;
+        const float q = y * y;
+        u1 += y;
+        u2 += q;
+        u3 = __builtin_fmaf(q, y, u3);
+        u4 = __builtin_fmaf(q, q, u4);
+      }
+    }
+    float cons_v = 0.f;
+    if constexpr (CONS) {
+      // removed keys + sentinels: U'[t], t < 2H, ascending keys
+      uint32_t z[64];
+#pragma unroll
+      for (int t = 0; t < 64; ++t) {
+        if (t < 2 * H) {
+          const uint32_t mreal = 0u - (uint32_t)((realm >> t) & 1);
+          const uint32_t kx = (0x80000000u & mreal) | (~mreal & (0u - (uint32_t)(((~lowm) >> t) & 1)));
+          z[t] = (uw[t] & mreal) ^ kx;
+        } else {
+          z[t] = ~0u;
+        }
+      }
+      sort_oem<64>(z);
+      // lower window half: position c - H + m pairs with U'[m] (lo) / U'[m - 1] (hi); upper half
+      // (stored complemented, position c + H - 1 - m): U'[2H - 1 - m] (lo) / U'[2H - 2 - m] (hi)
+      uint32_t clo = ~0u, chi = ~0u;
+#pragma unroll
+      for (int m = 0; m < H; ++m) {
+        const uint32_t wl = bload(ws, pc * 4, 2 * m * Dc * 4);
+        const uint32_t wu = ~bload(ws, (Dc + pc) * 4, 2 * m * Dc * 4);
+        clo = kmin(clo, winf_cand(wl, z[m]));
+        if (m) chi = kmin(chi, winf_cand(wl, z[m - 1]));
+        clo = kmin(clo, winf_cand(wu, z[2 * H - 1 - m]));
+        chi = kmin(chi, winf_cand(wu, z[2 * H - 2 - m]));
+      }
+      cons_v = 0.5f * (fkey_val<true>(clo) + fkey_val<true>(chi));
+    }
+
+    // reliable rows' power sums = all-row sums (phase A) - removed rows' sums
+    const double a1 = (double)u2f(bload(ws, pc * 4, MOM)), a2 = (double)u2f(bload(ws, pc * 4, MOM + Dc * 4));
+    const double a3 = (double)u2f(bload(ws, pc * 4, MOM + 2 * Dc * 4)), a4 = (double)u2f(bload(ws, pc * 4, MOM + 3 * Dc * 4));
+    const double r1 = a1 - (double)u1, r2 = a2 - (double)u2, r3 = a3 - (double)u3, r4 = a4 - (double)u4;
+    if (col < D) {
+      // trusted: no deep cancellation in the all-minus-removed difference, and the reliable mean within
+      // 2 sigma of the shift c1 (moments about a far shift cancel like (dl^2 / mu2)^2)
+      const double rdl = r1 / n, rmu2 = r2 / n - rdl * rdl;
+      const double wc = (double)p.win_cancel;
+      const bool good = r2 > 0.0 && a2 <= wc * r2 && a4 <= wc * r4 && rdl * rdl <= 4.0 * rmu2;
+      if (CONS) p.consensus[ob + col] = cons_v;
+      if (good) {
+        double dl;
+        float sk, ku;
+        const bool nz = moments_from_sums_d(n, r1, r2, r3, r4, dl, sk, ku);
+        if (CONS) {
+          p.skew[ob + col] = p.legacy ? 0.f : sk;
+          p.kurt[ob + col] = p.legacy ? 0.f : ku;
+        } else {
+          stage_out(ws, STG, Dc, 0, col, (float)((double)c1c + dl));
+          stage_out(ws, STG, Dc, 1, col, p.legacy ? 0.f : sk);
+          stage_out(ws, STG, Dc, 2, col, p.legacy ? 0.f : ku);
+          zv |= !nz;
+        }
+      } else {
+        // exact recomputation over the reliable rows below (each column listed once)
+        const int k = atomicAdd(&misc_i[2], 1);
+        bstore(ws, (uint32_t)col, k * 4, LST);
+      }
+    }
+  }
+  if (!CONS && zv && !p.legacy) misc_i[1] = 1;
+  __syncthreads();
+  // cleanup: one wave per listed column, lanes stride the rows, two-pass wave reductions
+  // (math.cairo:320-363): the reliable mean first, then the power sums about it (no cancellation)
+  const int nredo = misc_i[2];
+  if (nredo) {
+    for (int k = wave; k < nredo; k += WAVES) {
+      // (sc0: read through the vL1D -- the entry was written by another wave of this workgroup)
+      const int col = (int)__builtin_amdgcn_readfirstlane(__builtin_amdgcn_raw_buffer_load_b32(ws, 0, LST + k * 4, 1));
+      const float cc = p.c1[ob + col];
+      const float* xc = inst + col;
+      float y[NSEG];
+      float t1 = 0.f;
+#pragma unroll
+      for (int g = 0; g < NSEG; ++g) {
+        const int i = g * 64 + lane;
+        const bool use = i < N && ((relmask[g] >> lane) & 1);
+        y[g] = use ? xc[(int64_t)i * p.ld] - cc : 0.f;
+        t1 += y[g];
+      }
+      t1 += xor_lane<1>(t1); t1 += xor_lane<2>(t1); t1 += xor_lane<4>(t1);
+      t1 += xor_lane<8>(t1); t1 += xor_lane<16>(t1); t1 += xor_lane<32>(t1);
+      const float mu = t1 / (float)R;   // reliable mean - c1
+      float c1s = 0.f, t2 = 0.f, t3 = 0.f, t4 = 0.f;
+#pragma unroll
+      for (int g = 0; g < NSEG; ++g) {
+        const int i = g * 64 + lane;
+        const bool use = i < N && ((relmask[g] >> lane) & 1);
+        const float d = use ? y[g] - mu : 0.f;
+        const float q = d * d;
+        c1s += d;
+        t2 += q;
+        t3 = fmaf(q, d, t3);
+        t4 = fmaf(q, q, t4);
+      }
+      c1s += xor_lane<1>(c1s); t2 += xor_lane<1>(t2); t3 += xor_lane<1>(t3); t4 += xor_lane<1>(t4);
+      c1s += xor_lane<2>(c1s); t2 += xor_lane<2>(t2); t3 += xor_lane<2>(t3); t4 += xor_lane<2>(t4);
+      c1s += xor_lane<4>(c1s); t2 += xor_lane<4>(t2); t3 += xor_lane<4>(t3); t4 += xor_lane<4>(t4);
+      c1s += xor_lane<8>(c1s); t2 += xor_lane<8>(t2); t3 += xor_lane<8>(t3); t4 += xor_lane<8>(t4);
+      c1s += xor_lane<16>(c1s); t2 += xor_lane<16>(t2); t3 += xor_lane<16>(t3); t4 += xor_lane<16>(t4);
+      c1s += xor_lane<32>(c1s); t2 += xor_lane<32>(t2); t3 += xor_lane<32>(t3); t4 += xor_lane<32>(t4);
+      if (lane == 0) {
+        double dl;
+        float sk, ku;
+        const bool nz = moments_from_sums_d(n, c1s, t2, t3, t4, dl, sk, ku);
+        if (CONS) {
+          p.skew[ob + col] = p.legacy ? 0.f : sk;
+          p.kurt[ob + col] = p.legacy ? 0.f : ku;
+        } else {
+          stage_out(ws, STG, Dc, 0, col, (float)((double)cc + (double)mu + dl));
+          stage_out(ws, STG, Dc, 1, col, p.legacy ? 0.f : sk);
+          stage_out(ws, STG, Dc, 2, col, p.legacy ? 0.f : ku);
+          if (!nz && !p.legacy) misc_i[1] = 1;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // ------------------------------------------------------------ commit
+  // (constrained: written in place -- the pre-check ruled out every revert; unconstrained: copied from
+  // the staging area, only when the round succeeded)
+  if (!CONS) {
+    if (misc_i[1]) {
+      if (tid == 0) p.status[b] = ST_ZERO_VARIANCE;
+      return;
+    }
+    commit_staged<NT>(ws, STG, Dc, D, tid, p.consensus + ob, p.skew + ob, p.kurt + ob);
+    for (int t = tid; t < N; t += NT) {
+      p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
+      p.qr[(int64_t)b * N + t] = qr_lds[t];
+    }
+  }
+  if (tid == 0) {
+    p.rel[2 * (int64_t)b] = misc_f[0];
+    p.rel[2 * (int64_t)b + 1] = misc_f[1];
+    p.status[b] = ST_OK;
+  }
+}
+
+template <int NSEG, int WAVES, int H, bool CONS>
+static void launch_winf_w(const FastParams& p, hipStream_t stream) {
+  if (p.mode == 1) hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 1>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+  else if (p.mode == 2) hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 2>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+  else hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 0>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+}
+
+// Waves per workgroup: one workgroup per instance; N > 128 with at least two 8-wave slabs of columns
+// runs 8 waves (half the slabs per wave, 2 workgroups per CU: the bf16 kernel's measured choice,
+// profiles/r2_win_waves_ab.jsonl), everything else 4.
+template <int NSEG, int H, bool CONS>
+static void launch_winf_c(const FastParams& p, hipStream_t stream) {
+  if constexpr (NSEG == 4) {
+    if (p.D >= 2 * 8 * 16) return launch_winf_w<NSEG, 8, H, CONS>(p, stream);
+  }
+  launch_winf_w<NSEG, 4, H, CONS>(p, stream);
+}
+
+template <int NSEG>
+static void launch_winf(const FastParams& p, int H, hipStream_t stream) {
+  if (!p.constrained) launch_winf_c<NSEG, 5, false>(p, stream);   // no window: H = 5 keeps the layout
+  else if (H == 5) launch_winf_c<NSEG, 5, true>(p, stream);
+  else launch_winf_c<NSEG, 17, true>(p, stream);
+}
+
+}  // namespace svoc
+
+using namespace svoc;
+
+// Returns -2 when the window kernel does not apply (no workspace, f > 32, N > 256, ...): the caller
+// falls back to the two-network fp32 kernel.
+extern "C" int svoc_fast_round_f32_win(const FastParams* p, hipStream_t stream) {
+  if (p->B <= 0) return 0;
+  if (!p->work || p->N < 2 || p->N > 256 || p->D > p->ld) return -2;
+  if ((int64_t)p->N * p->ld * 4 >= (1ll << 31)) return -2;
+  if (p->mode == 2 && p->work_fresh) return -2;   // pass 1 ran elsewhere: no windows to read
+  if (p->n_failing < 0 || p->n_failing > 32 || p->n_failing > p->N - 2) return -2;
+  const int H = fast_win_h(p->N, p->n_failing);
+  if (H == 0) return -2;
+  if (p->work_pairs < fast_work_pairs(p->D) || p->work_pairs % 256 != 0 || p->work_stride < fast_work_words(p->D))
+    return -1;
+  if (p->N <= 64) launch_winf<1>(*p, H, stream);
+  else if (p->N <= 128) launch_winf<2>(*p, H, stream);
+  else launch_winf<4>(*p, H, stream);
+  return (int)hipGetLastError();
+}

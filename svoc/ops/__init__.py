@@ -63,7 +63,7 @@ from . import torch_ref  # noqa: E402,F401
 def fast_work_words(D: int) -> int:
     """u32 words per instance of the window kernel's workspace (csrc/include/svoc/launch.hpp)."""
     pairs = ((D + 1) // 2 + 255) // 256 * 256
-    return pairs * (2 * 17 + 8 + 2 + 6)
+    return pairs * 2 * (2 * 17 + 4 + 1 + 3)   # fp32 window layout (the larger of the two)
 
 
 def fast_work_numel(B: int, D: int) -> int:

@@ -132,7 +132,8 @@ def test_f32_reverts_leave_outputs_untouched():
 
 
 def test_f32_split_modes_match_whole_round():
-    """Mode 1 (c1 + qr partials) / mode 2 (from the summed qr) on two column slices == the whole round."""
+    """Mode 1 (c1 + qr partials) / mode 2 (from the summed qr) on two column slices == the whole round
+    (the two-network kernel, wave_hint -7: mode 2 reads nothing from mode 1 but c1 and the qr)."""
     B, N, D, f = 8, 100, 300, 10
     x = _f32(B, N, D, f, seed=11)[:, :, :D].contiguous()
     whole = run_fast(x.to(DEV), D, f, True)
@@ -142,12 +143,12 @@ def test_f32_split_modes_match_whole_round():
     op = svops.ops().fast_round
     for p, o in zip(parts, outs):
         op(p, None, p.shape[2], f, True, 1.0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"], o["qr"],
-           o["reliable"], o["status"], 0, 1, D, False, None)
+           o["reliable"], o["status"], -7, 1, D, False, None)
     qr = outs[0]["qr"] + outs[1]["qr"]
     for p, o in zip(parts, outs):
         o["qr"].copy_(qr)
         op(p, None, p.shape[2], f, True, 1.0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"], o["qr"],
-           o["reliable"], o["status"], 0, 2, D, False, fast_work(B, p.shape[2], DEV))
+           o["reliable"], o["status"], -7, 2, D, False, fast_work(B, p.shape[2], DEV))
     torch.cuda.synchronize()
     for o in outs:
         assert (o["status"] == 0).all()
@@ -176,3 +177,99 @@ def test_engine_fp32_storage_gpu():
     for k in ("status", "reliable", "consensus", "c1"):
         assert torch.equal(getattr(eg, k).cpu(), getattr(ec, k)), k
     torch.testing.assert_close(eg.rel.cpu(), ec.rel, rtol=1e-5, atol=1e-6)
+
+
+# ----------------------------------------------------------------------------------------------------
+# One-network window kernel (consensus_fast_winf.hip): the default for N <= 256, f <= 32.  Cross-checked
+# against the two-network fp32 kernel (wave_hint -7) and the PyTorch reference.
+
+WIN_SHAPES = [(256, 4096, 32), (256, 300, 32), (64, 1024, 8), (64, 100, 8), (200, 136, 20), (128, 512, 16),
+              (100, 260, 10), (33, 70, 4), (7, 6, 2), (256, 1000, 5), (250, 129, 31), (65, 129, 9)]
+
+
+@pytest.mark.parametrize("N,D,f", WIN_SHAPES)
+@pytest.mark.parametrize("constrained", [True, False])
+def test_f32_window_matches_two_network_kernel(N, D, f, constrained):
+    B = 6 if D >= 1000 else 12
+    x = _f32(B, N, D, f, seed=N * 7 + D + f)
+    if not constrained:
+        x = x * 4.0 - 1.5
+    xg = x.to(DEV)
+    w = run_fast(xg, D, f, constrained, 3.0)
+    t = run_fast(xg, D, f, constrained, 3.0, wave_hint=-7)
+    ref = torch_ref.fast_round(x[:, :, :D].to(DEV), f, constrained, 3.0)
+    torch.cuda.synchronize()
+    assert (w["status"] == 0).all() and (t["status"] == 0).all(), (w["status"], t["status"])
+    for k in ("c1", "reliable"):
+        assert torch.equal(w[k], t[k]), k
+    assert torch.equal(w["c1"], ref["c1"].float())
+    assert torch.equal(w["reliable"].bool(), ref["reliable"])
+    if constrained:
+        assert torch.equal(w["consensus"], t["consensus"])
+        assert torch.equal(w["consensus"], ref["consensus"])
+    else:
+        torch.testing.assert_close(w["consensus"], ref["consensus"], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(w["qr"], t["qr"], rtol=2e-5, atol=1e-6)
+    torch.testing.assert_close(w["rel"], ref["rel"], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(w["skew"], ref["skew"], rtol=1e-3, atol=5e-4)
+    torch.testing.assert_close(w["kurt"], ref["kurt"], rtol=1e-3, atol=5e-4)
+
+
+@pytest.mark.parametrize("cancel", ["0.5", "1e30"])
+def test_f32_window_cleanup_path(cancel, monkeypatch):
+    """SVOC_WIN_CANCEL=0.5 sends every column through the exact two-pass recomputation, 1e30 none: both
+    agree with the PyTorch reference (the cleanup is the cancellation guard of the all-minus-removed
+    power sums)."""
+    monkeypatch.setenv("SVOC_WIN_CANCEL", cancel)
+    B, N, D, f = 8, 256, 700, 32
+    x = _f32(B, N, D, f, seed=5)
+    o = run_fast(x.to(DEV), D, f, True)
+    ref = torch_ref.fast_round(x[:, :, :D].to(DEV), f, True)
+    torch.cuda.synchronize()
+    assert (o["status"] == 0).all()
+    assert torch.equal(o["consensus"], ref["consensus"])
+    torch.testing.assert_close(o["skew"], ref["skew"], rtol=1e-3, atol=5e-4)
+    torch.testing.assert_close(o["kurt"], ref["kurt"], rtol=1e-3, atol=5e-4)
+
+
+def test_f32_window_zero_variance_and_mixed_signed_zero():
+    """A constant reliable column (also one mixing +0.0 and -0.0: equal values) reverts the window round
+    with ZERO_VARIANCE, as the two-network kernel does; outputs stay untouched."""
+    B, N, D, f = 4, 256, 300, 32
+    x = _f32(B, N, D, f, seed=9)
+    x[1, :, 40] = 0.375
+    x[2, :, 7] = 0.0
+    x[2, ::2, 7] = -0.0
+    xg = x.to(DEV)
+    w = run_fast(xg, D, f, True)
+    t = run_fast(xg, D, f, True, wave_hint=-7)
+    torch.cuda.synchronize()
+    assert torch.equal(w["status"], t["status"])
+    st = w["status"].cpu()
+    assert st[1].item() != 0 and st[2].item() != 0 and st[0].item() == 0 and st[3].item() == 0
+
+
+def test_f32_window_split_modes_match_whole_round():
+    """D-sharded halves (mode 1 / mode 2 with a persistent workspace) through the window kernel."""
+    B, N, D, f = 6, 256, 520, 32
+    x = _f32(B, N, D, f, seed=13)[:, :, :D].contiguous()
+    whole = run_fast(x.to(DEV), D, f, True)
+    cut = 264
+    parts = [x[:, :, :cut].contiguous().to(DEV), x[:, :, cut:].contiguous().to(DEV)]
+    outs = [alloc_fast_out(B, N, p.shape[2], DEV) for p in parts]
+    works = [fast_work(B, p.shape[2], DEV) for p in parts]
+    op = svops.ops().fast_round
+    for p, o, w in zip(parts, outs, works):
+        op(p, None, p.shape[2], f, True, 1.0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"], o["qr"],
+           o["reliable"], o["status"], 0, 1, D, False, w)
+    qr = outs[0]["qr"] + outs[1]["qr"]
+    for p, o, w in zip(parts, outs, works):
+        o["qr"].copy_(qr)
+        op(p, None, p.shape[2], f, True, 1.0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"], o["qr"],
+           o["reliable"], o["status"], 0, 2, D, False, w)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert (o["status"] == 0).all()
+        assert torch.equal(o["reliable"], whole["reliable"])
+    for k in ("c1", "consensus"):
+        assert torch.equal(torch.cat([outs[0][k], outs[1][k]], 1), whole[k]), k

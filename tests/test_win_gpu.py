@@ -103,6 +103,19 @@ def test_win_zero_variance_flag():
     assert int(win["status"][0]) == 32      # ZERO_VARIANCE: the round reverts
 
 
+def test_win_zero_variance_mixed_signed_zero():
+    """A reliable column of +0.0 and -0.0 (equal values, different sort keys) is zero variance: the
+    window kernel's pre-check compares window bounds as values, so it reverts like the reg kernel."""
+    B, N, D, f = 4, 256, 128, 32
+    x, _ = beta_oracles(B, N, D, f, seed=21)
+    x[2, :, 9] = 0.0
+    x[2, ::2, 9] = -0.0
+    xg = x.to(DEV)
+    win, reg = _both(xg, D, f, True)
+    assert torch.equal(win["status"], reg["status"])
+    assert int(win["status"][2]) == 32 and int(win["status"][0]) == 0
+
+
 def test_win_legacy():
     x, _ = beta_oracles(6, 100, 200, 10, seed=1)
     xg = x.to(DEV)
