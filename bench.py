@@ -1,6 +1,6 @@
 """Headline benchmark: consensus updates/sec (N oracles x D dims, batched) at 1/2/4/8 MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c5|c4|c1] [--batch B]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 Configs (BASELINE.json):
@@ -8,15 +8,20 @@ Configs (BASELINE.json):
       independent instances.  One step on every rank = a batch of fresh predictions from 1/4 of the
       oracles of every local instance (synthetic stream, pre-generated in HBM, cycled) scattered into
       the state + one full two-pass consensus round per instance (fused HIP kernel) + an RCCL
-      all-reduce of the step's health metrics (reliability sum, OK count).
-  c2: 64 oracles x 1024 dims, 10k instances per GPU, one full consensus round per instance per step.
+      all-reduce of the step's health metrics (reliability sum, OK count).  Storage: fp32 -- the
+      reference computes on the 1e-6 wsad grid (contract/src/signed_decimal.cairo:82-83) and fp32 holds
+      every grid value of [0, 1] exactly; the bf16-storage step is measured too and reported as the
+      extra field ``config.alt_storage``.
+  c2: 64 oracles x 1024 dims, 10k instances per GPU (bf16, as BASELINE.json names it; fp32 storage
+      reported as ``config.alt_storage``), one full consensus round per instance per step.
 Weak scaling: per-GPU instances are fixed; ``value`` is the whole-job consensus rounds per second.
-Synthetic data (Beta(20,20) honest oracles, U(0,1) failing), random state, bf16 storage / fp32 math.
+Synthetic data (Beta(20,20) honest oracles, U(0,1) failing), random state.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -33,9 +38,9 @@ CONFIGS = {
     "c1": dict(model="plumbing: 4 oracles x 2 dims, one exact (wsad) round per step on the CPU engine", N=4, D=2,
                f=0, batch=1, update_frac=0.0, device="cpu", mode="exact", dtype="int64-wsad"),
     "c3": dict(model="svoc-consensus N=256 D=4096 streaming (f=32, constrained)", N=256, D=4096, f=32,
-               batch=1024, update_frac=0.25, pipeline=4),
+               batch=1024, update_frac=0.25, pipeline=4, storage="fp32", alt_storage="bf16"),
     "c2": dict(model="svoc-consensus N=64 D=1024 batched (f=8, constrained)", N=64, D=1024, f=8,
-               batch=10000, update_frac=0.0),
+               batch=10000, update_frac=0.0, storage="bf16", alt_storage="fp32"),
     "c4": dict(model="sentiment oracles: BERT-base (12x768, bf16) on 30-comment windows -> 7 oracles x 6 dims",
                N=7, D=6, f=2, batch=64, update_frac=1.0, seq_len=128),
     "c5": dict(model="deployed config 7 oracles x 6 dims, governance + reliability stream (1% instances vote/step)",
@@ -60,6 +65,167 @@ def _launch_ranks(n: int) -> int:
     return subprocess.call(cmd)
 
 
+def _dtype_name(mode: str, storage: str, c: dict) -> str:
+    if mode == "exact":
+        return f"{storage}-wsad"
+    return {"fp32": "fp32", "bf16": "bf16"}.get(storage, c.get("dtype", "bf16"))
+
+
+def measure(args, c, storage, dev, rank, world, dshard):
+    """Build the engine + update source for one storage dtype, warm up, time exactly args.steps steps
+    (barrier + device sync on both sides) and gather every rank's time and round outcomes."""
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    from svoc.parallel.dp import DataParallelConsensus
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    B = args.batch or c["batch"]
+    D_local = c["D"]
+    if dshard:
+        from svoc.parallel.dshard import run_round_sharded, shard_bounds
+        lo, hi = shard_bounds(c["D"], rank, world)
+        D_local = hi - lo
+    cfg = ConsensusConfig(n_oracles=c["N"], dimension=D_local, n_failing_oracles=c["f"], constrained=True)
+    mode = args.mode or c.get("mode", "fast")
+    eng = ConsensusEngine(cfg, batch=B, device=dev, mode=mode, storage=storage)
+    eng.wave_hint = args.wave_hint
+    dp = DataParallelConsensus(eng, rank=rank, world=world)
+    eng.randomize(seed=1000 + (0 if dshard else rank))
+
+    # synthetic update stream resident in HBM: `pool` steps of updates, cycled
+    U_per_inst = int(round(c["update_frac"] * c["N"]))
+    stream = pipe = gov = None
+    extra = {}
+    if args.config == "c4":
+        from svoc.models import corpus
+        from svoc.models.sentiment_oracle import SentimentOraclePipeline
+        pipe = SentimentOraclePipeline(eng, seed=0)
+        g = torch.Generator(device=dev).manual_seed(rank)
+        toks = [corpus.synthetic_token_batch(B * 30, c["seq_len"], 50265, g, dev) for _ in range(2)]
+        from svoc.models.encoder import flops_for_lengths
+        extra["comments_per_step"] = B * 30
+        lens = toks[0][1].sum(1).tolist()
+        extra["real_tokens_per_step"] = int(sum(lens))
+        extra["padded_tokens_per_step"] = B * 30 * c["seq_len"]
+        # the packed path computes real tokens only (as the reference pipeline, one comment at a time)
+        extra["encoder_gflop_per_step"] = flops_for_lengths(pipe.encoder.cfg, lens) / 1e9
+    elif U_per_inst:
+        from svoc.stream import SyntheticUpdateStream
+        # D-sharding: every rank streams the same updates (same seed), its own column slice of them
+        stream = SyntheticUpdateStream(B, c["N"], D_local, U_per_inst, c["f"], pool=2, device=dev,
+                                       seed=(0 if dshard else rank),
+                                       dtype=torch.int64 if mode == "exact" else eng.vdtype)
+    if args.config == "c5":
+        from svoc.codec import address_to_limbs
+        from svoc.governance import Governance
+        gov = Governance(B, 3, c["N"], dev, True, 2)
+        gov.admins.copy_(torch.tensor([address_to_limbs(1000 + a) for a in range(3)], device=dev).expand(B, 3, 4))
+        ora = torch.tensor([address_to_limbs(5000 + o) for o in range(c["N"])], device=dev)
+        gov.oracle_addr.copy_(ora.expand(B, c["N"], 4))
+        from svoc.stream import governance_stream
+        gov_batches = governance_stream(B, c["N"], [1000, 1001, 1002], dev, seed=rank, frac=c["gov_frac"])
+        extra["governance_actions_per_step"] = gov_batches[0][0].numel()
+        extra["state_bytes_per_instance"] = (eng.state_bytes_per_instance() + 3 * 4 * 8 + 3 * 8 + 3 * (1 + 4 + 32)
+                                             + c["N"] * 32)
+        extra["instances_per_288GB"] = int(288e9 // extra["state_bytes_per_instance"])
+
+    pipeline = args.pipeline if args.pipeline >= 0 else c.get("pipeline", 1)
+    if dshard or mode != "fast" or dev.type != "cuda":
+        pipeline = 1
+    extra["pipeline_chunks"] = pipeline
+
+    def run_round():
+        if dshard:
+            run_round_sharded(eng, c["D"], world=world)   # includes the qr all-reduce
+        else:
+            eng.run_round(only_touched=True)
+
+    def step(i):  # device-only work (capturable)
+        if pipe is not None:
+            pipe.fetch(*toks[i % 2])
+        elif stream is not None:
+            inst, orc, vals = stream.batch(i)
+            if pipeline > 1:   # the stream has distinct (instance, oracle), grouped by instance
+                eng.step_pipelined(inst, orc, vals, U_per_inst, chunks=pipeline)
+            else:
+                eng.apply_updates(inst, orc, vals, unique=True)
+                run_round()
+        else:
+            eng.touched.fill_(1)
+            run_round()
+        if gov is not None:
+            gov.submit_tensors(*gov_batches[i % len(gov_batches)])
+
+    for i in range(args.warmup):
+        step(i)
+        dp.reduce()
+    sync()
+
+    graph = None
+    graph_period = 1
+    if args.graph and dev.type == "cuda" and not (dshard and world > 1):   # (no collectives in a graph)
+        # the stream cycles with period `pool`: capture one period and replay it
+        period = 1
+        for k in (stream.pool if stream is not None else 1, len(gov_batches) if gov is not None else 1,
+                  2 if pipe is not None else 1):
+            period = period * k // math.gcd(period, k)
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            for i in range(period):
+                step(i)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        sync()
+        try:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for i in range(period):
+                    step(i)
+            graph_period = period
+        except Exception as e:  # graph capture is an optimisation; eager stays correct
+            if rank == 0:
+                print(f"[bench] graph capture failed ({e}); running eager", file=sys.stderr)
+            graph = None
+
+    fx0 = eng.metrics_fx.clone()   # this rank's round outcome counters before the timed steps
+    if world > 1:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    if graph is not None:
+        reps, rem = divmod(args.steps, graph_period)
+        for _ in range(reps):
+            graph.replay()
+            dp.reduce()            # one RCCL all-reduce of the step metrics per replay
+        for i in range(rem):       # exactly K steps: the tail of a period runs eagerly
+            step(i)
+            dp.reduce()
+    else:
+        for i in range(args.steps):
+            step(i)
+            dp.reduce()
+    sync()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    fx = (eng.metrics_fx - fx0).double()
+    ok_local = float(fx[1] / fx[2]) if float(fx[2]) > 0 else 0.0
+    mine = torch.tensor([t1 - t0, ok_local], dtype=torch.float64, device=dev)
+    if world > 1:
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = torch.stack(allr).cpu()
+    else:
+        per_rank = mine[None].cpu()
+    return dict(eng=eng, B=B, mode=mode, elapsed=float(per_rank[:, 0].max()),   # the slowest rank's time
+                U=U_per_inst, graph=graph is not None, extra=extra, step=step, storage=eng.storage,
+                rank_ms=[1e3 * float(t) / args.steps for t in per_rank[:, 0]],
+                rank_ok=[float(o) for o in per_rank[:, 1]], ok=dp.global_ok_fraction())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -77,7 +243,8 @@ def main():
     ap.add_argument("--mode", default=None, choices=["fast", "exact"],
                     help="override the config's engine mode (exact = bit-exact wsad int64 path)")
     ap.add_argument("--storage", default=None, choices=["bf16", "fp32", "int64", "int32"],
-                    help="engine value storage (exact mode: int64 default, int32 for constrained configs)")
+                    help="engine value storage (default: the config's; exact mode: int64, int32 for constrained "
+                         "configs).  Given explicitly, only that storage is measured (no alt_storage field)")
     ap.add_argument("--dshard", action="store_true",
                     help="strong scaling: every rank holds a column slice of ALL instances (D-sharding, one "
                          "[B, N] qr all-reduce per round) instead of its own instances (DP, default)")
@@ -111,179 +278,63 @@ def main():
             dist.init_process_group(args.backend or "nccl", device_id=dev)
         else:
             dist.init_process_group(args.backend or "gloo")
+    # the world size the initialised backend reports (not just the launcher's environment)
+    backend_world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
     dshard = args.dshard   # world 1: the split-kernel path without collectives (its overhead)
-
-    from svoc.config import ConsensusConfig
-    from svoc.engine import ConsensusEngine
-    from svoc.parallel.dp import DataParallelConsensus
-
-    def sync():
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
-
-    B = args.batch or c["batch"]
-    D_local, lo = c["D"], 0
-    if dshard:
-        from svoc.parallel.dshard import run_round_sharded, shard_bounds
-        lo, hi = shard_bounds(c["D"], rank, world)
-        D_local = hi - lo
-    cfg = ConsensusConfig(n_oracles=c["N"], dimension=D_local, n_failing_oracles=c["f"], constrained=True)
-    mode = args.mode or c.get("mode", "fast")
     if dshard and args.config in ("c4", "c5"):
         raise SystemExit("--dshard is for the column-sharded configs (c2, c3, fast or exact)")
-    eng = ConsensusEngine(cfg, batch=B, device=dev, mode=mode, storage=args.storage)
-    eng.wave_hint = args.wave_hint
-    dp = DataParallelConsensus(eng, rank=rank, world=world)
-    eng.randomize(seed=1000 + (0 if dshard else rank))
 
-    # synthetic update stream resident in HBM: `pool` steps of updates, cycled
-    U_per_inst = int(round(c["update_frac"] * c["N"]))
-    stream = pipe = gov = None
-    extra = {}
-    if args.config == "c4":
-        from svoc.models import corpus
-        from svoc.models.sentiment_oracle import SentimentOraclePipeline
-        pipe = SentimentOraclePipeline(eng, seed=0)
-        g = torch.Generator(device=dev).manual_seed(rank)
-        toks = [corpus.synthetic_token_batch(B * 30, c["seq_len"], 50265, g, dev) for _ in range(2)]
-        from svoc.models.encoder import flops_for_lengths
-        extra["comments_per_step"] = B * 30
-        lens = toks[0][1].sum(1).tolist()
-        extra["real_tokens_per_step"] = int(sum(lens))
-        extra["padded_tokens_per_step"] = B * 30 * c["seq_len"]
-        # the packed path computes real tokens only (as the reference pipeline, one comment at a time)
-        extra["encoder_gflop_per_step"] = flops_for_lengths(pipe.encoder.cfg, lens) / 1e9
-    elif U_per_inst:
-        from svoc.stream import SyntheticUpdateStream
-        # D-sharding: every rank streams the same updates (same seed), its own column slice of them
-        stream = SyntheticUpdateStream(B, c["N"], D_local, U_per_inst, c["f"], pool=2, device=dev,
-                                       seed=(0 if dshard else rank),
-                                       dtype=torch.int64 if mode == "exact" else torch.bfloat16)
-    if args.config == "c5":
-        from svoc.codec import address_to_limbs
-        from svoc.governance import Governance
-        gov = Governance(B, 3, c["N"], dev, True, 2)
-        gov.admins.copy_(torch.tensor([address_to_limbs(1000 + a) for a in range(3)], device=dev).expand(B, 3, 4))
-        ora = torch.tensor([address_to_limbs(5000 + o) for o in range(c["N"])], device=dev)
-        gov.oracle_addr.copy_(ora.expand(B, c["N"], 4))
-        from svoc.stream import governance_stream
-        gov_batches = governance_stream(B, c["N"], [1000, 1001, 1002], dev, seed=rank, frac=c["gov_frac"])
-        K = gov_batches[0][0].numel()
-        extra["governance_actions_per_step"] = K
-        extra["state_bytes_per_instance"] = eng.bytes_per_instance(c["N"], c["D"], "fast") + 3 * 4 * 8 + 3 * 8 + 3 * (1 + 4 + 32) + c["N"] * 32
-        extra["instances_per_288GB"] = int(288e9 // extra["state_bytes_per_instance"])
+    from svoc.utils.metrics import algorithmic_bytes_per_round
+    fast = (args.mode or c.get("mode", "fast")) == "fast"
+    storage = args.storage or (c.get("storage") if fast else None)
+    alt = c.get("alt_storage") if (fast and args.storage is None and dev.type == "cuda") else None
+    scale = 1 if dshard else world   # D-sharding: all ranks share the same B instances
 
-    pipeline = args.pipeline if args.pipeline >= 0 else c.get("pipeline", 1)
-    if dshard or mode != "fast" or dev.type != "cuda":
-        pipeline = 1
-    extra["pipeline_chunks"] = pipeline
+    def min_gbps(res, storage_bytes):
+        # data-flow floor (one read of the values + outputs + the update rows in and out), not measured bytes
+        rr = res["B"] * scale * args.steps
+        return algorithmic_bytes_per_round(c["N"], c["D"], storage_bytes, res["U"]) * rr / res["elapsed"] / 1e9
 
-    def run_round():
-        if dshard:
-            run_round_sharded(eng, c["D"], world=world)   # includes the qr all-reduce
-        else:
-            eng.run_round(only_touched=True)
-
-    def step(i):  # device-only work (capturable)
-        if pipe is not None:
-            pipe.fetch(*toks[i % 2])
-        elif stream is not None:
-            inst, orc, vals = stream.batch(i)
-            if pipeline > 1:   # the stream has distinct (instance, oracle), grouped by instance
-                eng.step_pipelined(inst, orc, vals, U_per_inst, chunks=pipeline)
-            else:
-                eng.apply_updates(inst, orc, vals, unique=True)
-                run_round()
-        else:
-            eng.touched.fill_(1)
-            run_round()
-        if gov is not None:
-            gov.submit_tensors(*gov_batches[i % len(gov_batches)])
-        dp.accumulate()
-
-    for i in range(args.warmup):
-        step(i)
-        dp.reduce()
-    sync()
-
-    graph = None
-    if args.graph and dev.type == "cuda" and not (dshard and world > 1):   # (no collectives in a graph)
-        # the stream cycles with period `pool`: capture one period and replay it
-        import math
-        period = 1
-        for k in (stream.pool if stream is not None else 1, len(gov_batches) if gov is not None else 1,
-                  2 if pipe is not None else 1):
-            period = period * k // math.gcd(period, k)
-        s = torch.cuda.Stream(device=dev)
-        s.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(s):
-            for i in range(period):
-                step(i)
-        torch.cuda.current_stream(dev).wait_stream(s)
-        sync()
-        try:
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                for i in range(period):
-                    step(i)
-            graph_period = period
-        except Exception as e:  # graph capture is an optimisation; eager stays correct
-            if rank == 0:
-                print(f"[bench] graph capture failed ({e}); running eager", file=sys.stderr)
-            graph = None
-
-    if world > 1:
-        dist.barrier()
-    sync()
-    t0 = time.perf_counter()
-    if graph is not None:
-        reps, rem = divmod(args.steps, graph_period)
-        for _ in range(reps):
-            graph.replay()
-            dp.reduce()            # one RCCL all-reduce of the step metrics per replay
-        for i in range(rem):       # exactly K steps: the tail of a period runs eagerly
-            step(i)
-            dp.reduce()
-        steps_done = args.steps
-    else:
-        for i in range(args.steps):
-            step(i)
-            dp.reduce()
-        steps_done = args.steps
-    sync()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    el = float(elapsed.item())
-    ms_per_step = 1e3 * el / steps_done
-    rounds = B * (1 if dshard else world) * steps_done   # D-sharding: all ranks share the same B instances
-    value = rounds / el
-    ok = dp.global_ok_fraction()
+    r = measure(args, c, storage, dev, rank, world, dshard)
+    B, mode, el, U, eng = r["B"], r["mode"], r["elapsed"], r["U"], r["eng"]
+    rounds = B * scale * args.steps
+    out = {
+        "metric": METRIC, "value": rounds / el, "unit": "consensus rounds/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * el / args.steps, "higher_is_better": True,
+        "scaling": "strong" if dshard else "weak", "vs_baseline": None,
+        "dtype": _dtype_name(mode, eng.storage, c), "data": "synthetic",
+        "config": {"model": c["model"], "global_batch": B * scale, "seq_len": c["D"],
+                   "parallelism": f"dshard{world}" if dshard else f"dp{world}", "engine_mode": mode,
+                   "storage": eng.storage, "n_oracles": c["N"], "dimension": c["D"], "n_failing": c["f"],
+                   "updates_per_instance_per_step": U, "oracle_updates_per_s": (U * rounds / el) if U else 0.0,
+                   "hip_graph": r["graph"], "ok_fraction": r["ok"], "backend_world": backend_world,
+                   "rank_ms_per_step": r["rank_ms"], "rank_ms_spread": [min(r["rank_ms"]), max(r["rank_ms"])],
+                   "rank_ok_fraction": r["rank_ok"], **r["extra"]},
+    }
+    if args.config in ("c2", "c3") and mode == "fast":
+        out["config"]["hbm_gbps_min_traffic"] = min_gbps(r, eng.values.element_size())
+    log_eng, log_step = eng, r["step"]
+    if alt:
+        # the same step at the alternative storage dtype (a fresh engine; the first one is freed first)
+        del r, eng
+        log_eng = log_step = None
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
+        ra = measure(args, c, alt, dev, rank, world, dshard)
+        out["config"]["alt_storage"] = {
+            "storage": ra["storage"], "value": ra["B"] * scale * args.steps / ra["elapsed"],
+            "ms_per_step": 1e3 * ra["elapsed"] / args.steps, "ok_fraction": ra["ok"],
+            "hbm_gbps_min_traffic": min_gbps(ra, ra["eng"].values.element_size()),
+            "rank_ms_spread": [min(ra["rank_ms"]), max(ra["rank_ms"])]}
+        log_eng, log_step = ra["eng"], ra["step"]
     if rank == 0:
-        out = {
-            "metric": METRIC, "value": value, "unit": "consensus rounds/s", "n_gpus": world,
-            "steps": steps_done, "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
-            "scaling": "strong" if dshard else "weak", "vs_baseline": None,
-            "dtype": f"{eng.storage}-wsad" if mode == "exact" else ("fp32-storage" if eng.storage == "fp32" else c.get("dtype", "bf16")), "data": "synthetic",
-            "config": {"model": c["model"], "global_batch": B * (1 if dshard else world), "seq_len": c["D"],
-                       "parallelism": f"dshard{world}" if dshard else f"dp{world}", "engine_mode": mode, "n_oracles": c["N"], "dimension": c["D"],
-                       "n_failing": c["f"], "updates_per_instance_per_step": U_per_inst,
-                       "oracle_updates_per_s": (U_per_inst * rounds / el) if U_per_inst else 0.0,
-                       "hip_graph": graph is not None, "ok_fraction": ok, **extra},
-        }
-        if args.config in ("c2", "c3"):
-            from svoc.utils.metrics import algorithmic_bytes_per_round
-            out["config"]["hbm_gbps_algorithmic"] = algorithmic_bytes_per_round(c["N"], c["D"], eng.values.element_size()) * rounds / el / 1e9
         print(json.dumps(out))
         if args.log:
             from svoc.utils.metrics import JsonlLogger, engine_health, kernel_table
             rec = dict(out)
-            rec["health"] = engine_health(eng)
+            rec["health"] = engine_health(log_eng)
             if args.kernel_table:
-                rec["kernels"] = kernel_table(lambda: step(0), steps=args.kernel_table)
+                rec["kernels"] = kernel_table(lambda: log_step(0), steps=args.kernel_table)
             with JsonlLogger(args.log, rank) as lg:
                 lg.log("bench", **rec)
     if world > 1:

@@ -145,7 +145,11 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
   p.mode = (int)mode;
   p.rel_dim = (int)rel_dim;
   p.legacy = legacy ? 1 : 0;
-  p.c1 = c1.data_ptr<float>();
+  // a whole round stages c1 and commits it only where the round succeeded (a reverted round leaves
+  // every output untouched); the D-sharded halves write it directly (mode 2 reads mode 1's c1)
+  at::Tensor c1_stage;
+  if (mode == 0) c1_stage = at::empty_like(c1);
+  p.c1 = mode == 0 ? c1_stage.data_ptr<float>() : c1.data_ptr<float>();
   p.consensus = cons.data_ptr<float>();
   p.skew = skew.data_ptr<float>();
   p.kurt = kurt.data_ptr<float>();
@@ -176,13 +180,12 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
   p.work_pairs = (int)fast_work_pairs(D);
   p.work_stride = words;
   auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
-  if (f32) {
-    const int rc = svoc_fast_round_f32(&p, stream);
-    TORCH_CHECK(rc == 0, "svoc_fast_round_f32 launch failed: ", rc);
-    return;
+  const int rc = f32 ? svoc_fast_round_f32(&p, stream) : svoc_fast_round_bf16(&p, stream);
+  TORCH_CHECK(rc == 0, f32 ? "svoc_fast_round_f32" : "svoc_fast_round_bf16", " launch failed: ", rc);
+  if (mode == 0) {
+    const int rc2 = svoc_commit_rows(c1_stage.data_ptr(), c1.data_ptr(), p.status, p.active, B, D, stream);
+    TORCH_CHECK(rc2 == 0, "svoc_commit_rows failed: ", rc2);
   }
-  const int rc = svoc_fast_round_bf16(&p, stream);
-  TORCH_CHECK(rc == 0, "svoc_fast_round_bf16 launch failed: ", rc);
 }
 
 // -------------------------------------------------------------------------------------- exact
@@ -254,7 +257,9 @@ void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& 
   p.n_failing = (int)n_failing;
   p.constrained = constrained ? 1 : 0;
   p.max_spread = max_spread;
-  p.c1 = c1.data_ptr<int64_t>();
+  at::Tensor c1_stage;   // whole rounds: c1 staged, committed where the round succeeded (as fast_round_hip)
+  if (mode == 0) c1_stage = at::empty_like(c1);
+  p.c1 = mode == 0 ? c1_stage.data_ptr<int64_t>() : c1.data_ptr<int64_t>();
   p.consensus = cons.data_ptr<int64_t>();
   p.skew = skew.data_ptr<int64_t>();
   p.kurt = kurt.data_ptr<int64_t>();
@@ -284,6 +289,10 @@ void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& 
   auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
   const int rc = svoc_exact_round(&p, stream);
   TORCH_CHECK(rc == 0, "svoc_exact_round launch failed: ", rc);
+  if (mode == 0) {
+    const int rc2 = svoc_commit_rows(c1_stage.data_ptr(), c1.data_ptr(), p.status, p.active, p.B, 2 * (int64_t)p.D, stream);
+    TORCH_CHECK(rc2 == 0, "svoc_commit_rows failed: ", rc2);
+  }
 }
 
 }  // namespace

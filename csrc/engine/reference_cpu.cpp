@@ -293,7 +293,9 @@ void fast_round_batch_cpu(const FastBatch& b, int threads) {
     FastOut o{c1.data(), qr.data(), rel.data(), cons.data(), sk.data(), ku.data(), 0.f, 0.f};
     int st = fast_round_one(x.data(), N, D, b.n_failing, b.constrained, b.max_spread, o, b.mode, b.rel_dim, b.legacy);
     b.status[i] = st;
-    if (b.c1 && b.n_failing <= N && N >= 2 && b.mode != 2) std::memcpy(b.c1 + i * D, c1.data(), D * sizeof(float));
+    // c1: written by pass 1 for the D-sharded second half; a whole round commits it only on success
+    if (b.c1 && b.n_failing <= N && N >= 2 && (b.mode == 1 || (b.mode == 0 && st == ST_OK)))
+      std::memcpy(b.c1 + i * D, c1.data(), D * sizeof(float));
     if (b.mode == 1) {
       if (st == ST_OK) std::memcpy(b.qr + i * N, qr.data(), N * sizeof(float));
       return;

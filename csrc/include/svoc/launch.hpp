@@ -130,6 +130,9 @@ struct UpdateParams {
 }  // namespace svoc
 
 extern "C" int svoc_apply_updates(const svoc::UpdateParams* p, hipStream_t stream);
+// row b of src -> dst (words 4-byte words per row) where status[b] == OK and (active null or set)
+extern "C" int svoc_commit_rows(const void* src, void* dst, const int32_t* status, const uint8_t* active, int64_t B,
+                                int64_t words, hipStream_t stream);
 
 extern "C" int svoc_qr_probe(const uint16_t* X, const float* C, float* qr, int B, int N, int D, int ld, int variant,
                              hipStream_t stream);

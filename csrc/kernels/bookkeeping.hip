@@ -47,9 +47,33 @@ __global__ __launch_bounds__(256) void round_epilogue_kernel(RoundBook r) {
   }
 }
 
+// Commit of staged per-instance rows (the round's c1): row b of src -> dst when instance b ran a round
+// (active, or every instance when active is null) and it succeeded.  A reverted round leaves dst
+// untouched, like every other output (contract.cairo:588-603).  Flat over B * words 4-byte words.
+__global__ __launch_bounds__(256) void commit_rows_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                         const int32_t* __restrict__ status,
+                                                         const uint8_t* __restrict__ active, uint32_t words,
+                                                         uint32_t total) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const uint32_t b = i / words;
+    if (status[b] == ST_OK && (!active || active[b])) dst[i] = src[i];
+  }
+}
+
 }  // namespace svoc
 
 using namespace svoc;
+
+extern "C" int svoc_commit_rows(const void* src, void* dst, const int32_t* status, const uint8_t* active, int64_t B,
+                                int64_t words, hipStream_t stream) {
+  const int64_t total = B * words;
+  if (total <= 0) return 0;
+  if (total >= (1ll << 32) || words <= 0) return -1;
+  const int64_t blocks = (total + 255) / 256;
+  hipLaunchKernelGGL(commit_rows_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, stream,
+                     (const uint32_t*)src, (uint32_t*)dst, status, active, (uint32_t)words, (uint32_t)total);
+  return (int)hipGetLastError();
+}
 
 extern "C" int svoc_round_prologue(const RoundBook* r, hipStream_t stream) {
   if (r->B <= 0) return 0;

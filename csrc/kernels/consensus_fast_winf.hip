@@ -23,6 +23,7 @@
 // falls back to consensus_fast_f32.hip otherwise.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <utility>
 
@@ -232,15 +233,28 @@ SVOC_DEV void qrf_moments_staged_even(__amdgpu_buffer_rsrc_t rs, int vo, int row
   }
 }
 
-template <int NSEG, int WAVES, int H, bool CONS, int MODE>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4))) void consensus_fast_winf_kernel(FastParams p) {
+// qr pass from the raw rows kept in registers across the network (RAW kernels: no re-read, no LDS).
+template <int P, bool MASKW, bool MASKROWS, int... Is>
+SVOC_DEV void qrf_regs_seq(uint32_t (&xs)[64], uint32_t mW, const QrCtxF& c, float* acc, f32x2& s1, f32x2& s2,
+                           f32x2& s3, f32x2& s4, std::integer_sequence<int, Is...>) {
+  if (MASKW) {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) xs[i] &= mW;
+  }
+  ((acc[Is] += qrf_tree<__builtin_ctz(P), Is, P, MASKROWS>(c, xs, s1, s2, s3, s4)), ...);
+}
+
+// RAW: the lane's 64 raw rows stay in registers across the window network (the qr pass reads them
+// there: no re-read, no LDS staging) at 3 waves per SIMD instead of 4.
+template <int NSEG, int WAVES, int H, bool CONS, int MODE, bool RAW>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW ? 3 : 4))) void consensus_fast_winf_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // columns per wave (phase A)
   constexpr int NPAD = 64 * NSEG;
   constexpr int W = WAVES * P;          // columns per workgroup step (phase A)
   constexpr int NT = WAVES * 64;
   constexpr int KEEP = 64 / P;
   // constrained: half of each slab (32 rows x 64 lanes, keys) staged per wave for the qr pass
-  constexpr bool STAGE = CONS && MODE != 2;
+  constexpr bool STAGE = CONS && MODE != 2 && !RAW;
   __shared__ uint32_t stage[STAGE ? WAVES * 32 * 64 : 1];
   __shared__ float qr_part[WAVES * NPAD];
   __shared__ float qr_lds[NPAD];
@@ -290,6 +304,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
     asm volatile("" : "+v"(nvl), "+v"(nll));
     float c1v;
     const uint32_t mW = vc ? 0xffffffffu : 0u;
+    uint32_t xs[RAW ? 64 : 1];   // RAW: the lane's raw rows, kept for the qr pass
     {
       uint32_t r[64];
       // (no sched_barrier after these loads -- it costs ~40 spilled VGPRs; the opaque stride keeps the
@@ -300,6 +315,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
         if (CONS) {
 #pragma unroll
           for (int i = 0; i < 64; ++i) r[i] = bload(rs, vo, i * rowb1);
+          if constexpr (RAW) {
+#pragma unroll
+            for (int i = 0; i < 64; ++i) xs[i] = r[i];
+          }
           // the staged rows go to LDS raw, straight from the load registers
           if constexpr (STAGE && NSEG == 4) {
 #pragma unroll
@@ -315,15 +334,21 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
           for (int i = 0; i < 64; ++i) r[i] ^= kp;
         } else {
 #pragma unroll
-          for (int i = 0; i < 64; ++i) r[i] = fkey<CONS>(bload(rs, vo, i * rowb1)) ^ pol;
+          for (int i = 0; i < 64; ++i) {
+            const uint32_t w = bload(rs, vo, i * rowb1);
+            if constexpr (RAW) xs[i] = w;
+            r[i] = fkey<CONS>(w) ^ pol;
+          }
         }
       } else {
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
           // real rows -> key; rows >= N -> 0 (the first lo1) / ~0 sentinels, so the middle of the
           // padded sort is the middle of the real rows
+          const uint32_t w = bload(rs, vo, i * rowb1);
+          if constexpr (RAW) xs[i] = w;
           const uint32_t hi_m = ~lt_mask(i, nll);
-          r[i] = ((fkey<CONS>(bload(rs, vo, i * rowb1)) & (lt_mask(i, nvl) | hi_m)) | hi_m) ^ pol;
+          r[i] = ((fkey<CONS>(w) & (lt_mask(i, nvl) | hi_m)) | hi_m) ^ pol;
         }
       }
       uint32_t klo, khi;
@@ -357,7 +382,16 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
     asm volatile("" : "+v"(vo2) : "v"(c1v));
     const QrCtxF qc{nvl, lane, vc ? c1v : 0.f};
     f32x2 s1 = {0.f, 0.f}, s2 = s1, s3 = s1, s4 = s1;
-    if (STAGE && N == NPAD) {
+    if constexpr (RAW) {
+      constexpr auto seq = std::make_integer_sequence<int, KEEP>{};
+      if ((s + 1) * W <= D) {
+        if (N == NPAD) qrf_regs_seq<P, false, false>(xs, mW, qc, acc, s1, s2, s3, s4, seq);
+        else qrf_regs_seq<P, false, true>(xs, mW, qc, acc, s1, s2, s3, s4, seq);
+      } else {
+        if (N == NPAD) qrf_regs_seq<P, true, false>(xs, mW, qc, acc, s1, s2, s3, s4, seq);
+        else qrf_regs_seq<P, true, true>(xs, mW, qc, acc, s1, s2, s3, s4, seq);
+      }
+    } else if (STAGE && N == NPAD) {
       if constexpr (STAGE && NSEG == 4) {
         if ((s + 1) * W <= D) qrf_moments_staged<P, false>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
         else qrf_moments_staged<P, true>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
@@ -715,22 +749,32 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   }
 }
 
-template <int NSEG, int WAVES, int H, bool CONS>
+template <int NSEG, int WAVES, int H, bool CONS, bool RAW>
 static void launch_winf_w(const FastParams& p, hipStream_t stream) {
-  if (p.mode == 1) hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 1>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
-  else if (p.mode == 2) hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 2>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
-  else hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 0>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+  if (p.mode == 1) hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 1, RAW>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+  else if (p.mode == 2) hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 2, false>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+  else hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 0, RAW>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
 }
 
-// Waves per workgroup: one workgroup per instance; N > 128 with at least two 8-wave slabs of columns
-// runs 8 waves (half the slabs per wave, 2 workgroups per CU: the bf16 kernel's measured choice,
-// profiles/r2_win_waves_ab.jsonl), everything else 4.
+// Geometry.  One workgroup per instance.  RAW (raw rows in registers, 3 waves per SIMD): 4-wave
+// workgroups.  Otherwise N > 128 with at least two 8-wave slabs of columns runs 8 waves (half the slabs
+// per wave, 2 workgroups per CU: the bf16 kernel's measured choice, profiles/r2_win_waves_ab.jsonl),
+// everything else 4.  SVOC_WINF_RAW=0/1 overrides the RAW choice (A/B).
+static int winf_raw(int nseg) {
+  static const int forced = [] {
+    const char* e = getenv("SVOC_WINF_RAW");
+    return e ? atoi(e) : -1;
+  }();
+  if (forced >= 0) return forced;
+  return nseg == 1 ? 1 : 0;
+}
 template <int NSEG, int H, bool CONS>
 static void launch_winf_c(const FastParams& p, hipStream_t stream) {
+  if (winf_raw(NSEG)) return launch_winf_w<NSEG, 4, H, CONS, true>(p, stream);
   if constexpr (NSEG == 4) {
-    if (p.D >= 2 * 8 * 16) return launch_winf_w<NSEG, 8, H, CONS>(p, stream);
+    if (p.D >= 2 * 8 * 16) return launch_winf_w<NSEG, 8, H, CONS, false>(p, stream);
   }
-  launch_winf_w<NSEG, 4, H, CONS>(p, stream);
+  launch_winf_w<NSEG, 4, H, CONS, false>(p, stream);
 }
 
 template <int NSEG>

@@ -76,6 +76,7 @@ class Client:
         self._lock = threading.RLock()        # one command at a time: the prompt and the auto-fetch loop
         self._auto_stop = threading.Event()
         self._auto_thread: Optional[threading.Thread] = None
+        self._auto_lock = threading.Lock()     # serialises auto_fetch on/off (FastAPI runs handlers in threads)
         self.auto_fetches = 0
         self.admins = [codec.shortstring(x) for x in ("Akashi", "Ozu", "Higuchi")]
         self.oracles = [codec.shortstring(f"oracle_{i:02d}") for i in range(N_ORACLES)]
@@ -142,12 +143,13 @@ class Client:
         return s
 
     # ---- auto fetch (simulation_mode, client/oracle_scheduler.py:163-171) -------------------------
-    def _auto_fetch_loop(self) -> None:
-        """Fetch, then sleep refresh_rate seconds, while auto_fetch stays on.  The reference runs this
-        loop inside the UI handler with eel.sleep; here it is a daemon thread next to the prompt."""
-        while not self._auto_stop.is_set():
+    def _auto_fetch_loop(self, stop: threading.Event) -> None:
+        """Fetch, then sleep refresh_rate seconds, until ``stop`` is set.  The reference runs this loop
+        inside the UI handler with eel.sleep; here it is a daemon thread next to the prompt.  Every loop
+        owns its stop event, so a loop that was switched off never comes back to life."""
+        while not stop.is_set():
             with self._lock:
-                if not self.flags["auto_fetch"]:
+                if stop.is_set() or not self.flags["auto_fetch"]:
                     break
                 try:
                     out = self.fetch()
@@ -155,23 +157,26 @@ class Client:
                     out = f"auto_fetch error: {e!r}"
                 self.auto_fetches += 1
             self.emit(out)
-            self._auto_stop.wait(self.refresh_rate)
+            stop.wait(self.refresh_rate)
 
     def set_auto_fetch(self, on: bool) -> str:
-        self.flags["auto_fetch"] = bool(on)
-        if on and (self._auto_thread is None or not self._auto_thread.is_alive()):
-            self._auto_stop.clear()
-            self._auto_thread = threading.Thread(target=self._auto_fetch_loop, name="svoc-auto-fetch", daemon=True)
-            self._auto_thread.start()
-            return "Auto-Fetch: ENABLED"
-        if not on:
-            self._auto_stop.set()
+        with self._auto_lock:
+            self.flags["auto_fetch"] = bool(on)
             t = self._auto_thread
-            if t is not None and t is not threading.current_thread():
-                t.join(timeout=max(1.0, 2 * self.refresh_rate) + 60.0)
+            if on:
+                if t is not None and t.is_alive() and not self._auto_stop.is_set():
+                    return "Auto-Fetch: ENABLED"      # already running: never a second loop
+                # (a loop switched off but still finishing a fetch exits on its own, already set event)
+                self._auto_stop = threading.Event()
+                self._auto_thread = threading.Thread(target=self._auto_fetch_loop, args=(self._auto_stop,),
+                                                     name="svoc-auto-fetch", daemon=True)
+                self._auto_thread.start()
+                return "Auto-Fetch: ENABLED"
+            self._auto_stop.set()
             self._auto_thread = None
-            return "Auto-Fetch: DISABLE"
-        return "Auto-Fetch: ENABLED"
+        if t is not None and t is not threading.current_thread():
+            t.join(timeout=max(1.0, 2 * self.refresh_rate) + 60.0)
+        return "Auto-Fetch: DISABLE"
 
     def close(self) -> None:
         self.set_auto_fetch(False)

@@ -95,12 +95,20 @@ class ConsensusEngine:
 
     # ------------------------------------------------------------------ sizing
     @staticmethod
-    def bytes_per_instance(n: int, d: int, mode: str = "fast") -> int:
-        """HBM bytes of state per instance (survey §7.6 sizing)."""
-        s = {"fast": 2, "exact": 8, "exact32": 4}[mode]
+    def bytes_per_instance(n: int, d: int, mode: str = "fast", storage: Optional[str] = None) -> int:
+        """HBM bytes of state per instance (survey §7.6 sizing).  ``storage``: the value dtype
+        ("bf16" / "fp32" fast, "int64" / "int32" exact; default bf16 fast, int64 exact); the legacy
+        mode name "exact32" means exact with int32 storage."""
+        if mode == "exact32":
+            mode, storage = "exact", storage or "int32"
+        s = {"bf16": 2, "fp32": 4, "int64": 8, "int32": 4}[storage or ("bf16" if mode == "fast" else "int64")]
         o = 4 if mode == "fast" else 8
         ld = _round_up(d, 8) if mode == "fast" else d
         return n * ld * s + 4 * d * o + n * (1 + 1 + o + 4) + 2 * o + 4 + 4 + 2
+
+    def state_bytes_per_instance(self) -> int:
+        """bytes_per_instance for this engine's own mode and storage dtype."""
+        return self.bytes_per_instance(self.N, self.D, self.mode, self.storage)
 
     # ------------------------------------------------------------------ updates
     def _as_storage(self, vals: torch.Tensor) -> torch.Tensor:

@@ -32,6 +32,10 @@ import torch.distributed as dist
 from ..status import Status
 
 
+# exact mode: a shard's qr partial is < 2^58, so the int64 sum of at most 2^5 partials cannot wrap
+MAX_EXACT_SHARDS = 32
+
+
 def shard_bounds(D: int, rank: int, world: int):
     per = (D + world - 1) // world
     lo = min(D, rank * per)
@@ -62,7 +66,7 @@ def run_round_sharded(engine, d_global: int, group=None, world: int = 1) -> None
     if e.mode == "fast":
         mx = float(e.cfg.unconstrained_max_spread)
         w = e.work()                                     # window kernel: pass 1 -> pass 2 state
-        head = (e.values, e._active, e.D, e.cfg.n_failing_oracles, e.cfg.constrained, mx, e.c1)
+        head = (e.values, e._active, e.D, e.cfg.n_failing_oracles, e.cfg.constrained, mx, sh.c1)
         # pass 1: local c1 + qr partials (into the shadow qr: the committed qr stays intact)
         e._ops.fast_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status,
                           e.wave_hint, 1, d_global, lg, w)
@@ -72,6 +76,10 @@ def run_round_sharded(engine, d_global: int, group=None, world: int = 1) -> None
         e._ops.fast_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status,
                           e.wave_hint, 2, d_global, lg, w)
     else:
+        if world > MAX_EXACT_SHARDS:
+            # each shard's int64 qr partial is bounded below 2^58 (status.hpp kExactQrPartialMax); the SUM
+            # all-reduce of more than 32 of them could wrap int64 and silently change the rank mask
+            raise ValueError(f"exact D-sharding supports at most {MAX_EXACT_SHARDS} shards (got {world})")
         head = (e.values, e._active, e.cfg.n_failing_oracles, e.cfg.constrained, e.cfg.max_spread_wsad, sh.c1)
         # first half: c1 + int64 qr partials; a shard that fails here (overflow) fails the round
         e._ops.exact_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status, lg,
@@ -92,7 +100,6 @@ def run_round_sharded(engine, d_global: int, group=None, world: int = 1) -> None
     e.rel.copy_(torch.where(ok1, sh.rel, e.rel))
     e.qr.copy_(torch.where(ok1, sh.qr, e.qr))
     e.reliable.copy_(torch.where(ok1, sh.reliable, e.reliable))
-    if e.mode != "fast":
-        e.c1.copy_(torch.where(ok1, sh.c1, e.c1))
+    e.c1.copy_(torch.where(ok1, sh.c1, e.c1))
     e._ops.round_epilogue(e._active, e.status, e.rel, e.consensus_active, e.touched, e.metrics_fx)
     e.rounds += 1

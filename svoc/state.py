@@ -54,6 +54,17 @@ def save(svc, path: str) -> None:
                            [s[1].detach().cpu().contiguous() for s in secs], [s[2] for s in secs])
 
 
+_DTYPE_STORAGE = {"float32": "fp32", "bfloat16": "bf16", "int64": "int64", "int32": "int32"}
+
+
+def storage_of(meta: dict):
+    """Storage name of a checkpoint.  Checkpoints written before the 'storage' key existed carry only
+    value_dtype: map it, so an fp32 fast checkpoint is not silently restored at bf16."""
+    if meta.get("storage"):
+        return meta["storage"]
+    return _DTYPE_STORAGE.get(str(meta.get("value_dtype", "")))
+
+
 def load(path: str, device="cpu"):
     """Rebuild a :class:`svoc.api.ConsensusService` from a checkpoint."""
     from .api import ConsensusService
@@ -67,7 +78,7 @@ def load(path: str, device="cpu"):
     # placeholder addresses, then the checkpoint's limb tensors copied in directly (no per-instance
     # host conversion: a 1M-instance checkpoint restores in seconds)
     svc = ConsensusService(cfg, B, [0] * cfg.n_admins, [0] * cfg.n_oracles, device=device, mode=meta["mode"],
-                           storage=meta.get("storage"))
+                           storage=storage_of(meta))
     e, g = svc.engine, svc.gov
     dev = e.device
     if cfg.n_admins:

@@ -141,6 +141,9 @@ def engine_health(engine) -> Dict[str, float]:
         rounds=int(getattr(engine, "rounds", 0)))
 
 
-def algorithmic_bytes_per_round(n: int, d: int, storage_bytes: int = 2) -> int:
-    """HBM bytes a fast round must move at minimum: the [N, D] values read once per pass."""
-    return 2 * n * d * storage_bytes
+def algorithmic_bytes_per_round(n: int, d: int, storage_bytes: int = 2, updates: int = 0) -> int:
+    """Lower bound of the HBM bytes one fast round must move (a data-flow floor, not a measurement):
+    the [N, D] values read ONCE (the one-network window kernels need no second read), the round's
+    outputs (consensus, skewness, kurtosis: 3 x D fp32; qr, reliable: N x 5 B; two reliabilities and a
+    status), plus, for streaming configs, the ``updates`` fresh rows read and written into the state."""
+    return n * d * storage_bytes + 3 * d * 4 + 5 * n + 12 + 2 * updates * d * storage_bytes

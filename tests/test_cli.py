@@ -56,3 +56,26 @@ def test_auto_fetch_is_a_periodic_loop(tmp_path):
     assert any("oracle 0x" in o for o in outs)          # auto_commit ran
     time.sleep(0.2)
     assert cl.auto_fetches == n                          # stopped
+
+
+def test_auto_fetch_concurrent_toggles_keep_one_loop(tmp_path):
+    """Concurrent 'auto_fetch on' requests (FastAPI handlers run in a thread pool) start one loop; 'on'
+    right after 'off' never revives the old loop next to the new one."""
+    import threading
+    import time
+    cl = Client(db_path=str(tmp_path / "db.sqlite"), refresh_rate=0.05, emit=lambda s: None)
+    ts = [threading.Thread(target=cl.set_auto_fetch, args=(True,)) for _ in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    loops = [t for t in threading.enumerate() if t.name == "svoc-auto-fetch"]
+    assert len(loops) == 1
+    for _ in range(3):
+        cl.set_auto_fetch(False)
+        cl.set_auto_fetch(True)
+    time.sleep(0.3)
+    assert len([t for t in threading.enumerate() if t.name == "svoc-auto-fetch" and t.is_alive()]) == 1
+    cl.set_auto_fetch(False)
+    time.sleep(0.2)
+    assert not [t for t in threading.enumerate() if t.name == "svoc-auto-fetch" and t.is_alive()]

@@ -115,7 +115,8 @@ def _ds_revert_worker(rank, world, port, outdir, x1, x2, cfgd):
         e.enabled.fill_(1); e.n_active.fill_(cfg.n_oracles); e.touched.fill_(1)
         run_round_sharded(e, cfg.dimension, world=world)
         out[k] = dict(cons=e.consensus.clone(), rel=e.rel.clone(), reliable=e.reliable.clone(), qr=e.qr.clone(),
-                      skew=e.skew.clone(), kurt=e.kurt.clone(), st=e.status.clone(), act=e.consensus_active.clone())
+                      skew=e.skew.clone(), kurt=e.kurt.clone(), st=e.status.clone(), act=e.consensus_active.clone(),
+                      c1=e.c1.clone())
     torch.save(dict(out=out, lo=lo, hi=hi), os.path.join(outdir, f"dsr{rank}.pt"))
     dist.destroy_process_group()
 
@@ -150,7 +151,7 @@ def test_dsharding_revert_is_atomic_across_shards():
         o1, o2 = s["out"][0], s["out"][1]
         assert o2["st"].tolist() == [0, 32, 0, 32]
         for inst in (1, 3):   # reverted: every output identical to round 1, bit for bit
-            for k in ("cons", "rel", "reliable", "qr", "skew", "kurt"):
+            for k in ("cons", "rel", "reliable", "qr", "skew", "kurt", "c1"):
                 assert torch.equal(o2[k][inst], o1[k][inst]), (k, inst)
         for inst in (0, 2):
             assert not torch.equal(o2["cons"][inst], o1["cons"][inst])
@@ -220,3 +221,15 @@ def test_dsharding_exact_bit_identical(constrained, world):
                 assert torch.equal(o[name], ref_o[name]), (k, name)
             for name in ("consensus", "skew", "kurt", "c1"):
                 assert torch.equal(o[name], ref_o[name][:, lo:hi]), (k, name)
+
+
+def test_dsharding_exact_rejects_more_than_32_shards():
+    """Exact D-sharding all-reduces int64 qr partials bounded below 2^58: more than 32 shards could wrap
+    the sum, so the sharded round refuses."""
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    from svoc.parallel.dshard import MAX_EXACT_SHARDS, run_round_sharded
+    e = ConsensusEngine(ConsensusConfig(n_oracles=8, dimension=4, n_failing_oracles=1, constrained=True), 2,
+                        device="cpu", mode="exact")
+    with pytest.raises(ValueError):
+        run_round_sharded(e, 4 * (MAX_EXACT_SHARDS + 1), world=MAX_EXACT_SHARDS + 1)

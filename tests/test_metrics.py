@@ -98,6 +98,25 @@ def test_bench_gpus_flag_spawns_ranks_gloo(tmp_path):
     assert len(lines) == 1, r.stdout          # rank 0 only
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["config"]["global_batch"] == 16
+    assert out["config"]["backend_world"] == 2 and len(out["config"]["rank_ms_per_step"]) == 2
+
+
+def test_bench_gpus_8_spawns_eight_ranks_gloo(tmp_path):
+    """The driver's 8-GPU form, `python bench.py --gpus 8`, rehearsed at world 8 on gloo: eight ranks, one
+    JSON line from rank 0, the backend's own world size, per-rank step times and outcomes."""
+    cfg = _cpu_cfg(tmp_path)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config-file", cfg, "--gpus", "8",
+                        "--steps", "3", "--warmup", "1"], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    c = out["config"]
+    assert out["n_gpus"] == 8 and c["backend_world"] == 8 and c["parallelism"] == "dp8"
+    assert c["global_batch"] == 8 * 8 and len(c["rank_ms_per_step"]) == 8 and len(c["rank_ok_fraction"]) == 8
+    lo, hi = c["rank_ms_spread"]
+    assert 0 < lo <= hi and abs(out["ms_per_step"] - hi) < 1e-6 * max(1.0, hi)   # the job time is the slowest rank
+    assert all(o == 1.0 for o in c["rank_ok_fraction"]) and c["ok_fraction"] == 1.0
 
 
 def test_bench_gpus_world_mismatch_fails(tmp_path):
@@ -115,4 +134,5 @@ def test_bench_fp32_storage_cpu(tmp_path):
                        timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    assert out["dtype"] == "fp32-storage" and out["value"] > 0 and out["config"]["ok_fraction"] == 1.0
+    assert out["dtype"] == "fp32" and out["config"]["storage"] == "fp32"
+    assert out["value"] > 0 and out["config"]["ok_fraction"] == 1.0

@@ -4,7 +4,8 @@ The reference reverts the whole transaction on any failed assert (contract.cairo
 variance column (sqrt(0) -> wsad_div by zero, math.cairo:322,331), a reliability outside [0, 1]
 (contract.cairo:467,488) or fewer than 4 reliable oracles (kurtosis (n-2)(n-3) = 0, math.cairo:362).
 Every fast HIP kernel (window, register-streaming, LDS-tiled, small-instance) stages its pass-2
-outputs and commits only when the instance's final status is OK.
+outputs and commits only when the instance's final status is OK; the pass-1 essence c1 is staged by the
+op and committed by svoc_commit_rows on the same condition.
 """
 import pytest
 import torch
@@ -14,8 +15,8 @@ from svoc import ops as svops
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-SENT = {"consensus": 7.25, "skew": -3.5, "kurt": 11.0, "rel": 0.125, "qr": 42.0, "reliable": 9}
-OUTS = ("consensus", "skew", "kurt", "rel", "qr", "reliable")
+SENT = {"consensus": 7.25, "skew": -3.5, "kurt": 11.0, "rel": 0.125, "qr": 42.0, "reliable": 9, "c1": 0.8125}
+OUTS = ("consensus", "skew", "kurt", "rel", "qr", "reliable", "c1")
 
 
 def _run(x, D, f, constrained, active, hint):
@@ -82,7 +83,7 @@ def test_engine_revert_keeps_previous_round():
     e.randomize(seed=3)
     e.run_round()
     assert (e.status == 0).all()
-    snap = {k: getattr(e, k).clone() for k in ("consensus", "skew", "kurt", "rel", "qr", "reliable")}
+    snap = {k: getattr(e, k).clone() for k in ("consensus", "skew", "kurt", "rel", "qr", "reliable", "c1")}
     inst = torch.tensor([2] * 64, device=DEV)
     orc = torch.arange(64, device=DEV)
     vals = torch.full((64, 1024), 0.5, device=DEV)      # every oracle of instance 2 -> one point

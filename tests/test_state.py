@@ -105,3 +105,23 @@ def test_fast_mode_roundtrip(tmp_path, storage):
     assert b.engine.storage == storage and b.engine.values.dtype == a.engine.values.dtype
     assert torch.equal(a.engine.values, b.engine.values)
     assert torch.equal(a.engine.consensus, b.engine.consensus)
+
+
+def test_old_checkpoint_without_storage_key(tmp_path, monkeypatch):
+    """A checkpoint from before the 'storage' meta key (only value_dtype) restores at its own dtype: an
+    fp32 fast checkpoint is not silently narrowed to bf16."""
+    import json
+    assert state.storage_of({"value_dtype": "float32"}) == "fp32"
+    assert state.storage_of({"value_dtype": "int32", "storage": "int32"}) == "int32"
+    cfg = ConsensusConfig(n_oracles=16, dimension=20, n_failing_oracles=2, n_admins=2)
+    a = ConsensusService(cfg, 4, ADMINS[:2], [100 + i for i in range(16)], device="cpu", mode="fast", storage="fp32")
+    a.engine.randomize(0)
+    a.engine.run_round()
+    dumps = json.dumps
+    monkeypatch.setattr(json, "dumps", lambda m, **k: dumps({x: y for x, y in m.items() if x != "storage"}, **k))
+    p = os.path.join(tmp_path, "old.svoc")
+    state.save(a, p)
+    monkeypatch.setattr(json, "dumps", dumps)
+    b = state.load(p)
+    assert b.engine.storage == "fp32"
+    assert torch.equal(a.engine.values, b.engine.values)
