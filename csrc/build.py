@@ -61,7 +61,7 @@ def build(force: bool = False, jobs: int = 8, debug: bool = False, verbose: bool
     jobs_list = []
     for src in hip_srcs:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-        # SVOC_HIPCC_FLAGS: extra kernel flags for A/B builds (e.g. -DSVOC_WIN_NT_STAGE=2)
+        # SVOC_HIPCC_FLAGS: extra kernel flags for A/B builds of experimental variants
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", *opt, *inc,
                *os.environ.get("SVOC_HIPCC_FLAGS", "").split(), "-c", src, "-o", obj]
         jobs_list.append((src, obj, cmd))

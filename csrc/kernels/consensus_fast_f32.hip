@@ -43,15 +43,6 @@
 #include "svoc/sortnet.hpp"
 #include "svoc/status.hpp"
 
-#ifndef SVOC_F32_KEEP_RAW
-#define SVOC_F32_KEEP_RAW 1   // N <= 64: the raw column kept in registers across the sort networks (no re-reads)
-#endif
-#ifndef SVOC_F32_RAW_NSEG
-#define SVOC_F32_RAW_NSEG 16   // lane groups that keep the raw column in pass 1 (all: fewer waves, still faster)
-#endif
-#ifndef SVOC_F32_WPE
-#define SVOC_F32_WPE 1   // waves per SIMD the register budget is capped for (4: <= 128 VGPRs)
-#endif
 
 namespace svoc {
 
@@ -112,13 +103,16 @@ SVOC_DEV T seg_sum(T v) {
 // MODE: 0 whole round; 1 pass 1 only (c1 + this shard's qr partials); 2 from the all-reduced qr
 // (D-sharding, svoc/parallel/dshard.py).
 template <int NSEG, int WAVES, bool CONS, int MODE>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC_F32_WPE))) void consensus_fast_f32_kernel(FastParams p) {
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(1))) void consensus_fast_f32_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;      // columns per wave
   constexpr int NPAD = 64 * NSEG;   // padded oracle rows
   constexpr int W = WAVES * P;      // columns per slab
   constexpr int NT = WAVES * 64;
   constexpr int KEEP = 64 / P;      // qr rows a lane holds after the butterfly
-  constexpr bool KEEP_RAW = SVOC_F32_KEEP_RAW && NSEG <= SVOC_F32_RAW_NSEG;   // pass 1 without the column re-read
+  // the raw column stays in registers across the pass-1 network (no re-read), at the waves per SIMD
+  // that register budget allows (capping at 128 VGPRs spilled and lost: profiles/r2_f32_wpe_ab.txt,
+  // r2_f32_keep_raw_ab.txt, r2_f32_raw_nseg_ab.txt)
+  constexpr bool KEEP_RAW = true;
   __shared__ float qr_part[WAVES * NPAD];
   __shared__ float qr_lds[NPAD];
   constexpr int NM = NSEG < 4 ? 4 : NSEG;   // 64-row mask words

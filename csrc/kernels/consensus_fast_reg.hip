@@ -1,11 +1,11 @@
 // Fused two-pass robust consensus, fast mode, "register-streaming" variant: no LDS tile.
 //
-// Same semantics and outputs as consensus_fast.hip (contract/src/contract.cairo:442-503 /
-// :370-434; see that file).  Difference: every lane loads its column-pair segment (64 rows x 2
-// bf16 = one dword per row) straight from HBM/L2 into VGPRs, so the workgroup holds no [N x W] LDS
-// tile and there is no slab barrier: occupancy is set by VGPRs only (the LDS tile capped the tiled
-// kernel at 2 workgroups per CU), and waves drift freely so one wave's loads overlap another's
-// sorting network.  The qr pass re-reads the same dwords (L2/MALL-hot, just touched); pass 2 reads
+// Semantics: contract/src/contract.cairo:442-503 (constrained) / :370-434 (unconstrained).  The
+// two-network fallback of the bf16 window kernel (consensus_fast_win.hip: f > 32, N > 256, or no
+// pass-1 windows in D-sharded mode 2) and the cross-check the tests compare it with (wave_hint -7).
+// Every lane loads its column-pair segment (64 rows x 2 bf16 = one dword per row) straight from
+// HBM/L2 into VGPRs: no LDS tile and no slab barrier, so occupancy is set by VGPRs only and waves
+// drift freely (one wave's loads overlap another's sorting network).  The qr pass re-reads the same dwords (L2/MALL-hot, just touched); pass 2 reads
 // the instance again, with unreliable rows turned into max-key sentinels by a register OR.
 // LDS holds only the per-wave qr partials, the reduced qr, the reliable bitmask and the status.
 #include <hip/hip_runtime.h>
@@ -16,16 +16,12 @@
 #include "svoc/sortnet.hpp"
 #include "svoc/status.hpp"
 
-#ifndef SVOC_REG_WIDE_BATCH
-#define SVOC_REG_WIDE_BATCH 0   // N > 256: batched qr re-read, 2 waves per SIMD
-#endif
-
 namespace svoc {
 
 // MODE 0: fused round; 1: pass 1 only (c1 + qr -> global); 2: rank + pass 2 from the global qr
 // (D-sharding: the caller all-reduces the qr partials in between).
-template <int NSEG, int WAVES, bool CONS, int MODE, bool RAW = false>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((RAW || (SVOC_REG_WIDE_BATCH && NSEG >= 8)) ? 2 : 4))) void consensus_fast_reg_kernel(FastParams p) {
+template <int NSEG, int WAVES, bool CONS, int MODE>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4))) void consensus_fast_reg_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // column pairs per wave
   constexpr int NPAD = 64 * NSEG;       // padded oracle rows
   constexpr int W = WAVES * P * 2;      // columns per workgroup step
@@ -78,17 +74,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((RAW
     float cA, cB;
     // columns past D contribute 0 to qr: their bf16 halves are masked to +0 and their centre is +0
     const uint32_t mW = vA ? (vB ? 0xffffffffu : 0x0000ffffu) : 0u;
-    uint32_t wraw[RAW ? 64 : 1];  // RAW: keep the raw words for the qr pass (no re-read)
     {
       u16x2 r[64];
-      if (RAW) {
-#pragma unroll
-        for (int i = 0; i < 64; ++i) {
-          wraw[i] = bload(rs, vo, i * rowb) & mW;
-          const uint32_t hi_m = ~lt_mask(i, nll);
-          r[i] = as_k((as_u32(to_key<CONS>(wraw[i])) & (lt_mask(i, nvl) | hi_m)) | hi_m);
-        }
-      } else if (N == NPAD) {  // uniform: no padding rows
+      if (N == NPAD) {  // uniform: no padding rows
         if (CONS) {  // key and run polarity in one XOR: raw ^ (0x80008000 ^ pol)
           const uint32_t kp = 0x80008000u ^ pol;
 #pragma unroll
@@ -104,7 +92,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((RAW
           r[i] = as_k((as_u32(to_key<CONS>(bload(rs, vo, i * rowb))) & (lt_mask(i, nvl) | hi_m)) | hi_m);
         }
       }
-      if (RAW || N != NPAD) {
+      if (N != NPAD) {
 #pragma unroll
         for (int i = 0; i < 64; ++i) r[i] = as_k(as_u32(r[i]) ^ pol);
       }
@@ -122,27 +110,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((RAW
     __builtin_amdgcn_sched_barrier(0);
     float part[64];
     const f32x2 c2 = {vA ? cA : 0.f, vB ? cB : 0.f};
-    constexpr bool WB = SVOC_REG_WIDE_BATCH && NSEG >= 8 && !RAW;
-    if constexpr (WB) {
-      // wide groups: the re-read as one batch of 64 loads ordered after the network's result (empty
-      // asm); written inline it kept two loads in flight
-      uint32_t wv[64];
-      int vo2 = vo;
-      asm volatile("" : "+v"(vo2) : "v"(cA), "v"(cB));
-#pragma unroll
-      for (int i = 0; i < 64; ++i) wv[i] = bload(rs, vo2, i * rowb);
-      __builtin_amdgcn_sched_barrier(0);
-      const uint32_t mm = (s + 1) * W > D ? mW : 0xffffffffu;
+    if ((s + 1) * W > D) {  // slab with columns past D (uniform): masked words
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
-        const f32x2 y = bf16x2_to_f32x2(wv[i] & mm) - c2;
-        const f32x2 q = y * y;
-        part[i] = q.x + q.y;
-      }
-    } else if (RAW || (s + 1) * W > D) {  // slab with columns past D (uniform): masked words
-#pragma unroll
-      for (int i = 0; i < 64; ++i) {
-        const uint32_t w = RAW ? wraw[i] : bload(rs, vo, i * rowb) & mW;  // else: L2/MALL-hot re-read
+        const uint32_t w = bload(rs, vo, i * rowb) & mW;  // L2/MALL-hot re-read
         const f32x2 y = bf16x2_to_f32x2(w) - c2;          // v_pk_add_f32
         const f32x2 q = y * y;                              // v_pk_mul_f32
         part[i] = q.x + q.y;
@@ -390,10 +361,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((RAW
   }
 }
 
-template <int NSEG, int WAVES, int MODE, bool RAW = false>
+template <int NSEG, int WAVES, int MODE>
 static void launch_reg_mode(const FastParams& p, hipStream_t stream) {
-  auto k = p.constrained ? consensus_fast_reg_kernel<NSEG, WAVES, true, MODE, RAW>
-                         : consensus_fast_reg_kernel<NSEG, WAVES, false, MODE, RAW>;
+  auto k = p.constrained ? consensus_fast_reg_kernel<NSEG, WAVES, true, MODE>
+                         : consensus_fast_reg_kernel<NSEG, WAVES, false, MODE>;
   hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
 }
 
@@ -403,8 +374,6 @@ static int launch_reg(const FastParams& p, hipStream_t stream) {
     launch_reg_mode<NSEG, WAVES, 1>(p, stream);
   } else if (p.mode == 2) {
     launch_reg_mode<NSEG, WAVES, 2>(p, stream);
-  } else if (p.wave_hint == -6) {
-    launch_reg_mode<NSEG, WAVES, 0, true>(p, stream);  // fused, raw words kept in VGPRs (no re-read)
   } else {
     // fused single launch.  (The former split form, hint -1, published the qr partials into the
     // output qr between its two launches: not revert-safe, removed.)
@@ -422,12 +391,8 @@ extern "C" int svoc_fast_round_bf16_reg(const FastParams* p, hipStream_t stream)
   if (p->N < 2 || p->N > 1024 || p->ld % 8 != 0 || p->D > p->ld) return -1;
   if (p->mode != 1 && (!p->work || p->work_pairs < fast_work_pairs(p->D) || p->work_stride < fast_work_words(p->D)))
     return -1;   // pass 2 stages its outputs in the workspace
-  // wave_hint -3 / -4: 8 / 2 waves per workgroup (fused); default 4 (16 waves per CU at <= 128 VGPRs)
-  if (p->N <= 64) {
-    if (p->wave_hint == -3) return launch_reg<1, 8>(*p, stream);
-    if (p->wave_hint == -4) return launch_reg<1, 2>(*p, stream);
-    return launch_reg<1, 4>(*p, stream);
-  }
+  // 4 waves per workgroup (16 waves per CU at <= 128 VGPRs)
+  if (p->N <= 64) return launch_reg<1, 4>(*p, stream);
   if (p->N <= 128) return launch_reg<2, 4>(*p, stream);
   if (p->N <= 256) return launch_reg<4, 4>(*p, stream);
   if (p->N <= 512) return launch_reg<8, 4>(*p, stream);

@@ -26,7 +26,6 @@
 // f - a + 1 <= H (H = 5 or 17); the dispatcher falls back to consensus_fast_reg.hip otherwise.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 
 #include <utility>
 
@@ -34,18 +33,6 @@
 #include "svoc/launch.hpp"
 #include "svoc/sortnet.hpp"
 #include "svoc/status.hpp"
-
-#ifndef SVOC_WIN_NT_STAGE
-#define SVOC_WIN_NT_STAGE 0
-#endif
-#ifndef SVOC_WIN_NT_REREAD
-#define SVOC_WIN_NT_REREAD 0
-#endif
-// SVOC_WIN_KEEP_RAW=1: the half of each slab that is not staged in LDS stays in 32 VGPRs across the
-// pass-1 window network (no qr re-read from memory), at 3 waves per SIMD instead of 4
-#ifndef SVOC_WIN_KEEP_RAW
-#define SVOC_WIN_KEEP_RAW 0
-#endif
 
 namespace svoc {
 
@@ -148,22 +135,17 @@ SVOC_DEV void qr_moments(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t m
 // i % 4 < 2, 32 rows) were written to the wave's LDS region as keys right after the pass-1 load; trees
 // 2 and 3 (32 rows) are re-read from memory, all 32 loads issued first so their latency overlaps the
 // LDS trees.  Same trees, same order of accumulation as qr_moments: bit-identical results.
-template <int P, bool MASKW, bool RAW = false>
+template <int P, bool MASKW>
 SVOC_DEV void qr_moments_staged(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, uint32_t kp,
                                 const uint32_t* st, int lane, const QrCtx& c, float* acc, f32x2& s1, f32x2& s2,
-                                f32x2& s3, f32x2& s4, const uint32_t* kr = nullptr) {
+                                f32x2& s3, f32x2& s4) {
   static_assert(P == 16, "staging layout: KEEP = 4 trees of 16 rows");
   constexpr int KEEP = 4, S = 4;
-  uint32_t wm[64];   // trees 2 and 3 from memory (indices i % 4 >= 2), or kept in registers (RAW)
+  uint32_t wm[64];   // trees 2 and 3 from memory (indices i % 4 >= 2)
 #pragma unroll
   for (int m = 0; m < 16; ++m) {
-    if constexpr (RAW) {
-      wm[2 + KEEP * m] = kr[2 * m];
-      wm[3 + KEEP * m] = kr[2 * m + 1];
-    } else {
-      wm[2 + KEEP * m] = bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (2 + KEEP * m) * rowb);
-      wm[3 + KEEP * m] = bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (3 + KEEP * m) * rowb);
-    }
+    wm[2 + KEEP * m] = bload(rs, vo, (2 + KEEP * m) * rowb);
+    wm[3 + KEEP * m] = bload(rs, vo, (3 + KEEP * m) * rowb);
   }
   {
     uint32_t wv[64];
@@ -202,17 +184,16 @@ SVOC_DEV void qr_moments_staged(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uin
 // in-flight loads; the first butterfly half of the single tree when KEEP = 1) come from the wave's
 // LDS region, the odd rows are re-read from memory with all 32 loads issued before the LDS reads.
 // Same trees, same leaf order as qr_moments: bit-identical results.
-template <int P, bool MASKW, bool RAW = false>
+template <int P, bool MASKW>
 SVOC_DEV void qr_moments_staged_even(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, uint32_t kp,
                                      const uint32_t* st, int lane, const QrCtx& c, float* acc, f32x2& s1,
-                                     f32x2& s2, f32x2& s3, f32x2& s4, const uint32_t* kr = nullptr) {
+                                     f32x2& s2, f32x2& s3, f32x2& s4) {
   constexpr int KEEP = 64 / P, S = __builtin_ctz(P);
   static_assert(KEEP <= 2, "even-row staging: one or two trees");
   if constexpr (KEEP == 1) {
     uint32_t wv[64];
 #pragma unroll
-    for (int m = 0; m < 32; ++m)
-      wv[2 * m + 1] = RAW ? kr[m] : bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (2 * m + 1) * rowb);
+    for (int m = 0; m < 32; ++m) wv[2 * m + 1] = bload(rs, vo, (2 * m + 1) * rowb);
 #pragma unroll
     for (int m = 0; m < 32; ++m) wv[2 * m] = st[m * 64 + lane] ^ kp;
     if (MASKW) {
@@ -221,10 +202,9 @@ SVOC_DEV void qr_moments_staged_even(__amdgpu_buffer_rsrc_t rs, int vo, int rowb
     }
     acc[0] += qr_tree<S, 0, P, false>(c, wv, s1, s2, s3, s4);
   } else {
-    uint32_t wm[64];   // tree 1 (odd rows) from memory, loads issued first (or kept in registers: RAW)
+    uint32_t wm[64];   // tree 1 (odd rows) from memory, loads issued first
 #pragma unroll
-    for (int m = 0; m < 32; ++m)
-      wm[2 * m + 1] = RAW ? kr[m] : bload_p<SVOC_WIN_NT_REREAD>(rs, vo, (2 * m + 1) * rowb);
+    for (int m = 0; m < 32; ++m) wm[2 * m + 1] = bload(rs, vo, (2 * m + 1) * rowb);
     {
       uint32_t wv[64];
 #pragma unroll
@@ -244,7 +224,7 @@ SVOC_DEV void qr_moments_staged_even(__amdgpu_buffer_rsrc_t rs, int vo, int rowb
 }
 
 template <int NSEG, int WAVES, int H, bool CONS, int MODE>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC_WIN_KEEP_RAW ? 3 : 4))) void consensus_fast_win_kernel(FastParams p) {
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4))) void consensus_fast_win_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // column pairs per wave (phase A)
   constexpr int NPAD = 64 * NSEG;
   constexpr int W = WAVES * P * 2;      // columns per workgroup step (phase A)
@@ -290,7 +270,6 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
   float acc[KEEP];
 #pragma unroll
   for (int i = 0; i < KEEP; ++i) acc[i] = 0.f;
-  constexpr bool RAW = SVOC_WIN_KEEP_RAW && STAGE && (NSEG == 4 || NSEG == 1);
 
   // ------------------------------------------------------------ phase A: pass 1
   const int pass1_slabs = MODE == 2 ? 0 : nslab;
@@ -304,34 +283,21 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
     asm volatile("" : "+v"(nvl), "+v"(nll));
     float cA, cB;
     const uint32_t mW = vA ? (vB ? 0xffffffffu : 0x0000ffffu) : 0u;
-    uint32_t kr[RAW ? 32 : 1];   // the rows not staged in LDS, raw (RAW: no qr re-read)
     {
       u16x2 r[64];
       if (N == NPAD) {
         if (CONS) {
 #pragma unroll
-          for (int i = 0; i < 64; ++i) {
-            // rows staged in LDS are not read again: streaming policy for them, so the L2 keeps the
-            // rows the qr pass re-reads (SVOC_WIN_NT_STAGE, profiles/r2_win_nt_ab.txt)
-            const bool staged = STAGE && (NSEG == 4 ? (i & 3) < 2 : (i & 1) == 0);
-            r[i] = as_k((staged ? bload_p<SVOC_WIN_NT_STAGE>(rs, vo, i * rowb) : bload(rs, vo, i * rowb)) ^ kp);
-          }
+          for (int i = 0; i < 64; ++i) r[i] = as_k(bload(rs, vo, i * rowb) ^ kp);
           if constexpr (STAGE && NSEG == 4) {
 #pragma unroll
             for (int m = 0; m < 16; ++m) {
               stw[(2 * m) * 64 + lane] = as_u32(r[4 * m]);
               stw[(2 * m + 1) * 64 + lane] = as_u32(r[4 * m + 1]);
-              if constexpr (RAW) {
-                kr[2 * m] = as_u32(r[4 * m + 2]) ^ kp;
-                kr[2 * m + 1] = as_u32(r[4 * m + 3]) ^ kp;
-              }
             }
           } else if constexpr (STAGE) {
 #pragma unroll
-            for (int m = 0; m < 32; ++m) {
-              stw[m * 64 + lane] = as_u32(r[2 * m]);
-              if constexpr (RAW) kr[m] = as_u32(r[2 * m + 1]) ^ kp;
-            }
+            for (int m = 0; m < 32; ++m) stw[m * 64 + lane] = as_u32(r[2 * m]);
           }
         } else {
 #pragma unroll
@@ -382,11 +348,11 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(SVOC
     f32x2 s1 = {0.f, 0.f}, s2 = s1, s3 = s1, s4 = s1;
     if (STAGE && N == NPAD) {
       if constexpr (STAGE && NSEG == 4) {
-        if ((s + 1) * W <= D) qr_moments_staged<P, false, RAW>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4, kr);
-        else qr_moments_staged<P, true, RAW>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4, kr);
+        if ((s + 1) * W <= D) qr_moments_staged<P, false>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
+        else qr_moments_staged<P, true>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
       } else if constexpr (STAGE) {
-        if ((s + 1) * W <= D) qr_moments_staged_even<P, false, RAW>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4, kr);
-        else qr_moments_staged_even<P, true, RAW>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4, kr);
+        if ((s + 1) * W <= D) qr_moments_staged_even<P, false>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
+        else qr_moments_staged_even<P, true>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
       }
     } else if ((s + 1) * W <= D) {
       if (N == NPAD) qr_moments<P, false, false>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
@@ -771,36 +737,22 @@ static void launch_win_w(const FastParams& p, hipStream_t stream) {
   else hipLaunchKernelGGL((consensus_fast_win_kernel<NSEG, WAVES, H, CONS, 0>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
 }
 
-// Waves per workgroup (N > 128).  One workgroup per instance; 4 waves x 4 workgroups per CU (LDS
-// and the 128-VGPR cap) fill the 4 wave slots of every SIMD only from B = 4 x CUs instances on, and
-// c3's pipelined step launches ranges of 256-512.  8 waves (half the slabs per wave, 75 KiB of LDS,
-// 2 workgroups per CU) fill the SIMDs from 2 x CUs instances on and measured faster at every range
+// Waves per workgroup.  One workgroup per instance; 4 waves x 4 workgroups per CU (LDS and the
+// 128-VGPR cap) fill the 4 wave slots of every SIMD only from B = 4 x CUs instances on, and c3's
+// pipelined step launches ranges of 256-512.  For N > 128, 8 waves (half the slabs per wave, 75 KiB of
+// LDS, 2 workgroups per CU) fill the SIMDs from 2 x CUs instances on and measured faster at every range
 // count, also at 1024 instances (c3: 4 waves 763 k / 771 k / 690 k rounds/s at 1 / 2 / 4 ranges,
 // 8 waves 784 k / 782 k / 803 k, 16 waves 757 k / 775 k / 728 k; profiles/r2_win_waves_ab.jsonl).
-// SVOC_WIN_WAVES=4|8|16 forces one.
+// N <= 64 (c2: the grid is full) stays at 4 (profiles/r2_win_waves_c2.jsonl).
 static int win_waves(const FastParams& p, int nseg) {
-  static const int forced = [] {
-    const char* e = getenv("SVOC_WIN_WAVES");
-    return e ? atoi(e) : 0;
-  }();
-  if (nseg == 1) return forced == 2 || forced == 8 ? forced : 4;
-  if (nseg != 4) return 4;
-  if (forced == 4 || forced == 8 || forced == 16) return forced;
   constexpr int W8 = 8 * 16 * 2;   // columns per 8-wave slab
-  return p.D >= 2 * W8 ? 8 : 4;
+  return nseg == 4 && p.D >= 2 * W8 ? 8 : 4;
 }
 
 template <int NSEG, int H, bool CONS>
 static void launch_win_c(const FastParams& p, hipStream_t stream) {
-  if constexpr (NSEG == 1) {
-    const int w = win_waves(p, NSEG);
-    if (w == 2) return launch_win_w<NSEG, 2, H, CONS>(p, stream);
-    if (w == 8) return launch_win_w<NSEG, 8, H, CONS>(p, stream);
-  }
   if constexpr (NSEG == 4) {
-    const int w = win_waves(p, NSEG);
-    if (w == 8) return launch_win_w<NSEG, 8, H, CONS>(p, stream);
-    if (w == 16) return launch_win_w<NSEG, 16, H, CONS>(p, stream);
+    if (win_waves(p, NSEG) == 8) return launch_win_w<NSEG, 8, H, CONS>(p, stream);
   }
   launch_win_w<NSEG, 4, H, CONS>(p, stream);
 }
@@ -830,4 +782,23 @@ extern "C" int svoc_fast_round_bf16_win(const FastParams* p, hipStream_t stream)
   else if (p->N <= 128) launch_win<2>(*p, H, stream);
   else launch_win<4>(*p, H, stream);
   return (int)hipGetLastError();
+}
+
+extern "C" int svoc_fast_round_bf16_reg(const FastParams* p, hipStream_t stream);
+extern "C" int svoc_fast_round_bf16_small(const FastParams* p, hipStream_t stream);
+
+// The bf16-storage fast round: which kernel runs.
+//   small instances (N <= 16, D <= 128, whole round): several instances per wave, registers only
+//     (consensus_fast_small.hip);
+//   default: this one-network window kernel where it applies (workspace given, f <= 32, N <= 256);
+//   otherwise, and for wave_hint -7 (tests: the cross-check), the two-network register-streaming kernel
+//     (consensus_fast_reg.hip).
+extern "C" int svoc_fast_round_bf16(const FastParams* p, hipStream_t stream) {
+  if (p->B <= 0) return 0;
+  if (p->wave_hint == 0 && p->mode == 0 && p->N <= 16 && p->D <= 128) return svoc_fast_round_bf16_small(p, stream);
+  if (p->wave_hint != -7) {
+    const int rc = svoc_fast_round_bf16_win(p, stream);
+    if (rc != -2) return rc;
+  }
+  return svoc_fast_round_bf16_reg(p, stream);
 }

@@ -16,7 +16,6 @@ from __future__ import annotations
 
 import dataclasses
 import math
-import os
 from typing import List, Optional
 
 import torch
@@ -96,7 +95,6 @@ class PackPlan:
     B: int
     S: int
     max_len: int
-    parts: Optional[list] = None   # sequence-range sub-plans for the two-stream overlap (see overlap)
 
 
 def _linear_gelu(x: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
@@ -126,12 +124,8 @@ class SentimentEncoder(nn.Module):
         self.head = nn.Linear(c.hidden, c.n_labels)
         self.apply(self._init)
         self.packed = True                 # unpadded token path on the GPU (see plan())
-        # sequence ranges interleaved over two HIP streams (packed path): the memory-bound attention /
-        # LayerNorm kernels of one range overlap the GEMMs of the next (_forward_overlapped).  Off by
-        # default: c4 1918 vs 2053 windows/s single-stream (half-size GEMMs lose more than the overlap
-        # gains; docs/PERF.md).  SVOC_ENC_OVERLAP=2 turns it on.
-        self.overlap = int(os.environ.get("SVOC_ENC_OVERLAP", "1"))
-        self._side_streams = {}
+        # (a two-stream variant that overlapped one sequence range's attention / LayerNorm with the
+        # next range's GEMMs measured 1918 vs 2053 windows/s single-stream and is gone: docs/PERF.md)
         self._plan_cache = []              # [(mask tensor, version, plan)], most recent last
         # random-init head scaled so the synthetic scores spread like a trained multi-label head's
         # (larger logits than the default init): keeps honest bootstrap oracles distinguishable at wsad
@@ -164,82 +158,10 @@ class SentimentEncoder(nn.Module):
             cu[1:] = lens.cumsum(0).to(torch.int32)
             plan = PackPlan(idx=idx, pos=idx % S + 2, cu=cu, lens=lens.to(torch.float32).clamp(min=1), T=int(idx.numel()),
                             B=B, S=S, max_len=int(lens.max()) if B else 0)
-            if self.overlap > 1 and B >= 2 * self.overlap:
-                # contiguous sequence ranges (their tokens are contiguous in packed order); host values
-                # computed here, once per mask, so replays need no synchronisation
-                cuh = cu.cpu().tolist()
-                parts = []
-                for k in range(self.overlap):
-                    b0, b1 = k * B // self.overlap, (k + 1) * B // self.overlap
-                    t0, t1 = cuh[b0], cuh[b1]
-                    parts.append(PackPlan(idx=idx[t0:t1], pos=plan.pos[t0:t1], cu=(cu[b0:b1 + 1] - t0).contiguous(),
-                                          lens=plan.lens[b0:b1], T=t1 - t0, B=b1 - b0, S=S, max_len=plan.max_len))
-                plan.parts = parts
         self._plan_cache = self._plan_cache[-3:] + [(attention_mask, attention_mask._version, plan)]
         return plan
 
-    def _side_stream(self, k: int, device) -> torch.cuda.Stream:
-        key = (k, device.index)
-        if key not in self._side_streams:
-            self._side_streams[key] = torch.cuda.Stream(device=device)
-        return self._side_streams[key]
-
-    def _forward_overlapped(self, ids: torch.Tensor, p: PackPlan) -> torch.Tensor:
-        """The packed forward on the plan's sequence ranges with two HIP streams: every GEMM of every
-        range on the main stream (one GEMM at a time: hipBLASLt's stream-K kernels are not run
-        concurrently), the memory-bound attention and residual-add + LayerNorm kernels on a side
-        stream, handed over by events, so that range k's attention / LayerNorm runs under range k+1's
-        GEMMs.  Capturable in a HIP graph (events become graph edges)."""
-        from .. import ops as svops
-        o = svops.ops()
-        main = torch.cuda.current_stream(ids.device)
-        side = self._side_stream(1, ids.device)
-
-        def handoff(src, dst, *ts):   # dst waits for src's work so far; ts are used on dst from here
-            ev = torch.cuda.Event()
-            ev.record(src)
-            dst.wait_event(ev)
-            for t in ts:
-                t.record_stream(dst)
-
-        flat = ids.reshape(-1)
-        K = len(p.parts)
-        xs = [o.embed_layernorm(flat[q.idx], q.pos, self.tok.weight, self.pos.weight, self.typ.weight,
-                                self.ln.weight, self.ln.bias, self.ln.eps) for q in p.parts]
-        on_side = [False] * K   # x[k] last written on the side stream
-        for layer in self.layers:
-            att = [None] * K
-            for k, q in enumerate(p.parts):
-                if on_side[k]:
-                    handoff(side, main, xs[k])
-                qkv = layer.qkv(xs[k])
-                handoff(main, side, qkv)
-                with torch.cuda.stream(side):
-                    att[k] = o.attention_varlen(qkv, q.cu, q.max_len, layer.heads)
-            for k in range(K):
-                handoff(side, main, att[k])
-                y = layer.out(att[k])
-                handoff(main, side, y, xs[k])
-                with torch.cuda.stream(side):
-                    xs[k] = _add_ln(xs[k], y, layer.ln1)
-            for k in range(K):
-                handoff(side, main, xs[k])
-                f = layer.fc2(_linear_gelu(xs[k], layer.fc1))
-                handoff(main, side, f, xs[k])
-                with torch.cuda.stream(side):
-                    xs[k] = _add_ln(xs[k], f, layer.ln2)
-                on_side[k] = True
-        for k in range(K):
-            if on_side[k]:
-                handoff(side, main, xs[k])
-        pooled = [xs[k][q.cu[:-1].long()] if self.cfg.pool == "cls" else o.segment_mean(xs[k], q.cu)
-                  for k, q in enumerate(p.parts)]
-        h = torch.tanh(self.dense(torch.cat(pooled)))
-        return torch.sigmoid(self.head(h).float())
-
     def _forward_packed(self, ids: torch.Tensor, p: PackPlan) -> torch.Tensor:
-        if p.parts is not None and self.overlap > 1:
-            return self._forward_overlapped(ids, p)
         from .. import ops as svops
         o = svops.ops()
         # embeddings + LayerNorm in one HIP kernel (gather, two adds, LN), [T, H]

@@ -133,23 +133,3 @@ def test_segment_mean_bf16():
     assert torch.equal(out[1].float(), torch.zeros(H, device="cuda"))
     cpu = svops.ops().segment_mean(x.cpu(), cu.cpu())
     torch.testing.assert_close(out.cpu().float(), cpu.float(), rtol=1e-2, atol=1e-2)
-
-
-def test_encoder_overlapped_streams_match_single_stream():
-    """Two sequence ranges on two HIP streams (layer-interleaved) give the single-stream scores."""
-    from svoc.models.encoder import EncoderConfig, build
-    cfg = EncoderConfig(vocab_size=500, hidden=768, layers=2, heads=12, ffn=3072, max_positions=130)
-    enc = build("cuda", torch.bfloat16, seed=5, cfg=cfg)
-    g = torch.Generator().manual_seed(3)
-    lens = torch.randint(1, 129, (24,), generator=g)
-    ids = torch.randint(3, 500, (24, 128), generator=g).cuda()
-    mask = (torch.arange(128)[None] < lens[:, None]).to(torch.int64).cuda()
-    with torch.no_grad():
-        enc.overlap = 2
-        a = enc(ids, mask)
-        assert enc.plan(mask).parts is not None and sum(q.T for q in enc.plan(mask).parts) == int(lens.sum())
-        enc.overlap, enc._plan_cache = 1, []
-        b = enc(ids, mask)
-        assert enc.plan(mask).parts is None
-    torch.cuda.synchronize()
-    torch.testing.assert_close(a, b, rtol=0, atol=0.02)

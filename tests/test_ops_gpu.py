@@ -30,11 +30,8 @@ _SHAPES = [(7, 6, 2, True), (64, 1024, 8, True), (64, 1000, 8, False), (50, 300,
            (7, 6, 2, False), (16, 100, 3, True), (9, 1, 2, True), (12, 128, 4, False), (8, 33, 2, True)]
 
 
-# hint 0: default dispatch (window kernel / small kernel); -7: register-streaming kernel; -3 / -4: 8 / 2
-# waves per workgroup; 1 / 2 / 8: the LDS-tiled kernel (consensus_fast.hip)
-@pytest.mark.parametrize("N,D,f,constrained,hint",
-                         [s + (h,) for s in _SHAPES for h in (0, -7, 1)]
-                         + [(64, 1024, 8, True, h) for h in (-3, -4, 2, 8)] + [(33, 70, 4, False, h) for h in (-3, -4)])
+# hint 0: default dispatch (window kernel / small kernel); -7: the two-network register-streaming kernel
+@pytest.mark.parametrize("N,D,f,constrained,hint", [s + (h,) for s in _SHAPES for h in (0, -7)])
 def test_fast_hip_vs_torch(N, D, f, constrained, hint):
     B = 12
     x, _ = beta_oracles(B, N, D, f, seed=7 * N + D)
@@ -186,8 +183,8 @@ def test_fast_hip_split_modes_match_full(N, D, f, constrained):
         torch.testing.assert_close(os_["rel"][ok], full["rel"][ok], rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("N,D,hint", [(7, 6, 0), (64, 1024, 0), (256, 700, 0), (64, 1024, -6), (200, 96, -6),
-                                      (128, 512, 1)])
+@pytest.mark.parametrize("N,D,hint", [(7, 6, 0), (64, 1024, 0), (256, 700, 0), (64, 1024, -7), (200, 96, -7),
+                                      (128, 512, 0)])
 def test_fast_kernels_deterministic(N, D, hint):
     """Same inputs -> bitwise identical outputs (no float atomics; fixed reduction orders)."""
     x, _ = beta_oracles(9, N, D, max(1, N // 8), seed=N + D)

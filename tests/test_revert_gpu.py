@@ -3,7 +3,7 @@
 The reference reverts the whole transaction on any failed assert (contract.cairo:588-603): a zero
 variance column (sqrt(0) -> wsad_div by zero, math.cairo:322,331), a reliability outside [0, 1]
 (contract.cairo:467,488) or fewer than 4 reliable oracles (kurtosis (n-2)(n-3) = 0, math.cairo:362).
-Every fast HIP kernel (window, register-streaming, LDS-tiled, small-instance) stages its pass-2
+Every fast HIP kernel (window, register-streaming, small-instance) stages its pass-2
 outputs and commits only when the instance's final status is OK; the pass-1 essence c1 is staged by the
 op and committed by svoc_commit_rows on the same condition.
 """
@@ -30,9 +30,9 @@ def _run(x, D, f, constrained, active, hint):
 
 
 # (N, D, f, constrained, wave_hint): window kernel (H 5 / 17, NSEG 1 / 2 / 4, unconstrained), the
-# register-streaming kernel (forced, f > 32), the LDS-tiled kernel, the small kernel
+# register-streaming kernel (forced, f > 32), the small kernel
 CASES = [(64, 1024, 8, True, 0), (256, 600, 32, True, 0), (128, 512, 16, True, 0), (100, 260, 10, False, 0),
-         (64, 1024, 8, True, -7), (128, 300, 40, True, 0), (64, 1000, 8, False, -7), (64, 256, 8, True, 1),
+         (64, 1024, 8, True, -7), (128, 300, 40, True, 0), (64, 1000, 8, False, -7), (64, 256, 8, True, -7),
          (200, 136, 20, False, -7), (7, 6, 2, True, 0), (16, 100, 3, False, 0)]
 
 
@@ -62,7 +62,7 @@ def test_revert_leaves_outputs_untouched(N, D, f, constrained, hint):
             assert bool((oc[k][b] == SENT[k]).all()) == untouched, (k, b)
 
 
-@pytest.mark.parametrize("N,D,hint", [(64, 512, 0), (34, 512, 0), (64, 512, -7), (8, 6, 0), (40, 200, 1)])
+@pytest.mark.parametrize("N,D,hint", [(64, 512, 0), (34, 512, 0), (64, 512, -7), (8, 6, 0), (40, 200, -7)])
 def test_too_few_reliable_reverts(N, D, hint):
     """f = N - 3: three reliable oracles, kurtosis undefined -> every round reverts."""
     B, f = 4, N - 3
