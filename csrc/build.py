@@ -36,6 +36,15 @@ def headers():
     return glob.glob(os.path.join(CSRC, "**", "*.hpp"), recursive=True)
 
 
+def file_flags(src):
+    """Extra hipcc flags a kernel source asks for in its header (``// svoc-hipcc-flags: ...``)."""
+    with open(src, encoding="utf-8") as f:
+        for _, line in zip(range(60), f):
+            if "svoc-hipcc-flags:" in line:
+                return line.split("svoc-hipcc-flags:", 1)[1].split()
+    return []
+
+
 def stale(obj, src, deps):
     if not os.path.exists(obj):
         return True
@@ -61,8 +70,9 @@ def build(force: bool = False, jobs: int = 8, debug: bool = False, verbose: bool
     jobs_list = []
     for src in hip_srcs:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        # per-file kernel flags: a "// svoc-hipcc-flags: ..." line in the source's header comment
         # SVOC_HIPCC_FLAGS: extra kernel flags for A/B builds of experimental variants
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", *opt, *inc,
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", *opt, *inc, *file_flags(src),
                *os.environ.get("SVOC_HIPCC_FLAGS", "").split(), "-c", src, "-o", obj]
         jobs_list.append((src, obj, cmd))
     py_inc = sysconfig.get_paths()["include"]

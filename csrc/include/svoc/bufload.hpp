@@ -18,6 +18,19 @@ SVOC_DEV __amdgpu_buffer_rsrc_t instance_rsrc(const void* base, uint32_t bytes) 
                                            (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
+// The same descriptor as four SGPR words, for inline asm (buffer_load ... lds): words 0-1 base, 2
+// num_records, 3 the flags make_buffer_rsrc sets.
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+struct BufDesc {
+  v4i_t w;
+};
+SVOC_DEV BufDesc buf_desc(const void* base, uint32_t bytes) {
+  const uint64_t pa = (uint64_t)base;
+  return BufDesc{v4i_t{(int)__builtin_amdgcn_readfirstlane((uint32_t)pa),
+                       (int)(__builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32)) & 0xffffu),
+                       (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000}};
+}
+
 SVOC_DEV uint32_t bload(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
 }

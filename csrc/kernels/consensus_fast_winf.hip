@@ -17,13 +17,17 @@
 //     the reliable rows' power sums are the all-row sums minus the removed rows' (fp64 combination),
 //     with an exact two-pass recomputation for columns where that difference would cancel.
 // Versus consensus_fast_f32.hip (the two-network kernel): no second 64*NSEG-key network and no second
-// read of the instance.  HBM per round: the pass-1 read, half of it re-read for the qr pass (the other
-// half staged in LDS, constrained), the window round trip and the f removed rows.
+// read of the instance.  HBM per round: ONE read of the instance (phase A streams it through LDS by
+// DMA, double-buffered against the compute through the registers: see SlabDma), the window round trip
+// and the f removed rows.
 // Valid for f <= 32 with a + 1 <= H and f - a + 1 <= H (a = N/2 - R/2, H = 5 or 17); the dispatcher
 // falls back to consensus_fast_f32.hip otherwise.
+//
+// svoc-hipcc-flags: -fno-slp-vectorize
+// (ROCm 7.2's SLP vectorizer turns the 64-key register arrays into <2 x i32> groups whose instruction
+// selection crashes clang; the packed math here is written with explicit f32x2 types anyway.)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include <stdlib.h>
 
 #include <utility>
 
@@ -75,39 +79,40 @@ SVOC_DEV bool moments_from_sums_d(double n, double t1, double t2, double t3, dou
   return true;
 }
 
-// The lane's rows {I0 + STEP * m}, every load issued before any is consumed.  The row stride is made
-// opaque here, so the SGPR row offsets are recomputed per batch (s_mul) instead of being hoisted out of
-// the slab loop into 64 live SGPRs -- spilled to VGPR lanes, and then the compiler serialises every
-// load behind its v_readlane and its consumer (one load in flight).
-template <int I0, int STEP, int CNT>
-SVOC_DEV void load_rows(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t (&x)[64]) {
-  asm volatile("" : "+s"(rowb));
+// qr partials of the lane's 64 rows (one column), reduced across the wave's P columns by the
+// transposing butterfly (stage MSK exchanges with lane ^ MSK and halves the row set: the lane ends with
+// the KEEP = 64 / P row sums its "base" slot names in the qr reduction below), with the power sums of
+// d = x - c1 accumulated on the way, two rows (i, i + 32) per packed instruction (v_pk_add / v_pk_fma).
+// The row leaves are formed in one flat pass over the raw rows kept in registers (no re-read).
+// MASKW: slab with columns past D (mw = 0 there: words +0, centre +0); MASKROWS: rows >= N (read as 0)
+// masked out of the power sums.
+template <int MSK, int H>
+SVOC_DEV void qr_halve(float (&part)[64], int lane) {
+  if constexpr (MSK >= 1) {
+    const bool up = (lane & MSK) != 0;
 #pragma unroll
-  for (int m = 0; m < CNT; ++m) x[I0 + STEP * m] = bload(rs, vo, (I0 + STEP * m) * rowb);
-  __builtin_amdgcn_sched_barrier(0);
+    for (int i = 0; i < H; ++i) {
+      const float lo_v = part[i], hi_v = part[i + H];
+      const float send = up ? lo_v : hi_v;
+      const float keep = up ? hi_v : lo_v;
+      part[i] = keep + xor_lane<MSK>(send);
+    }
+    qr_halve<MSK / 2, H / 2>(part, lane);
+  }
 }
-
-// qr partials of the lane's 64 rows (one column) reduced across the wave's P columns by the
-// transposing butterfly (stage L exchanges with lane ^ (P >> L) and halves the row set), evaluated
-// depth-first.  The two leaves of a level-1 node (rows I and I + 32) are formed as one packed pair, so
-// the power sums of d = x - c1 accumulate on v_pk_add / v_pk_fma (two rows per instruction).
-// MASKROWS: rows >= N (read as 0 past the buffer end) are masked out of the power sums.
-struct QrCtxF {
-  int nvl, lane;
-  float c;
-};
-template <int L, int I, int P, bool MASKROWS>
-SVOC_DEV float qrf_tree(const QrCtxF& c, const uint32_t (&wv)[64], f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
-  static_assert(L >= 1, "level-1 nodes are the packed leaves");
-  constexpr int msk = P >> L;
-  float lo_v, hi_v;
-  if constexpr (L == 1) {
-    f32x2 y = f32x2{u2f(wv[I]), u2f(wv[I + 32])} - f32x2{c.c, c.c};
+template <int P, bool MASKW, bool MASKROWS>
+SVOC_DEV void qr_moments_regs(const uint32_t (&xs)[64], int nvl, float c, uint32_t mw, int lane, float* acc,
+                              f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
+  float part[64];
+#pragma unroll
+  for (int m = 0; m < 32; ++m) {
+    const uint32_t w0 = MASKW ? xs[m] & mw : xs[m], w1 = MASKW ? xs[m + 32] & mw : xs[m + 32];
+    f32x2 y = f32x2{u2f(w0), u2f(w1)} - f32x2{c, c};
     f32x2 q = y * y;
-    lo_v = q.x;
-    hi_v = q.y;
+    part[m] = q.x;
+    part[m + 32] = q.y;
     if (MASKROWS) {
-      const uint32_t m0 = lt_mask(I, c.nvl), m1 = lt_mask(I + 32, c.nvl);
+      const uint32_t m0 = lt_mask(m, nvl), m1 = lt_mask(m + 32, nvl);
       const float y0 = y.x, y1 = y.y, q0 = q.x, q1 = q.y;
       y = f32x2{fand(y0, m0), fand(y1, m1)};
       q = f32x2{fand(q0, m0), fand(q1, m1)};
@@ -116,146 +121,63 @@ SVOC_DEV float qrf_tree(const QrCtxF& c, const uint32_t (&wv)[64], f32x2& s1, f3
     s2 += q;
     s3 = __builtin_elementwise_fma(q, y, s3);
     s4 = __builtin_elementwise_fma(q, q, s4);
-  } else {
-    lo_v = qrf_tree<L - 1, I, P, MASKROWS>(c, wv, s1, s2, s3, s4);
-    hi_v = qrf_tree<L - 1, I + (64 >> L), P, MASKROWS>(c, wv, s1, s2, s3, s4);
   }
-  const bool up = (c.lane & msk) != 0;
-  const float send = up ? lo_v : hi_v;
-  const float keep = up ? hi_v : lo_v;
-  return keep + xor_lane<msk>(send);
-}
-// One butterfly tree (final slot I): its 64/KEEP rows are loaded together, then reduced depth-first; an
-// empty asm closes the tree so the next tree's loads are not hoisted into it.
-template <int P, int I, bool MASKW, bool MASKROWS>
-SVOC_DEV void qrf_tree_slot(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, const QrCtxF& c, float* acc,
-                            f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
-  constexpr int KEEP = 64 / P;
-  uint32_t wv[64];
-  load_rows<I, KEEP, 64 / KEEP>(rs, vo, rowb, wv);
-  if (MASKW) {
+  qr_halve<P / 2, 32>(part, lane);
 #pragma unroll
-    for (int m = 0; m < 64 / KEEP; ++m) wv[I + KEEP * m] &= mW;
-  }
-  constexpr int S = __builtin_ctz(P);
-  acc[I] += qrf_tree<S, I, P, MASKROWS>(c, wv, s1, s2, s3, s4);
-  asm volatile("" : "+v"(acc[I]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
-}
-template <int P, bool MASKW, bool MASKROWS, int... Is>
-SVOC_DEV void qrf_seq(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, const QrCtxF& c, float* acc,
-                      f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4, std::integer_sequence<int, Is...>) {
-  (qrf_tree_slot<P, Is, MASKW, MASKROWS>(rs, vo, rowb, mW, c, acc, s1, s2, s3, s4), ...);
-}
-template <int P, bool MASKW, bool MASKROWS>
-SVOC_DEV void qrf_moments(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, const QrCtxF& c, float* acc,
-                          f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
-  qrf_seq<P, MASKW, MASKROWS>(rs, vo, rowb, mW, c, acc, s1, s2, s3, s4, std::make_integer_sequence<int, 64 / P>{});
+  for (int i = 0; i < 64 / P; ++i) acc[i] += part[i];
 }
 
-// qr pass with half of the slab staged in LDS (N = NPAD = 256, constrained): trees 0 and 1 (rows
-// i % 4 < 2) come from the wave's LDS region (raw bits, written straight from the pass-1 load registers),
-// trees 2 and 3 are re-read with all 32 loads issued first so their latency overlaps the LDS trees.
-template <int P, bool MASKW>
-SVOC_DEV void qrf_moments_staged(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, uint32_t kp,
-                                 const uint32_t* st, int lane, const QrCtxF& c, float* acc, f32x2& s1, f32x2& s2,
-                                 f32x2& s3, f32x2& s4) {
-  static_assert(P == 16, "staging layout: KEEP = 4 trees of 16 rows");
-  constexpr int KEEP = 4, S = 4;
-  uint32_t wm[64];
-  {
-    asm volatile("" : "+s"(rowb));
+// One phase-A slab of the workgroup lands in LDS by DMA (buffer_load_dwordx4 ... lds: no VGPR
+// destination).  Layout: [NPAD rows][WC = WAVES * P columns], 4-byte words, rows lane-linear in 16-B
+// chunks as the DMA writes them; the chunk of global column c of row r sits at column c ^ (P * (r >> 6))
+// (a chunk-level XOR applied on the DMA's SOURCE address, the LDS side stays lane-linear), so the reader
+// instruction -- P consecutive columns of the NSEG rows i, 64 + i, ... -- touches 64 distinct banks.
+// One DMA instruction moves 64 chunks = 1 KiB; a slab is 16 instructions per wave.
+template <int NSEG, int WAVES>
+struct SlabDma {
+  static constexpr int P = 64 / NSEG, WC = WAVES * P, CPR = WC / 4, RPI = 64 / CPR;
+  int vlane;   // this lane's part of every piece's voffset: (l / CPR) row of the piece, (l % CPR) chunk
+  int lchunk;
+  SVOC_DEV SlabDma(int lane, int rowb) : vlane((lane / CPR) * rowb), lchunk(lane % CPR) {}
+  // issue this wave's 16 pieces of the slab whose first column is col0.  Inline asm: the
+  // __builtin_amdgcn_raw_ptr_buffer_load_lds form crashes ROCm 7.2's instruction selection inside this
+  // kernel (register pressure of the network + qr pass around it); M0 is saved and restored around the
+  // piece (the compiler reserves it), and the caller waits for the pieces with an explicit vmcnt(0).
+  SVOC_DEV void issue(const BufDesc& rs, uint32_t* slab, int wave, int rowb, int col0) const {
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      wm[2 + KEEP * m] = bload(rs, vo, (2 + KEEP * m) * rowb);
-      wm[3 + KEEP * m] = bload(rs, vo, (3 + KEEP * m) * rowb);
+    for (int j = 0; j < 16; ++j) {
+      const int k = wave * 16 + j;                      // piece: rows k * RPI .. k * RPI + RPI - 1
+      const int swz = (P / 4) * ((k * RPI) >> 6);       // chunk XOR of those rows (uniform per piece)
+      const int vo = vlane + 16 * (lchunk ^ swz) + col0 * 4;
+      const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(slab + k * 256);
+      int keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\t"
+          "s_mov_b32 m0, %3\n\t"
+          "s_nop 0\n\t"
+          "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+          "s_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(vo), "s"(rs.w), "s"(lds), "s"(k * RPI * rowb)
+          : "memory");
     }
   }
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    uint32_t wv[64];
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      wv[t + KEEP * m] = st[(2 * m + t) * 64 + lane];
-      if (MASKW) wv[t + KEEP * m] &= mW;
-    }
-    if (t == 0) acc[0] += qrf_tree<S, 0, P, false>(c, wv, s1, s2, s3, s4);
-    else acc[1] += qrf_tree<S, 1, P, false>(c, wv, s1, s2, s3, s4);
-    asm volatile("" : "+v"(acc[0]), "+v"(acc[1]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
-  }
-  if (MASKW) {
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-      wm[2 + KEEP * m] &= mW;
-      wm[3 + KEEP * m] &= mW;
-    }
-  }
-  acc[2] += qrf_tree<S, 2, P, false>(c, wm, s1, s2, s3, s4);
-  asm volatile("" : "+v"(acc[2]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
-  acc[3] += qrf_tree<S, 3, P, false>(c, wm, s1, s2, s3, s4);
-}
+};
 
-// qr pass with the even rows staged in LDS for N <= 128 (NSEG 1 and 2, constrained): the odd rows are
-// re-read with all 32 loads issued before the LDS reads.
-template <int P, bool MASKW>
-SVOC_DEV void qrf_moments_staged_even(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t mW, uint32_t kp,
-                                      const uint32_t* st, int lane, const QrCtxF& c, float* acc, f32x2& s1,
-                                      f32x2& s2, f32x2& s3, f32x2& s4) {
-  constexpr int KEEP = 64 / P, S = __builtin_ctz(P);
-  static_assert(KEEP <= 2, "even-row staging: one or two trees");
-  if constexpr (KEEP == 1) {
-    uint32_t wv[64];
-    load_rows<1, 2, 32>(rs, vo, rowb, wv);
-#pragma unroll
-    for (int m = 0; m < 32; ++m) wv[2 * m] = st[m * 64 + lane];
-    if (MASKW) {
-#pragma unroll
-      for (int i = 0; i < 64; ++i) wv[i] &= mW;
-    }
-    acc[0] += qrf_tree<S, 0, P, false>(c, wv, s1, s2, s3, s4);
-  } else {
-    uint32_t wm[64];
-    load_rows<1, 2, 32>(rs, vo, rowb, wm);
-    {
-      uint32_t wv[64];
-#pragma unroll
-      for (int m = 0; m < 32; ++m) {
-        wv[2 * m] = st[m * 64 + lane];
-        if (MASKW) wv[2 * m] &= mW;
-      }
-      acc[0] += qrf_tree<S, 0, P, false>(c, wv, s1, s2, s3, s4);
-      asm volatile("" : "+v"(acc[0]), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4));
-    }
-    if (MASKW) {
-#pragma unroll
-      for (int m = 0; m < 32; ++m) wm[2 * m + 1] &= mW;
-    }
-    acc[1] += qrf_tree<S, 1, P, false>(c, wm, s1, s2, s3, s4);
-  }
-}
-
-// qr pass from the raw rows kept in registers across the network (RAW kernels: no re-read, no LDS).
-template <int P, bool MASKW, bool MASKROWS, int... Is>
-SVOC_DEV void qrf_regs_seq(uint32_t (&xs)[64], uint32_t mW, const QrCtxF& c, float* acc, f32x2& s1, f32x2& s2,
-                           f32x2& s3, f32x2& s4, std::integer_sequence<int, Is...>) {
-  if (MASKW) {
-#pragma unroll
-    for (int i = 0; i < 64; ++i) xs[i] &= mW;
-  }
-  ((acc[Is] += qrf_tree<__builtin_ctz(P), Is, P, MASKROWS>(c, xs, s1, s2, s3, s4)), ...);
-}
-
-// RAW: the lane's 64 raw rows stay in registers across the window network (the qr pass reads them
-// there: no re-read, no LDS staging) at 3 waves per SIMD instead of 4.
-template <int NSEG, int WAVES, int H, bool CONS, int MODE, bool RAW>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW ? 3 : 4))) void consensus_fast_winf_kernel(FastParams p) {
+// One workgroup per instance.  Phase A streams the instance through LDS one WAVES * P-column slab at a
+// time: wait for the slab's DMA + barrier, every lane copies its column's 64 rows (its lane-group
+// segment) into registers (raw values and sort keys), barrier, the next slab's DMA is issued, and the
+// network, window, c1 and qr pass run on the registers while it lands.  2 waves per SIMD (<= 256
+// VGPRs: 64 keys + 64 raw rows + the window), LDS = WAVES x 16 KiB.
+template <int NSEG, int WAVES, int H, bool CONS, int MODE>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2))) void consensus_fast_winf_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // columns per wave (phase A)
   constexpr int NPAD = 64 * NSEG;
   constexpr int W = WAVES * P;          // columns per workgroup step (phase A)
   constexpr int NT = WAVES * 64;
   constexpr int KEEP = 64 / P;
-  // constrained: half of each slab (32 rows x 64 lanes, keys) staged per wave for the qr pass
-  constexpr bool STAGE = CONS && MODE != 2 && !RAW;
-  __shared__ uint32_t stage[STAGE ? WAVES * 32 * 64 : 1];
+  constexpr bool PASS1 = MODE != 2;
+  __shared__ uint32_t slab[PASS1 ? WAVES * 64 * 64 : 1];
   __shared__ float qr_part[WAVES * NPAD];
   __shared__ float qr_lds[NPAD];
   __shared__ uint64_t relmask[4];
@@ -265,7 +187,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW 
 
   const int b = blockIdx.x;
   if (p.active && !p.active[b]) return;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // (wave made explicitly uniform: it feeds the DMA's M0 and SGPR row offsets)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid < 32) urow[tid] = 0;  // f < 32: unused slots still name a valid row
   if (tid == 0) misc_i[2] = 0;
   const int seg = lane / P, cw = lane % P;
@@ -273,6 +196,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW 
   const int rowb = p.ld * 4;
   const float* inst = (const float*)p.values + (int64_t)b * p.inst_stride;
   const __amdgpu_buffer_rsrc_t rs = instance_rsrc(inst, (uint32_t)(N * rowb));
+  const BufDesc rsd = buf_desc(inst, (uint32_t)(N * rowb));   // the same descriptor, for the DMA asm
   const int nslab = (D + W - 1) / W;
   const int Dc = 2 * p.work_pairs;      // workspace columns (launch.hpp: fast_work_words)
   // this instance's workspace: [H][2][Dc] window keys, at byte MOM the [4][Dc] all-row power sums, at
@@ -284,71 +208,47 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW 
   const int lo1 = (NPAD - N + 1) >> 1;
   const int nv = N - seg * 64;
   const int nl = N + lo1 - seg * 64;
-  const int seg_off = seg * 64 * rowb;
   const uint32_t pol = group_polarity<NSEG>(seg);
   const uint32_t kp = 0x80000000u ^ pol;   // constrained key = raw ^ kp
-  uint32_t* const stw = stage + (STAGE ? wave * 32 * 64 : 0);
 
   float acc[KEEP];
 #pragma unroll
   for (int i = 0; i < KEEP; ++i) acc[i] = 0.f;
 
   // ------------------------------------------------------------ phase A: pass 1 (contract.cairo:455-463)
-  const int pass1_slabs = MODE == 2 ? 0 : nslab;
+  const int pass1_slabs = PASS1 ? nslab : 0;
+  const SlabDma<NSEG, WAVES> dma(lane, rowb);
+  // this lane's words in the LDS slab: row seg * 64 + i at word (seg * 64 + i) * W + (column ^ P * seg)
+  const uint32_t* const mine = slab + (PASS1 ? seg * 64 * W + ((wave * P + cw) ^ (P * seg)) : 0);
+  if (pass1_slabs > 0) dma.issue(rsd, slab, wave, rowb, 0);
 #pragma nounroll
   for (int s = 0; s < pass1_slabs; ++s) {
     const int col = s * W + wave * P + cw;
     const bool vc = col < D;
-    const int vo = seg_off + (vc ? col * 4 : 0);
     int nvl = nv, nll = nl;
     asm volatile("" : "+v"(nvl), "+v"(nll));
     float c1v;
     const uint32_t mW = vc ? 0xffffffffu : 0u;
-    uint32_t xs[RAW ? 64 : 1];   // RAW: the lane's raw rows, kept for the qr pass
+    uint32_t xs[64];   // the lane's raw rows, kept for the qr pass
+    __builtin_amdgcn_s_waitcnt(0x0070);      // vmcnt(0): this wave's pieces of slab s have landed
+    __syncthreads();                         // ... and every other wave's
+#pragma unroll
+    for (int i = 0; i < 64; ++i) xs[i] = mine[i * W];
+
+    __syncthreads();                         // every wave holds its rows: the buffer is free
+    if (s + 1 < pass1_slabs) dma.issue(rsd, slab, wave, rowb, (s + 1) * W);
     {
       uint32_t r[64];
-      // (no sched_barrier after these loads -- it costs ~40 spilled VGPRs; the opaque stride keeps the
-      // 64 row offsets out of the slab loop's SGPR live set)
-      int rowb1 = rowb;
-      asm volatile("" : "+s"(rowb1));
       if (N == NPAD) {
-        if (CONS) {
 #pragma unroll
-          for (int i = 0; i < 64; ++i) r[i] = bload(rs, vo, i * rowb1);
-          if constexpr (RAW) {
-#pragma unroll
-            for (int i = 0; i < 64; ++i) xs[i] = r[i];
-          }
-          // the staged rows go to LDS raw, straight from the load registers
-          if constexpr (STAGE && NSEG == 4) {
-#pragma unroll
-            for (int m = 0; m < 16; ++m) {
-              stw[(2 * m) * 64 + lane] = r[4 * m];
-              stw[(2 * m + 1) * 64 + lane] = r[4 * m + 1];
-            }
-          } else if constexpr (STAGE) {
-#pragma unroll
-            for (int m = 0; m < 32; ++m) stw[m * 64 + lane] = r[2 * m];
-          }
-#pragma unroll
-          for (int i = 0; i < 64; ++i) r[i] ^= kp;
-        } else {
-#pragma unroll
-          for (int i = 0; i < 64; ++i) {
-            const uint32_t w = bload(rs, vo, i * rowb1);
-            if constexpr (RAW) xs[i] = w;
-            r[i] = fkey<CONS>(w) ^ pol;
-          }
-        }
+        for (int i = 0; i < 64; ++i) r[i] = CONS ? xs[i] ^ kp : fkey<CONS>(xs[i]) ^ pol;
       } else {
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
-          // real rows -> key; rows >= N -> 0 (the first lo1) / ~0 sentinels, so the middle of the
-          // padded sort is the middle of the real rows
-          const uint32_t w = bload(rs, vo, i * rowb1);
-          if constexpr (RAW) xs[i] = w;
+          // real rows -> key; rows >= N (read as 0) -> 0 (the first lo1) / ~0 sentinels, so the middle of
+          // the padded sort is the middle of the real rows
           const uint32_t hi_m = ~lt_mask(i, nll);
-          r[i] = ((fkey<CONS>(w) & (lt_mask(i, nvl) | hi_m)) | hi_m) ^ pol;
+          r[i] = ((fkey<CONS>(xs[i]) & (lt_mask(i, nvl) | hi_m)) | hi_m) ^ pol;
         }
       }
       uint32_t klo, khi;
@@ -375,37 +275,11 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW 
       c1v = 0.5f * (fkey_val<CONS>(klo) + fkey_val<CONS>(khi));
     }
     if (seg == 0 && vc) p.c1[(int64_t)b * D + col] = c1v;
-    __builtin_amdgcn_sched_barrier(0);
-    // the re-read's offset depends on the network's result (empty asm): otherwise the loads are hoisted
-    // above the network and both 64-register arrays are live at once (spills)
-    int vo2 = vo;
-    asm volatile("" : "+v"(vo2) : "v"(c1v));
-    const QrCtxF qc{nvl, lane, vc ? c1v : 0.f};
+    const float cq = vc ? c1v : 0.f;
     f32x2 s1 = {0.f, 0.f}, s2 = s1, s3 = s1, s4 = s1;
-    if constexpr (RAW) {
-      constexpr auto seq = std::make_integer_sequence<int, KEEP>{};
-      if ((s + 1) * W <= D) {
-        if (N == NPAD) qrf_regs_seq<P, false, false>(xs, mW, qc, acc, s1, s2, s3, s4, seq);
-        else qrf_regs_seq<P, false, true>(xs, mW, qc, acc, s1, s2, s3, s4, seq);
-      } else {
-        if (N == NPAD) qrf_regs_seq<P, true, false>(xs, mW, qc, acc, s1, s2, s3, s4, seq);
-        else qrf_regs_seq<P, true, true>(xs, mW, qc, acc, s1, s2, s3, s4, seq);
-      }
-    } else if (STAGE && N == NPAD) {
-      if constexpr (STAGE && NSEG == 4) {
-        if ((s + 1) * W <= D) qrf_moments_staged<P, false>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
-        else qrf_moments_staged<P, true>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
-      } else if constexpr (STAGE) {
-        if ((s + 1) * W <= D) qrf_moments_staged_even<P, false>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
-        else qrf_moments_staged_even<P, true>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
-      }
-    } else if ((s + 1) * W <= D) {
-      if (N == NPAD) qrf_moments<P, false, false>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
-      else qrf_moments<P, false, true>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
-    } else {
-      if (N == NPAD) qrf_moments<P, true, false>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
-      else qrf_moments<P, true, true>(rs, vo2, rowb, mW, qc, acc, s1, s2, s3, s4);
-    }
+    // one instantiation, masks applied at run time (all-ones on full slabs of N = NPAD rows): with a
+    // second, mask-free one the compiler demotes half of xs to scratch (read by both branches)
+    qr_moments_regs<P, true, true>(xs, nvl, cq, mW, lane, acc, s1, s2, s3, s4);
     float t1 = s1.x + s1.y, t2 = s2.x + s2.y, t3 = s3.x + s3.y, t4 = s4.x + s4.y;
     if constexpr (NSEG == 4) {
       t1 += xor_lane<16>(t1); t2 += xor_lane<16>(t2); t3 += xor_lane<16>(t3); t4 += xor_lane<16>(t4);
@@ -749,32 +623,18 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(RAW 
   }
 }
 
-template <int NSEG, int WAVES, int H, bool CONS, bool RAW>
+template <int NSEG, int WAVES, int H, bool CONS>
 static void launch_winf_w(const FastParams& p, hipStream_t stream) {
-  if (p.mode == 1) hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 1, RAW>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
-  else if (p.mode == 2) hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 2, false>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
-  else hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 0, RAW>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+  if (p.mode == 1) hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 1>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+  else if (p.mode == 2) hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 2>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+  else hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 0>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
 }
 
-// Geometry.  One workgroup per instance.  RAW (raw rows in registers, 3 waves per SIMD): 4-wave
-// workgroups.  Otherwise N > 128 with at least two 8-wave slabs of columns runs 8 waves (half the slabs
-// per wave, 2 workgroups per CU: the bf16 kernel's measured choice, profiles/r2_win_waves_ab.jsonl),
-// everything else 4.  SVOC_WINF_RAW=0/1 overrides the RAW choice (A/B).
-static int winf_raw(int nseg) {
-  static const int forced = [] {
-    const char* e = getenv("SVOC_WINF_RAW");
-    return e ? atoi(e) : -1;
-  }();
-  if (forced >= 0) return forced;
-  return nseg == 1 ? 1 : 0;
-}
+// 4-wave workgroups: 64 KiB of LDS slab each, two workgroups per CU (2 waves per SIMD) -- one's
+// barriers and slab-0 load overlap the other's compute.
 template <int NSEG, int H, bool CONS>
 static void launch_winf_c(const FastParams& p, hipStream_t stream) {
-  if (winf_raw(NSEG)) return launch_winf_w<NSEG, 4, H, CONS, true>(p, stream);
-  if constexpr (NSEG == 4) {
-    if (p.D >= 2 * 8 * 16) return launch_winf_w<NSEG, 8, H, CONS, false>(p, stream);
-  }
-  launch_winf_w<NSEG, 4, H, CONS, false>(p, stream);
+  launch_winf_w<NSEG, 4, H, CONS>(p, stream);
 }
 
 template <int NSEG>

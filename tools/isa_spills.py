@@ -11,10 +11,18 @@ import sys
 import tempfile
 
 
+def file_flags(src):
+    """The kernel source's own extra hipcc flags (``// svoc-hipcc-flags: ...``, csrc/build.py)."""
+    for line in open(src, encoding="utf-8").readlines()[:60]:
+        if "svoc-hipcc-flags:" in line:
+            return line.split("svoc-hipcc-flags:", 1)[1].split()
+    return []
+
+
 def isa(src, incs):
     d = tempfile.mkdtemp()
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-std=c++17", "-O3", *[f"-I{i}" for i in incs],
-           "-c", os.path.abspath(src), "-o", os.path.join(d, "x.o"), "-save-temps"]
+           *file_flags(src), "-c", os.path.abspath(src), "-o", os.path.join(d, "x.o"), "-save-temps"]
     subprocess.run(cmd, cwd=d, check=True, capture_output=True)
     return open(os.path.join(d, [f for f in os.listdir(d) if f.endswith(".s") and "gfx950" in f][0])).read()
 
