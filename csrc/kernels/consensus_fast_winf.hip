@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
 #include <utility>
 
 #include "svoc/bufload.hpp"
@@ -79,6 +80,14 @@ SVOC_DEV bool moments_from_sums_d(double n, double t1, double t2, double t3, dou
   return true;
 }
 
+// The lane's 64 raw rows as two 32-wide vectors (one SSA value each): a plain array is split by SROA into
+// a promoted part and a scratch part when several code paths read it.
+typedef uint32_t u32x32_t __attribute__((ext_vector_type(32)));
+struct RawRows {
+  u32x32_t lo, hi;   // rows 0..31, 32..63
+  SVOC_DEV uint32_t at(int i) const { return i < 32 ? lo[i] : hi[i - 32]; }
+};
+
 // qr partials of the lane's 64 rows (one column), reduced across the wave's P columns by the
 // transposing butterfly (stage MSK exchanges with lane ^ MSK and halves the row set: the lane ends with
 // the KEEP = 64 / P row sums its "base" slot names in the qr reduction below), with the power sums of
@@ -101,12 +110,12 @@ SVOC_DEV void qr_halve(float (&part)[64], int lane) {
   }
 }
 template <int P, bool MASKW, bool MASKROWS>
-SVOC_DEV void qr_moments_regs(const uint32_t (&xs)[64], int nvl, float c, uint32_t mw, int lane, float* acc,
+SVOC_DEV void qr_moments_regs(const RawRows& xs, int nvl, float c, uint32_t mw, int lane, float* acc,
                               f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
   float part[64];
 #pragma unroll
   for (int m = 0; m < 32; ++m) {
-    const uint32_t w0 = MASKW ? xs[m] & mw : xs[m], w1 = MASKW ? xs[m + 32] & mw : xs[m + 32];
+    const uint32_t w0 = MASKW ? xs.lo[m] & mw : xs.lo[m], w1 = MASKW ? xs.hi[m] & mw : xs.hi[m];
     f32x2 y = f32x2{u2f(w0), u2f(w1)} - f32x2{c, c};
     f32x2 q = y * y;
     part[m] = q.x;
@@ -127,29 +136,28 @@ SVOC_DEV void qr_moments_regs(const uint32_t (&xs)[64], int nvl, float c, uint32
   for (int i = 0; i < 64 / P; ++i) acc[i] += part[i];
 }
 
-// One phase-A slab of the workgroup lands in LDS by DMA (buffer_load_dwordx4 ... lds: no VGPR
-// destination).  Layout: [NPAD rows][WC = WAVES * P columns], 4-byte words, rows lane-linear in 16-B
-// chunks as the DMA writes them; the chunk of global column c of row r sits at column c ^ (P * (r >> 6))
-// (a chunk-level XOR applied on the DMA's SOURCE address, the LDS side stays lane-linear), so the reader
-// instruction -- P consecutive columns of the NSEG rows i, 64 + i, ... -- touches 64 distinct banks.
-// One DMA instruction moves 64 chunks = 1 KiB; a slab is 16 instructions per wave.
-template <int NSEG, int WAVES>
+// Phase-A streaming by LDS-DMA (buffer_load_dwordx4 ... lds: no VGPR destination).  Every wave owns a
+// 16-KiB LDS region holding its next slab -- its P columns x the NPAD rows -- so a wave waits for its
+// own pieces only (no workgroup barrier in phase A).  Region layout: LDS row q = NSEG * (r % 64) + r / 64
+// of global row r, P words per row: the NSEG rows a reader instruction touches (r, r + 64, ...; one per
+// lane-group segment) are adjacent, i.e. on 64 distinct banks.  One DMA instruction (piece) writes 1 KiB
+// lane-linearly = RPI consecutive LDS rows; 16 pieces fill the region.
+template <int NSEG>
 struct SlabDma {
-  static constexpr int P = 64 / NSEG, WC = WAVES * P, CPR = WC / 4, RPI = 64 / CPR;
-  int vlane;   // this lane's part of every piece's voffset: (l / CPR) row of the piece, (l % CPR) chunk
-  int lchunk;
-  SVOC_DEV SlabDma(int lane, int rowb) : vlane((lane / CPR) * rowb), lchunk(lane % CPR) {}
-  // issue this wave's 16 pieces of the slab whose first column is col0.  Inline asm: the
-  // __builtin_amdgcn_raw_ptr_buffer_load_lds form crashes ROCm 7.2's instruction selection inside this
-  // kernel (register pressure of the network + qr pass around it); M0 is saved and restored around the
-  // piece (the compiler reserves it), and the caller waits for the pieces with an explicit vmcnt(0).
-  SVOC_DEV void issue(const BufDesc& rs, uint32_t* slab, int wave, int rowb, int col0) const {
+  static constexpr int P = 64 / NSEG, CPR = P / 4, RPI = 64 / CPR;
+  int vlane;   // this lane's part of every piece's voffset
+  SVOC_DEV SlabDma(int lane, int rowb) {
+    const int j = lane / CPR;   // LDS row of the piece this lane fills
+    vlane = ((j % NSEG) * 64 + j / NSEG) * rowb + (lane % CPR) * 16;
+  }
+  // issue this wave's 16 pieces of the slab whose first column (of this wave) is col0.  Inline asm: the
+  // __builtin_amdgcn_raw_ptr_buffer_load_lds form crashes ROCm 7.2's instruction selection in this
+  // kernel; M0 is saved and restored around the piece (the compiler reserves it).
+  SVOC_DEV void issue(const BufDesc& rs, uint32_t* region, int rowb, int col0) const {
+    const int vo = vlane + col0 * 4;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int k = wave * 16 + j;                      // piece: rows k * RPI .. k * RPI + RPI - 1
-      const int swz = (P / 4) * ((k * RPI) >> 6);       // chunk XOR of those rows (uniform per piece)
-      const int vo = vlane + 16 * (lchunk ^ swz) + col0 * 4;
-      const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(slab + k * 256);
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(region + k * 256);
       int keep;
       asm volatile(
           "s_mov_b32 %0, m0\n\t"
@@ -158,7 +166,7 @@ struct SlabDma {
           "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
           "s_mov_b32 m0, %0"
           : "=&s"(keep)
-          : "v"(vo), "s"(rs.w), "s"(lds), "s"(k * RPI * rowb)
+          : "v"(vo), "s"(rs.w), "s"(lds), "s"(k * (RPI / NSEG) * rowb)
           : "memory");
     }
   }
@@ -177,7 +185,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
   constexpr int NT = WAVES * 64;
   constexpr int KEEP = 64 / P;
   constexpr bool PASS1 = MODE != 2;
-  __shared__ uint32_t slab[PASS1 ? WAVES * 64 * 64 : 1];
+  __shared__ uint32_t slab[PASS1 ? WAVES * 64 * 64 : 1];   // one 16-KiB DMA region per wave
   __shared__ float qr_part[WAVES * NPAD];
   __shared__ float qr_lds[NPAD];
   __shared__ uint64_t relmask[4];
@@ -217,38 +225,43 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
 
   // ------------------------------------------------------------ phase A: pass 1 (contract.cairo:455-463)
   const int pass1_slabs = PASS1 ? nslab : 0;
-  const SlabDma<NSEG, WAVES> dma(lane, rowb);
-  // this lane's words in the LDS slab: row seg * 64 + i at word (seg * 64 + i) * W + (column ^ P * seg)
-  const uint32_t* const mine = slab + (PASS1 ? seg * 64 * W + ((wave * P + cw) ^ (P * seg)) : 0);
-  if (pass1_slabs > 0) dma.issue(rsd, slab, wave, rowb, 0);
-#pragma nounroll
-  for (int s = 0; s < pass1_slabs; ++s) {
+  const SlabDma<NSEG> dma(lane, rowb);
+  uint32_t* const region = slab + (PASS1 ? wave * 64 * 64 : 0);
+  // this lane's words: global row seg * 64 + i at LDS row NSEG * i + seg, i.e. word 64 i + seg P + cw
+  const uint32_t* const mine = region + (PASS1 ? seg * P + cw : 0);
+  if (pass1_slabs > 0) dma.issue(rsd, region, rowb, wave * P);
+  // One slab of phase A.  FULL: every column of the slab is < D and N = NPAD, so no masks at all; the
+  // masked form serves the tail slab and padded N.  (One body per loop: reading the raw rows in two
+  // branches of one loop makes the compiler demote them to scratch.)
+  auto slab_body = [&](auto full_c, int s) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(full_c)::value;
     const int col = s * W + wave * P + cw;
-    const bool vc = col < D;
+    const bool vc = FULL || col < D;
     int nvl = nv, nll = nl;
     asm volatile("" : "+v"(nvl), "+v"(nll));
     float c1v;
     const uint32_t mW = vc ? 0xffffffffu : 0u;
-    uint32_t xs[64];   // the lane's raw rows, kept for the qr pass
-    __builtin_amdgcn_s_waitcnt(0x0070);      // vmcnt(0): this wave's pieces of slab s have landed
-    __syncthreads();                         // ... and every other wave's
+    RawRows xs;        // the lane's raw rows, kept for the qr pass
+    __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): this wave's pieces of slab s have landed
 #pragma unroll
-    for (int i = 0; i < 64; ++i) xs[i] = mine[i * W];
-
-    __syncthreads();                         // every wave holds its rows: the buffer is free
-    if (s + 1 < pass1_slabs) dma.issue(rsd, slab, wave, rowb, (s + 1) * W);
+    for (int i = 0; i < 32; ++i) {
+      xs.lo[i] = mine[i * 64];
+      xs.hi[i] = mine[(i + 32) * 64];
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0): the region is read, the next slab may land
+    if (s + 1 < pass1_slabs) dma.issue(rsd, region, rowb, (s + 1) * W + wave * P);
     {
       uint32_t r[64];
-      if (N == NPAD) {
+      if (FULL || N == NPAD) {
 #pragma unroll
-        for (int i = 0; i < 64; ++i) r[i] = CONS ? xs[i] ^ kp : fkey<CONS>(xs[i]) ^ pol;
+        for (int i = 0; i < 64; ++i) r[i] = CONS ? xs.at(i) ^ kp : fkey<CONS>(xs.at(i)) ^ pol;
       } else {
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
           // real rows -> key; rows >= N (read as 0) -> 0 (the first lo1) / ~0 sentinels, so the middle of
           // the padded sort is the middle of the real rows
           const uint32_t hi_m = ~lt_mask(i, nll);
-          r[i] = ((fkey<CONS>(xs[i]) & (lt_mask(i, nvl) | hi_m)) | hi_m) ^ pol;
+          r[i] = ((fkey<CONS>(xs.at(i)) & (lt_mask(i, nvl) | hi_m)) | hi_m) ^ pol;
         }
       }
       uint32_t klo, khi;
@@ -277,9 +290,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     if (seg == 0 && vc) p.c1[(int64_t)b * D + col] = c1v;
     const float cq = vc ? c1v : 0.f;
     f32x2 s1 = {0.f, 0.f}, s2 = s1, s3 = s1, s4 = s1;
-    // one instantiation, masks applied at run time (all-ones on full slabs of N = NPAD rows): with a
-    // second, mask-free one the compiler demotes half of xs to scratch (read by both branches)
-    qr_moments_regs<P, true, true>(xs, nvl, cq, mW, lane, acc, s1, s2, s3, s4);
+    qr_moments_regs<P, !FULL, !FULL>(xs, nvl, cq, mW, lane, acc, s1, s2, s3, s4);
     float t1 = s1.x + s1.y, t2 = s2.x + s2.y, t3 = s3.x + s3.y, t4 = s4.x + s4.y;
     if constexpr (NSEG == 4) {
       t1 += xor_lane<16>(t1); t2 += xor_lane<16>(t2); t3 += xor_lane<16>(t3); t4 += xor_lane<16>(t4);
@@ -293,7 +304,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       bstore(ws, f2u(t3), col * 4, MOM + 2 * Dc * 4);
       bstore(ws, f2u(t4), col * 4, MOM + 3 * Dc * 4);
     }
-  }
+  };
+  const int nfull = N == NPAD ? min(D / W, pass1_slabs) : 0;
+#pragma nounroll
+  for (int s = 0; s < nfull; ++s) slab_body(std::true_type{}, s);
+#pragma nounroll
+  for (int s = nfull; s < pass1_slabs; ++s) slab_body(std::false_type{}, s);
 
   // ------------------------------------------------------------ qr reduction
   {

@@ -8,7 +8,7 @@ CONFIGS="${AB_CONFIGS:---config c2|--config-file configs/ab_c128.yaml}"
 REPS="${AB_REPS:-3}"
 if [ "${AB_TESTS:-1}" = "1" ]; then
   cp ab/_C_new.so svoc/_C.so
-  timeout -k 10 300 python -u -m pytest tests/test_win_gpu.py tests/test_win_gpu_extra.py -x -q --timeout 120 --timeout-method thread > gpurun_out/win_tests.log 2>&1 || exit 1; tail -1 gpurun_out/win_tests.log
+  timeout -k 10 300 python -u -m pytest ${AB_TEST_FILES:-tests/test_win_gpu.py tests/test_win_gpu_extra.py} -x -q --timeout 120 --timeout-method thread > gpurun_out/win_tests.log 2>&1 || { tail -5 gpurun_out/win_tests.log; exit 1; }; tail -1 gpurun_out/win_tests.log
 fi
 IFS='|' read -ra CFGS <<< "$CONFIGS"
 for rep in $(seq 1 $REPS); do
