@@ -85,7 +85,7 @@ def measure(args, c, storage, dev, rank, world, dshard):
     B = args.batch or c["batch"]
     D_local = c["D"]
     if dshard:
-        from svoc.parallel.dshard import run_round_sharded, shard_bounds
+        from svoc.parallel.dshard import flush_sharded, run_round_sharded, shard_bounds
         lo, hi = shard_bounds(c["D"], rank, world)
         D_local = hi - lo
     cfg = ConsensusConfig(n_oracles=c["N"], dimension=D_local, n_failing_oracles=c["f"], constrained=True)
@@ -132,6 +132,10 @@ def measure(args, c, storage, dev, rank, world, dshard):
                                              + c["N"] * 32)
         extra["instances_per_288GB"] = int(288e9 // extra["state_bytes_per_instance"])
 
+    transactional = bool(c.get("transactional")) and stream is not None
+    if transactional and mode != "exact":
+        raise SystemExit("transactional streaming is the exact engine's per-update replay (mode: exact)")
+    extra["transactional"] = transactional
     pipeline = args.pipeline if args.pipeline >= 0 else c.get("pipeline", 1)
     if dshard or mode != "fast" or dev.type != "cuda":
         pipeline = 1
@@ -139,7 +143,9 @@ def measure(args, c, storage, dev, rank, world, dshard):
 
     def run_round():
         if dshard:
-            run_round_sharded(eng, c["D"], world=world)   # includes the qr all-reduce
+            # one packed all-reduce per round (qr partials + the previous round's status codes: the
+            # previous round commits from it); the last round commits at flush()
+            run_round_sharded(eng, c["D"], world=world, defer=world > 1)
         else:
             eng.run_round(only_touched=True)
 
@@ -148,7 +154,9 @@ def measure(args, c, storage, dev, rank, world, dshard):
             pipe.fetch(*toks[i % 2])
         elif stream is not None:
             inst, orc, vals = stream.batch(i)
-            if pipeline > 1:   # the stream has distinct (instance, oracle), grouped by instance
+            if transactional:   # exact: every update its own transaction (store + round, revert on failure)
+                eng.step(inst, orc, vals, updates_per_instance=U_per_inst)
+            elif pipeline > 1:   # the stream has distinct (instance, oracle), grouped by instance
                 eng.step_pipelined(inst, orc, vals, U_per_inst, chunks=pipeline)
             else:
                 eng.apply_updates(inst, orc, vals, unique=True)
@@ -159,9 +167,18 @@ def measure(args, c, storage, dev, rank, world, dshard):
         if gov is not None:
             gov.submit_tensors(*gov_batches[i % len(gov_batches)])
 
+    def flush():
+        if dshard:
+            flush_sharded(eng, world=world)
+
+    def step_metrics():   # DP: one all-reduce of the round counters per step (D-shard: every rank
+        if not dshard:    # commits the same rounds, so the counters are reduced once, after the loop)
+            dp.reduce()
+
     for i in range(args.warmup):
         step(i)
-        dp.reduce()
+        step_metrics()
+    flush()
     sync()
 
     graph = None
@@ -199,14 +216,15 @@ def measure(args, c, storage, dev, rank, world, dshard):
         reps, rem = divmod(args.steps, graph_period)
         for _ in range(reps):
             graph.replay()
-            dp.reduce()            # one RCCL all-reduce of the step metrics per replay
+            step_metrics()         # one RCCL all-reduce of the step metrics per replay
         for i in range(rem):       # exactly K steps: the tail of a period runs eagerly
             step(i)
-            dp.reduce()
+            step_metrics()
     else:
         for i in range(args.steps):
             step(i)
-            dp.reduce()
+            step_metrics()
+    flush()                        # (D-shard) the last round's commit: inside the timed region
     sync()
     if world > 1:
         dist.barrier()
@@ -221,6 +239,7 @@ def measure(args, c, storage, dev, rank, world, dshard):
     else:
         per_rank = mine[None].cpu()
     return dict(eng=eng, B=B, mode=mode, elapsed=float(per_rank[:, 0].max()),   # the slowest rank's time
+                rounds_per_instance=U_per_inst if transactional else 1,
                 U=U_per_inst, graph=graph is not None, extra=extra, step=step, storage=eng.storage,
                 rank_ms=[1e3 * float(t) / args.steps for t in per_rank[:, 0]],
                 rank_ok=[float(o) for o in per_rank[:, 1]], ok=dp.global_ok_fraction())
@@ -297,7 +316,8 @@ def main():
 
     r = measure(args, c, storage, dev, rank, world, dshard)
     B, mode, el, U, eng = r["B"], r["mode"], r["elapsed"], r["U"], r["eng"]
-    rounds = B * scale * args.steps
+    # transactional streaming: one round per update transaction (U per instance per step)
+    rounds = B * scale * args.steps * r["rounds_per_instance"]
     out = {
         "metric": METRIC, "value": rounds / el, "unit": "consensus rounds/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * el / args.steps, "higher_is_better": True,
@@ -306,7 +326,7 @@ def main():
         "config": {"model": c["model"], "global_batch": B * scale, "seq_len": c["D"],
                    "parallelism": f"dshard{world}" if dshard else f"dp{world}", "engine_mode": mode,
                    "storage": eng.storage, "n_oracles": c["N"], "dimension": c["D"], "n_failing": c["f"],
-                   "updates_per_instance_per_step": U, "oracle_updates_per_s": (U * rounds / el) if U else 0.0,
+                   "updates_per_instance_per_step": U, "oracle_updates_per_s": (U * B * scale * args.steps / el) if U else 0.0,
                    "hip_graph": r["graph"], "ok_fraction": r["ok"], "backend_world": backend_world,
                    "rank_ms_per_step": r["rank_ms"], "rank_ms_spread": [min(r["rank_ms"]), max(r["rank_ms"])],
                    "rank_ok_fraction": r["rank_ok"], **r["extra"]},

@@ -81,9 +81,10 @@ void apply_updates_cpu(at::Tensor values, at::Tensor enabled, at::Tensor n_activ
   const int64_t row_bytes = (int64_t)p.D * p.elem_bytes;
   for (int64_t u = 0; u < p.U; ++u) {  // sequential = last writer wins
     const int64_t b = p.inst[u], o = p.oracle[u];
+    // the contract's check order (contract.cairo:588-596): the prediction's interval check before the
+    // caller's oracle lookup (as row_status in updates.hip)
     int st = ST_OK;
-    if (b < 0 || b >= p.B || o < 0 || o >= p.N) st = ST_NOT_ORACLE;
-    if (st == ST_OK && p.constrained)
+    if (p.constrained)
       for (int d = 0; d < p.D; ++d)
         if (!in_range_cpu(p, u, d)) { st = ST_INTERVAL_INPUT; break; }
     if (st == ST_OK && !p.constrained && p.dtype <= 1)
@@ -96,6 +97,7 @@ void apply_updates_cpu(at::Tensor values, at::Tensor enabled, at::Tensor n_activ
         }();
         if (!std::isfinite(f)) { st = ST_NON_FINITE; break; }
       }
+    if (st == ST_OK && (b < 0 || b >= p.B || o < 0 || o >= p.N)) st = ST_NOT_ORACLE;
     p.upd_status[u] = st;
     if (st != ST_OK) continue;
     std::memcpy((unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes,

@@ -49,6 +49,13 @@ __device__ __forceinline__ bool group_all(bool ok) {
   return (bad & gm) == 0;
 }
 
+// The transaction's status in the contract's check order (contract.cairo:588-596): the prediction's
+// interval check (finite values, unconstrained floats) before the caller's oracle lookup -- an update
+// failing both reports INTERVAL_INPUT, as the reference does.
+__device__ __forceinline__ int row_status(bool ok, bool fin, bool bad) {
+  return !ok ? ST_INTERVAL_INPUT : !fin ? ST_NON_FINITE : bad ? ST_NOT_ORACLE : ST_OK;
+}
+
 // validate every update, then claim its (instance, oracle) slot with an atomicMax on the update's
 // sequence number: the last valid writer wins (coalescing is exact: survey §2.8-13)
 template <int L>
@@ -56,15 +63,15 @@ __global__ __launch_bounds__(256) void upd_validate_kernel(UpdateParams p) {
   const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
   const int sub = threadIdx.x & (L - 1);
   const bool in = u < p.U;
-  int st = ST_OK;
+  bool bad = false;   // unknown instance / oracle: reported after the row checks (see row_status)
   int64_t b = 0, o = 0;
   if (in) {
     b = p.inst[u];
     o = p.oracle[u];
-    if (b < 0 || b >= p.B || o < 0 || o >= p.N) st = ST_NOT_ORACLE;
+    bad = b < 0 || b >= p.B || o < 0 || o >= p.N;
   }
   bool ok = true;
-  if (in && st == ST_OK && p.constrained) {
+  if (in && p.constrained) {
     const uint16_t* row = (const uint16_t*)p.upd + u * p.D;
     if (p.dtype == 0 && (p.D & 7) == 0 && (((uintptr_t)row) & 15) == 0) {
       for (int c = sub; c < p.D / 8; c += L) {
@@ -78,13 +85,12 @@ __global__ __launch_bounds__(256) void upd_validate_kernel(UpdateParams p) {
     }
   }
   bool fin = true;
-  if (in && st == ST_OK && !p.constrained && p.dtype <= 1)
+  if (in && !p.constrained && p.dtype <= 1)
     for (int d = sub; d < p.D; d += L) fin = fin && finite_at(p, u, d);
   ok = group_all<L>(ok);  // all lanes reach the ballots (no early return above)
   fin = group_all<L>(fin);
   if (in && sub == 0) {
-    if (st == ST_OK && !ok) st = ST_INTERVAL_INPUT;
-    if (st == ST_OK && !fin) st = ST_NON_FINITE;
+    const int st = row_status(ok, fin, bad);
     p.upd_status[u] = st;
     if (st == ST_OK) atomicMax(&p.winner[b * p.N + o], (int)u);
   }
@@ -126,12 +132,12 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
   const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
   const int sub = threadIdx.x & (L - 1);
   const bool in = u < p.U;
-  int st = ST_OK;
+  bool bad = false;   // unknown instance / oracle: reported after the row checks (row_status)
   int64_t b = 0, o = 0;
   if (in) {
     b = p.inst[u];
     o = p.oracle[u];
-    if (b < 0 || b >= p.B || o < 0 || o >= p.N) st = ST_NOT_ORACLE;
+    bad = b < 0 || b >= p.B || o < 0 || o >= p.N;
   }
   const int64_t row_bytes = (int64_t)p.D * p.elem_bytes;
   const unsigned char* src = (const unsigned char*)p.upd + u * row_bytes;
@@ -145,7 +151,7 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
   if (p.dtype <= 1 && vec && nch <= (int64_t)RB * L) {  // uniform over the launch
     uint4 v[RB];
     bool ok = true, fin = true;
-    const bool live = in && st == ST_OK;
+    const bool live = in;
 #pragma unroll
     for (int k = 0; k < RB; ++k) {
       const int64_t i = sub + (int64_t)k * L;
@@ -170,8 +176,7 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
     ok = group_all<L>(ok);
     fin = group_all<L>(fin);
     if (!in) return;
-    if (st == ST_OK && !ok) st = ST_INTERVAL_INPUT;
-    if (st == ST_OK && !fin) st = ST_NON_FINITE;
+    const int st = row_status(ok, fin, bad);
     if (sub == 0) p.upd_status[u] = st;
     if (st != ST_OK) return;
 #pragma unroll
@@ -196,8 +201,7 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
       else fin = fin && ((w[k] & 0x7f80u) != 0x7f80u) && ((w[k] & 0x7f800000u) != 0x7f800000u);
     }
     if (!in) return;
-    if (st == ST_OK && !ok) st = ST_INTERVAL_INPUT;
-    if (st == ST_OK && !fin) st = ST_NON_FINITE;
+    const int st = row_status(ok, fin, bad);
     p.upd_status[u] = st;
     if (st != ST_OK) return;
 #pragma unroll
@@ -205,7 +209,7 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
       if (k < nw) ((uint32_t*)dst)[k] = w[k];
   } else {
     bool ok = true, fin = true;
-    if (in && st == ST_OK) {
+    if (in) {
       if (p.dtype == 0 && vec) {
         for (int64_t i = sub; i < nch; i += L) {
           const uint4 v = ((const uint4*)src)[i];
@@ -226,8 +230,7 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
     ok = group_all<L>(ok);   // every lane reaches the ballots
     fin = group_all<L>(fin);
     if (!in) return;
-    if (st == ST_OK && !ok) st = ST_INTERVAL_INPUT;
-    if (st == ST_OK && !fin) st = ST_NON_FINITE;
+    const int st = row_status(ok, fin, bad);
     if (sub == 0) p.upd_status[u] = st;
     if (st != ST_OK) return;
     // the row was just read by these lanes: the copy re-reads it from L2

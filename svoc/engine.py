@@ -229,51 +229,97 @@ class ConsensusEngine:
         m[0] *= (2.0 ** -32) if self.mode == "fast" else 1e-6
         return m
 
-    def step(self, inst, oracle, vals) -> torch.Tensor:
+    def step(self, inst, oracle, vals, updates_per_instance: Optional[int] = None) -> torch.Tensor:
         """update_prediction for a batch of (instance, oracle, prediction) + the consensus rounds.
 
         fast: one coalesced round per touched instance.  exact: per-instance sequential
-        transactions (a reverted round restores that update's previous row)."""
+        transactions (a reverted round restores that update's previous row).
+        ``updates_per_instance=K`` (exact): the batch is laid out as K updates of every instance in
+        instance order (update b * K + k is instance b's k-th; SyntheticUpdateStream's layout), so
+        the transaction waves are strided views: no host synchronisation at all (graph-capturable).
+        That layout is trusted, as in :meth:`step_pipelined` (an instance twice in one wave breaks the
+        sequential order); any other batch goes through the general device-side grouping."""
         if self.mode == "fast":
             st = self.apply_updates(inst, oracle, vals)
             self.run_round()
             return st
-        return self._exact_transactions(inst, oracle, vals)
+        return self._exact_transactions(inst, oracle, vals, updates_per_instance)
 
-    def _exact_transactions(self, inst, oracle, vals) -> torch.Tensor:
-        inst_h = np.asarray(torch.as_tensor(inst).cpu(), dtype=np.int64).reshape(-1)
-        orc_h = np.asarray(torch.as_tensor(oracle).cpu(), dtype=np.int64).reshape(-1)
+    def _transaction_waves(self, inst: torch.Tensor, oracle: torch.Tensor):
+        """Device-side grouping of a batch into transaction waves: wave k = the k-th valid update of every
+        instance (batch order kept per instance).  Returns (order, bounds): the update indices sorted by
+        (wave, batch index) and the host list of wave boundaries -- the one device->host copy (K + 1
+        integers), before any wave is issued."""
+        U = inst.numel()
+        idx = torch.arange(U, device=self.device)
+        ok = (inst >= 0) & (inst < self.B) & (oracle >= 0) & (oracle < self.N)
+        key = torch.where(ok, inst, torch.full_like(inst, self.B))
+        by_inst = torch.sort(key * U + idx).indices                 # grouped by instance, batch order
+        sk = key[by_inst]
+        first = torch.searchsorted(sk, sk)                          # first position of the own instance
+        occ = torch.empty_like(idx)
+        occ[by_inst] = torch.arange(U, device=self.device) - first  # rank within the instance
+        occ = torch.where(ok, occ, torch.full_like(occ, U))          # invalid updates: after every wave
+        order = torch.sort(occ * U + idx).indices
+        counts = torch.bincount(occ, minlength=U + 1)[:U].cpu()      # updates per wave (host, once)
+        n_waves = int(torch.count_nonzero(counts))
+        bounds = [0] + torch.cumsum(counts[:n_waves], 0).tolist()
+        return order, bounds
+
+    def _exact_transactions(self, inst, oracle, vals, updates_per_instance: Optional[int] = None) -> torch.Tensor:
+        """Sequential per-update transactions (contract.cairo:588-603: update_prediction stores the row,
+        then the full consensus round; a round that fails reverts the whole transaction), replayed as
+        waves: wave k applies the k-th update of every instance at once -- instances are independent,
+        so this is the per-instance sequential order.  Everything stays on the device: per wave one
+        gather of the old rows, the batched store, the round over the touched instances and a masked
+        restore for the transactions whose round failed."""
+        inst = torch.as_tensor(inst, dtype=torch.int64, device=self.device).reshape(-1)
+        oracle = torch.as_tensor(oracle, dtype=torch.int64, device=self.device).reshape(-1)
         vals = self._as_storage(torch.as_tensor(vals))
-        U = inst_h.size
+        U = inst.numel()
         out = torch.full((U,), int(Status.NOT_ORACLE), dtype=torch.int32, device=self.device)
-        ok_idx = (inst_h >= 0) & (inst_h < self.B) & (orc_h >= 0) & (orc_h < self.N)
-        # wave k = the k-th update of every instance (order preserved per instance)
-        occ = np.full(U, -1, dtype=np.int64)
-        seen: Dict[int, int] = {}
-        for u in np.nonzero(ok_idx)[0].tolist():
-            b = int(inst_h[u])
-            occ[u] = seen.get(b, 0)
-            seen[b] = occ[u] + 1
-        for k in range(int(occ.max()) + 1 if U else 0):
-            sel_h = np.nonzero(occ == k)[0]
-            sel = torch.as_tensor(sel_h, device=self.device)
-            bi = torch.as_tensor(inst_h[sel_h], device=self.device)
-            oi = torch.as_tensor(orc_h[sel_h], device=self.device)
-            old_rows = self.values[bi, oi].clone()
-            old_en = self.enabled[bi, oi].clone()
-            old_na = self.n_active[bi].clone()
+        if U == 0:
+            return out
+        K = int(updates_per_instance or 0)
+        if K:
+            if U % K:
+                raise ValueError("_exact_transactions: updates_per_instance must divide the batch")
+            waves = [torch.arange(k, U, K, device=self.device) for k in range(K)]
+        else:
+            order, bounds = self._transaction_waves(inst, oracle)
+            waves = [order[bounds[k]:bounds[k + 1]] for k in range(len(bounds) - 1)]
+            if bounds[-1] < U:   # unknown instance / oracle: status only (interval check first), no store
+                bad = order[bounds[-1]:]
+                out[bad] = self.apply_updates(inst[bad], oracle[bad], vals[bad])
+        for sel in waves:
+            bi, oi = inst[sel], oracle[sel]
+            if K:
+                # out-of-range entries (status NOT_ORACLE, never applied) point their no-op gathers and
+                # write-backs at their own layout slot (instance sel // K): with one entry per instance
+                # per wave they cannot collide with another entry's restore.  (The general path drops
+                # them in _transaction_waves.)
+                okw = (bi >= 0) & (bi < self.B) & (oi >= 0) & (oi < self.N)
+                bi_c = torch.where(okw, bi, sel // K)
+                oi_c = torch.where(okw, oi, torch.zeros_like(oi))
+            else:
+                okw, bi_c, oi_c = None, bi, oi
+            old_rows = self.values[bi_c, oi_c].clone()
+            old_en = self.enabled[bi_c, oi_c].clone()
+            old_na = self.n_active[bi_c].clone()
             self.touched.zero_()
             st_u = self.apply_updates(bi, oi, vals[sel])
             self.run_round(only_touched=True)        # outputs are only written when a round succeeds
-            st_b = self.status[bi]
-            full = self.n_active[bi] == self.N
+            st_b = self.status[bi_c]
+            full = self.n_active[bi_c] == self.N
             tx = torch.where(st_u != 0, st_u,
                              torch.where(full, st_b, torch.full_like(st_b, int(Status.NOT_ACTIVE))))
             revert = (st_u == 0) & full & (st_b != int(Status.OK))
+            if okw is not None:
+                revert = revert & okw
             # roll back reverted transactions (contract semantics: the whole tx disappears)
-            self.values[bi, oi] = torch.where(revert[:, None], old_rows, self.values[bi, oi])
-            self.enabled[bi, oi] = torch.where(revert, old_en, self.enabled[bi, oi])
-            self.n_active[bi] = torch.where(revert, old_na, self.n_active[bi])
+            self.values[bi_c, oi_c] = torch.where(revert[:, None], old_rows, self.values[bi_c, oi_c])
+            self.enabled[bi_c, oi_c] = torch.where(revert, old_en, self.enabled[bi_c, oi_c])
+            self.n_active[bi_c] = torch.where(revert, old_na, self.n_active[bi_c])
             out[sel] = tx
         return out
 

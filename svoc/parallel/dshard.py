@@ -55,51 +55,106 @@ class _Shadow:
         self.reliable = torch.zeros_like(e.reliable)
 
 
-def run_round_sharded(engine, d_global: int, group=None, world: int = 1) -> None:
-    """Consensus round for an engine holding a column shard of every instance."""
+def _pack(qr: torch.Tensor, prev: torch.Tensor, cur: torch.Tensor, rank: int, world: int) -> torch.Tensor:
+    """[B, N + 2 * world] all-reduce buffer: the qr partials, then this rank's previous-round (deferred)
+    pass-2 status and this round's pass-1 status in its own slots (zeros elsewhere).  A SUM of it is the
+    global qr AND every rank's status codes exactly (x + 0 = x; codes < 64 are exact in fp32), so one
+    collective replaces the separate status MAX reductions."""
+    B, N = qr.shape
+    buf = torch.zeros((B, N + 2 * world), dtype=qr.dtype, device=qr.device)
+    buf[:, :N] = qr
+    buf[:, N + rank] = prev.to(qr.dtype)
+    buf[:, N + world + rank] = cur.to(qr.dtype)
+    return buf
+
+
+def _commit(e, sh, active: torch.Tensor, status: torch.Tensor, qr=None, c1=None) -> None:
+    """Shadow outputs -> state for the instances whose (globally reduced) status is OK, then the epilogue.
+    (A deferred round passes its own qr / c1: the next round's pass 1 rewrites those shadows.)"""
+    qr = sh.qr if qr is None else qr
+    c1 = sh.c1 if c1 is None else c1
+    ok1 = ((active != 0) & (status == int(Status.OK)))[:, None]
+    e.consensus.copy_(torch.where(ok1, sh.consensus, e.consensus))
+    e.skew.copy_(torch.where(ok1, sh.skew, e.skew))
+    e.kurt.copy_(torch.where(ok1, sh.kurt, e.kurt))
+    e.rel.copy_(torch.where(ok1, sh.rel, e.rel))
+    e.qr.copy_(torch.where(ok1, qr, e.qr))
+    e.reliable.copy_(torch.where(ok1, sh.reliable, e.reliable))
+    e.c1.copy_(torch.where(ok1, c1, e.c1))
+    e._ops.round_epilogue(active, status, e.rel, e.consensus_active, e.touched, e.metrics_fx)
+
+
+def run_round_sharded(engine, d_global: int, group=None, world: int = 1, defer: bool = False) -> None:
+    """Consensus round for an engine holding a column shard of every instance.
+
+    Collectives per round (world > 1): one SUM of the packed buffer (qr partials + status slots, _pack),
+    then one status MAX after pass 2 -- or, with ``defer=True``, none: the round's pass-2 verdicts ride
+    in the NEXT round's packed buffer, which commits this round before its own pass 2 (one collective
+    per round).  A deferred round is pending until that next round or :func:`flush_sharded`; its
+    instances' ``touched`` flags are cleared at once (the epilogue clears them anyway), so the next
+    round's selection is unchanged."""
     e = engine
     sh = getattr(e, "_dshard_shadow", None)
     if sh is None:
         sh = e._dshard_shadow = _Shadow(e)
+    rank = dist.get_rank(group) if world > 1 else 0
+    pend = getattr(e, "_dshard_pending", None)
     e._ops.round_prologue(e.n_active, e.touched, e.N, True, e._active)
     lg = e.cfg.legacy
     if e.mode == "fast":
         mx = float(e.cfg.unconstrained_max_spread)
         w = e.work()                                     # window kernel: pass 1 -> pass 2 state
         head = (e.values, e._active, e.D, e.cfg.n_failing_oracles, e.cfg.constrained, mx, sh.c1)
-        # pass 1: local c1 + qr partials (into the shadow qr: the committed qr stays intact)
-        e._ops.fast_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status,
-                          e.wave_hint, 1, d_global, lg, w)
-        if world > 1:
-            dist.all_reduce(sh.qr, op=dist.ReduceOp.SUM, group=group)
-        # pass 2 from the global qr, into the shadow outputs; status = this shard's verdict
-        e._ops.fast_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status,
-                          e.wave_hint, 2, d_global, lg, w)
+
+        def half(mode):
+            e._ops.fast_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status,
+                              e.wave_hint, mode, d_global, lg, w)
     else:
         if world > MAX_EXACT_SHARDS:
             # each shard's int64 qr partial is bounded below 2^58 (status.hpp kExactQrPartialMax); the SUM
             # all-reduce of more than 32 of them could wrap int64 and silently change the rank mask
             raise ValueError(f"exact D-sharding supports at most {MAX_EXACT_SHARDS} shards (got {world})")
         head = (e.values, e._active, e.cfg.n_failing_oracles, e.cfg.constrained, e.cfg.max_spread_wsad, sh.c1)
-        # first half: c1 + int64 qr partials; a shard that fails here (overflow) fails the round
-        e._ops.exact_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status, lg,
-                           1, d_global)
-        if world > 1:
-            dist.all_reduce(sh.qr, op=dist.ReduceOp.SUM, group=group)
-            dist.all_reduce(e.status, op=dist.ReduceOp.MAX, group=group)
-        # second half on the instances every shard passed (the kernel skips non-OK statuses)
-        e._ops.exact_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status, lg,
-                           2, d_global)
+
+        def half(mode):
+            e._ops.exact_round(*head, sh.consensus, sh.skew, sh.kurt, sh.rel, sh.qr, sh.reliable, e.status, lg,
+                               mode, d_global)
+    # pass 1: local c1 + qr partials into the shadow qr (the committed qr stays intact); status = this
+    # shard's pass-1 verdict (exact: a partial past 2^58 fails the round)
+    half(1)
+    if world > 1:
+        prev = pend[1] if pend is not None else torch.zeros_like(e.status)
+        buf = _pack(sh.qr, prev, e.status, rank, world)
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+        N = sh.qr.shape[1]
+        sh.qr.copy_(buf[:, :N])
+        if pend is not None:     # the previous (deferred) round: every rank's pass-2 verdict, then commit
+            _commit(e, sh, pend[0], buf[:, N:N + world].amax(1).to(e.status.dtype), pend[2], pend[3])
+            e._dshard_pending = pend = None
+        e.status.copy_(buf[:, N + world:].amax(1).to(e.status.dtype))
+    # pass 2 from the global qr on the instances every shard passed, into the shadow outputs
+    half(2)
+    if defer and world > 1:
+        # (active, local pass-2 status, global qr, c1): pass 1 of the next round rewrites the qr / c1 shadows
+        e._dshard_pending = (e._active.clone(), e.status.clone(), sh.qr.clone(), sh.c1.clone())
+        e.touched.zero_()
+        e.rounds += 1
+        return
     if world > 1:
         dist.all_reduce(e.status, op=dist.ReduceOp.MAX, group=group)
-    ok = (e._active != 0) & (e.status == int(Status.OK))
-    ok1 = ok[:, None]
-    e.consensus.copy_(torch.where(ok1, sh.consensus, e.consensus))
-    e.skew.copy_(torch.where(ok1, sh.skew, e.skew))
-    e.kurt.copy_(torch.where(ok1, sh.kurt, e.kurt))
-    e.rel.copy_(torch.where(ok1, sh.rel, e.rel))
-    e.qr.copy_(torch.where(ok1, sh.qr, e.qr))
-    e.reliable.copy_(torch.where(ok1, sh.reliable, e.reliable))
-    e.c1.copy_(torch.where(ok1, sh.c1, e.c1))
-    e._ops.round_epilogue(e._active, e.status, e.rel, e.consensus_active, e.touched, e.metrics_fx)
+    _commit(e, sh, e._active, e.status)
     e.rounds += 1
+
+
+def flush_sharded(engine, group=None, world: int = 1) -> None:
+    """Commit a deferred sharded round (one status MAX all-reduce); no-op when none is pending."""
+    e = engine
+    pend = getattr(e, "_dshard_pending", None)
+    if pend is None:
+        return
+    st = pend[1].clone()
+    if world > 1:
+        dist.all_reduce(st, op=dist.ReduceOp.MAX, group=group)
+    _commit(e, e._dshard_shadow, pend[0], st, pend[2], pend[3])
+    e.status.copy_(st)
+    e._dshard_pending = None

@@ -164,6 +164,72 @@ def test_dsharding_revert_is_atomic_across_shards():
         assert torch.equal(snaps[1]["qr"][inst], snaps[0]["qr"][inst])
 
 
+def _ds_defer_worker(rank, world, port, outdir, xs, cfgd, mode):
+    """The same rounds eagerly committed and deferred (one collective per round, flush at the end),
+    counting the all-reduces of the deferred run."""
+    _init(rank, world, port)
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    from svoc.parallel import dshard
+    cfg = ConsensusConfig(**cfgd)
+    lo, hi = dshard.shard_bounds(cfg.dimension, rank, world)
+    lcfg = ConsensusConfig(**{**cfgd, "dimension": hi - lo})
+    engines = [ConsensusEngine(lcfg, xs[0].shape[0], device="cpu", mode=mode) for _ in range(2)]
+    calls = []
+    real = dist.all_reduce
+
+    def counting(t, *a, **k):
+        calls.append(tuple(t.shape))
+        return real(t, *a, **k)
+
+    out = []
+    for j, e in enumerate(engines):
+        dist.all_reduce = counting if j == 1 else real
+        try:
+            for x in xs:
+                e.values[:, :, : hi - lo] = x[:, :, lo:hi]
+                e.enabled.fill_(1); e.n_active.fill_(cfg.n_oracles); e.touched.fill_(1)
+                dshard.run_round_sharded(e, cfg.dimension, world=world, defer=(j == 1))
+                if j == 1:
+                    calls.append("round")
+            dshard.flush_sharded(e, world=world)
+        finally:
+            dist.all_reduce = real
+        out.append({k: getattr(e, k).clone() for k in ("consensus", "rel", "reliable", "qr", "skew", "kurt", "c1",
+                                                       "status", "consensus_active", "touched", "metrics_fx")})
+    torch.save(dict(out=out, calls=calls), os.path.join(outdir, f"dd{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["fast", "exact"])
+def test_dsharding_deferred_commit_one_collective_per_round(mode):
+    """defer=True: each round issues ONE all-reduce (qr partials + every rank's status codes packed in one
+    SUM buffer; the previous round commits from it), plus one status MAX at flush -- and the state after
+    the flush is identical to the eagerly committed rounds, reverts included."""
+    from helpers import beta_oracles
+    from svoc.config import WSAD
+    B, N, D, f, world = 4, 16, 24, 2, 2
+    xs = []
+    for seed in (31, 32, 33):
+        x, _ = beta_oracles(B, N, D, f, seed=seed)
+        xs.append(x[:, :, :D].contiguous())
+    xs[1][1, :, 2] = 0.5        # round 2: zero variance in shard 0's column 2 only -> instance 1 reverts
+    xs[2][3, :, 20] = 0.25      # round 3: shard 1 only -> instance 3 reverts
+    if mode == "exact":
+        xs = [(x.double() * WSAD).to(torch.int64) for x in xs]
+    cfgd = dict(n_oracles=N, dimension=D, n_failing_oracles=f, constrained=True)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ds_defer_worker, args=(world, _free_port(), d, xs, cfgd, mode), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"dd{i}.pt"), weights_only=True) for i in range(world)]
+    for s in r:
+        eager, deferred = s["out"]
+        for k in eager:
+            assert torch.equal(eager[k], deferred[k]), k
+        assert eager["status"].tolist()[1] == 0 and eager["status"].tolist()[3] != 0
+        # one collective per round, the packed [B, N + 2 * world] buffer; the flush's status MAX last
+        assert s["calls"] == [(B, N + 2 * world), "round"] * 3 + [(B,)], s["calls"]
+
+
 def _ds_exact_worker(rank, world, port, outdir, xs, cfgd):
     _init(rank, world, port)
     from svoc.config import ConsensusConfig

@@ -136,3 +136,20 @@ def test_bench_fp32_storage_cpu(tmp_path):
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["dtype"] == "fp32" and out["config"]["storage"] == "fp32"
     assert out["value"] > 0 and out["config"]["ok_fraction"] == 1.0
+
+
+def test_bench_exact_transactional_stream_cpu(tmp_path):
+    """configs/c*_exact_stream.yaml's form: exact mode, every update its own transaction -- rounds/s
+    counts one round per update (U per instance per step)."""
+    p = tmp_path / "cpu_tx.yaml"
+    p.write_text("name: cpu_tx\nmodel: test N=7 D=6 exact transactional stream\nN: 7\nD: 6\nf: 2\nbatch: 64\n"
+                 "update_frac: 0.2857142857142857\ndevice: cpu\nmode: exact\ntransactional: true\n")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config-file", str(p), "--steps", "3",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    cfg = out["config"]
+    assert cfg["transactional"] and cfg["engine_mode"] == "exact" and cfg["updates_per_instance_per_step"] == 2
+    assert abs(out["value"] - cfg["oracle_updates_per_s"]) < 1e-6 * out["value"]   # one round per update
+    assert abs(out["value"] * out["ms_per_step"] / 1e3 - 64 * 2) < 1e-6 * 128
+    assert 0 < cfg["ok_fraction"] <= 1.0
