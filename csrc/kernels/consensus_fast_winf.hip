@@ -88,13 +88,13 @@ struct RawRows {
   SVOC_DEV uint32_t at(int i) const { return i < 32 ? lo[i] : hi[i - 32]; }
 };
 
-// qr partials of the lane's 64 rows (one column), reduced across the wave's P columns by the
-// transposing butterfly (stage MSK exchanges with lane ^ MSK and halves the row set: the lane ends with
-// the KEEP = 64 / P row sums its "base" slot names in the qr reduction below), with the power sums of
-// d = x - c1 accumulated on the way, two rows (i, i + 32) per packed instruction (v_pk_add / v_pk_fma).
-// The row leaves are formed in one flat pass over the raw rows kept in registers (no re-read).
+// qr partials: every lane accumulates (x - c1)^2 of its 64 rows (rows m, m + 32 as one packed pair)
+// over all the columns it visits in phase A, with the column's power sums of d = x - c1 on the way
+// (v_pk_add / v_pk_fma); the rows' sums across the wave's P column lanes are formed once, after phase
+// A, by the transposing butterfly qr_halve (stage MSK exchanges with lane ^ MSK and halves the row set:
+// the lane ends with the KEEP = 64 / P row sums its "base" slot names).
 // MASKW: slab with columns past D (mw = 0 there: words +0, centre +0); MASKROWS: rows >= N (read as 0)
-// masked out of the power sums.
+// masked out of the power sums (their qr partials are never read).
 template <int MSK, int H>
 SVOC_DEV void qr_halve(float (&part)[64], int lane) {
   if constexpr (MSK >= 1) {
@@ -109,17 +109,15 @@ SVOC_DEV void qr_halve(float (&part)[64], int lane) {
     qr_halve<MSK / 2, H / 2>(part, lane);
   }
 }
-template <int P, bool MASKW, bool MASKROWS>
-SVOC_DEV void qr_moments_regs(const RawRows& xs, int nvl, float c, uint32_t mw, int lane, float* acc,
+template <bool MASKW, bool MASKROWS>
+SVOC_DEV void qr_moments_regs(const RawRows& xs, int nvl, float c, uint32_t mw, f32x2 (&acc)[32],
                               f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
-  float part[64];
 #pragma unroll
   for (int m = 0; m < 32; ++m) {
     const uint32_t w0 = MASKW ? xs.lo[m] & mw : xs.lo[m], w1 = MASKW ? xs.hi[m] & mw : xs.hi[m];
     f32x2 y = f32x2{u2f(w0), u2f(w1)} - f32x2{c, c};
     f32x2 q = y * y;
-    part[m] = q.x;
-    part[m + 32] = q.y;
+    acc[m] += q;
     if (MASKROWS) {
       const uint32_t m0 = lt_mask(m, nvl), m1 = lt_mask(m + 32, nvl);
       const float y0 = y.x, y1 = y.y, q0 = q.x, q1 = q.y;
@@ -131,9 +129,20 @@ SVOC_DEV void qr_moments_regs(const RawRows& xs, int nvl, float c, uint32_t mw, 
     s3 = __builtin_elementwise_fma(q, y, s3);
     s4 = __builtin_elementwise_fma(q, q, s4);
   }
+}
+
+// the lane's KEEP row sums of a packed partial set (qr_halve across the wave's P column lanes)
+template <int P>
+SVOC_DEV void qr_keep(const f32x2 (&a)[32], int lane, float (&keep)[64 / P], bool add) {
+  float part[64];
+#pragma unroll
+  for (int m = 0; m < 32; ++m) {
+    part[m] = a[m].x;
+    part[m + 32] = a[m].y;
+  }
   qr_halve<P / 2, 32>(part, lane);
 #pragma unroll
-  for (int i = 0; i < 64 / P; ++i) acc[i] += part[i];
+  for (int i = 0; i < 64 / P; ++i) keep[i] = add ? keep[i] + part[i] : part[i];
 }
 
 // Phase-A streaming by LDS-DMA (buffer_load_dwordx4 ... lds: no VGPR destination).  Every wave owns a
@@ -219,9 +228,16 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
   const uint32_t pol = group_polarity<NSEG>(seg);
   const uint32_t kp = 0x80000000u ^ pol;   // constrained key = raw ^ kp
 
-  float acc[KEEP];
+  // qr partials of rows (m, m + 32) summed over the lane's phase-A columns, reduced across the column
+  // lanes once after phase A (ACC64); the unconstrained kernels (more live registers: general key
+  // mapping, two-median network) reduce them every slab into KEEP row sums instead
+  constexpr bool ACC64 = CONS;
+  f32x2 acc[ACC64 ? 32 : 1];
 #pragma unroll
-  for (int i = 0; i < KEEP; ++i) acc[i] = 0.f;
+  for (int i = 0; i < (ACC64 ? 32 : 1); ++i) acc[i] = f32x2{0.f, 0.f};
+  float keep[KEEP];
+#pragma unroll
+  for (int i = 0; i < KEEP; ++i) keep[i] = 0.f;
 
   // ------------------------------------------------------------ phase A: pass 1 (contract.cairo:455-463)
   const int pass1_slabs = PASS1 ? nslab : 0;
@@ -290,7 +306,15 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     if (seg == 0 && vc) p.c1[(int64_t)b * D + col] = c1v;
     const float cq = vc ? c1v : 0.f;
     f32x2 s1 = {0.f, 0.f}, s2 = s1, s3 = s1, s4 = s1;
-    qr_moments_regs<P, !FULL, !FULL>(xs, nvl, cq, mW, lane, acc, s1, s2, s3, s4);
+    if constexpr (ACC64) {
+      qr_moments_regs<!FULL, !FULL>(xs, nvl, cq, mW, acc, s1, s2, s3, s4);
+    } else {
+      f32x2 slab_acc[32];
+#pragma unroll
+      for (int i = 0; i < 32; ++i) slab_acc[i] = f32x2{0.f, 0.f};
+      qr_moments_regs<!FULL, !FULL>(xs, nvl, cq, mW, slab_acc, s1, s2, s3, s4);
+      qr_keep<P>(slab_acc, lane, keep, true);
+    }
     float t1 = s1.x + s1.y, t2 = s2.x + s2.y, t3 = s3.x + s3.y, t4 = s4.x + s4.y;
     if constexpr (NSEG == 4) {
       t1 += xor_lane<16>(t1); t2 += xor_lane<16>(t2); t3 += xor_lane<16>(t3); t4 += xor_lane<16>(t4);
@@ -313,11 +337,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
 
   // ------------------------------------------------------------ qr reduction
   {
+    if constexpr (ACC64) qr_keep<P>(acc, lane, keep, false);
     int base = 0;
 #pragma unroll
     for (int h = 32, msk = P / 2; msk >= 1; h >>= 1, msk >>= 1) base += (lane & msk) ? h : 0;
 #pragma unroll
-    for (int i = 0; i < KEEP; ++i) qr_part[wave * NPAD + seg * 64 + base + i] = acc[i];
+    for (int i = 0; i < KEEP; ++i) qr_part[wave * NPAD + seg * 64 + base + i] = keep[i];
   }
   __syncthreads();
   for (int t = tid; t < NPAD; t += NT) {
