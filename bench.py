@@ -38,7 +38,7 @@ CONFIGS = {
     "c1": dict(model="plumbing: 4 oracles x 2 dims, one exact (wsad) round per step on the CPU engine", N=4, D=2,
                f=0, batch=1, update_frac=0.0, device="cpu", mode="exact", dtype="int64-wsad"),
     "c3": dict(model="svoc-consensus N=256 D=4096 streaming (f=32, constrained)", N=256, D=4096, f=32,
-               batch=1024, update_frac=0.25, pipeline=4, storage="fp32", alt_storage="bf16"),
+               batch=1024, update_frac=0.25, pipeline=2, storage="fp32", alt_storage="bf16"),
     "c2": dict(model="svoc-consensus N=64 D=1024 batched (f=8, constrained)", N=64, D=1024, f=8,
                batch=10000, update_frac=0.0, storage="bf16", alt_storage="fp32"),
     "c4": dict(model="sentiment oracles: BERT-base (12x768, bf16) on 30-comment windows -> 7 oracles x 6 dims",

@@ -118,13 +118,13 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
   const int64_t B = values.size(0), N = values.size(1), ld = values.size(2);
   if (f32) {
     // reference-resolution storage: the column-parallel fp32 kernel (consensus_fast_f32.hip)
-    TORCH_CHECK(N >= 2 && N <= 1024, "GPU fp32 fast path supports 2 <= N <= 1024 oracles");
+    TORCH_CHECK(N >= 2 && N <= 4096, "GPU fp32 fast path supports 2 <= N <= 4096 oracles");
     TORCH_CHECK(B < (1ll << 31) && D < (1 << 30), "size limits");
     TORCH_CHECK(N * ld * 4 < (1ll << 31) && fast_work_words(D) * 4 < (1ll << 31),
                 "instance too large for 32-bit buffer offsets (N * ld * 4 B and the workspace must stay < 2 GiB)");
   }
   if (!f32) {
-    TORCH_CHECK(N >= 2 && N <= 1024, "GPU fast path supports 2 <= N <= 1024 oracles");
+    TORCH_CHECK(N >= 2 && N <= 4096, "GPU fast path supports 2 <= N <= 4096 oracles");
     TORCH_CHECK(ld % 8 == 0, "row stride (ld) must be a multiple of 8 bf16 (16 B)");
     TORCH_CHECK(((uintptr_t)values.data_ptr() & 15) == 0 && values.stride(0) % 8 == 0, "values must be 16-B aligned");
     TORCH_CHECK(B < (1ll << 31) && D < (1 << 30), "size limits");

@@ -377,14 +377,14 @@ SVOC_DEV void median_group(K (&r)[64], K& lo, K& hi) {
   }
 }
 
-// The two middle order statistics for wide groups (NSEG = 8 / 16: N up to 512 / 1024 oracles): a
+// The two middle order statistics for wide groups (NSEG = 8 .. 64: N up to 512 .. 4096 oracles): a
 // full cross-lane bitonic sort of the 64*NSEG keys (sort_group: in-lane odd-even merge sort, then
 // per merge level a cross-lane flip, cross-lane half-cleaners and an in-lane merge), then the keys
 // at sorted positions NPAD/2 - 1 and NPAD/2 read from their owner lanes (middle_pair).  Keys in true
 // polarity (group_polarity<NSEG> = 0 for these widths).
 template <int NSEG, int P, class K>
 SVOC_DEV void median_group_wide(K (&r)[64], int seg, int lane, K& lo, K& hi) {
-  static_assert(NSEG == 8 || NSEG == 16, "wide groups");
+  static_assert(NSEG == 8 || NSEG == 16 || NSEG == 32 || NSEG == 64, "wide groups");
   sort_group<NSEG, P>(r, seg);
   middle_pair<NSEG, P>(r, seg, lane, lo, hi);
 }

@@ -511,7 +511,7 @@ using namespace svoc;
 // -1: shape / workspace outside what the kernel supports (the binding checks these first).
 extern "C" int svoc_fast_round_f32(const FastParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
-  if (p->N < 2 || p->N > 1024 || p->D > p->ld || p->mode < 0 || p->mode > 2) return -1;
+  if (p->N < 2 || p->N > 4096 || p->D > p->ld || p->mode < 0 || p->mode > 2) return -1;
   if ((int64_t)p->N * p->ld * 4 >= (1ll << 31)) return -1;   // 32-bit buffer offsets
   if (p->mode != 1 && (!p->work || p->work_pairs < fast_work_pairs(p->D) || p->work_stride < fast_work_words(p->D)))
     return -1;   // pass 2 stages its outputs in the workspace
@@ -525,5 +525,8 @@ extern "C" int svoc_fast_round_f32(const FastParams* p, hipStream_t stream) {
   if (p->N <= 128) return launch_f32<2>(*p, stream);
   if (p->N <= 256) return launch_f32<4>(*p, stream);
   if (p->N <= 512) return launch_f32<8>(*p, stream);
-  return launch_f32<16>(*p, stream);
+  if (p->N <= 1024) return launch_f32<16>(*p, stream);
+  // N > 1024: 32 / 64 lanes per column (two / one column per wave), the same cross-lane bitonic sort
+  if (p->N <= 2048) return launch_f32<32>(*p, stream);
+  return launch_f32<64>(*p, stream);
 }

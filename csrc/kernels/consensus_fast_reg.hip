@@ -21,7 +21,7 @@ namespace svoc {
 // MODE 0: fused round; 1: pass 1 only (c1 + qr -> global); 2: rank + pass 2 from the global qr
 // (D-sharding: the caller all-reduces the qr partials in between).
 template <int NSEG, int WAVES, bool CONS, int MODE>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4))) void consensus_fast_reg_kernel(FastParams p) {
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(NSEG >= 64 ? 1 : NSEG >= 32 ? 2 : 4))) void consensus_fast_reg_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // column pairs per wave
   constexpr int NPAD = 64 * NSEG;       // padded oracle rows
   constexpr int W = WAVES * P * 2;      // columns per workgroup step
@@ -388,7 +388,7 @@ using namespace svoc;
 
 extern "C" int svoc_fast_round_bf16_reg(const FastParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
-  if (p->N < 2 || p->N > 1024 || p->ld % 8 != 0 || p->D > p->ld) return -1;
+  if (p->N < 2 || p->N > 4096 || p->ld % 8 != 0 || p->D > p->ld) return -1;
   if (p->mode != 1 && (!p->work || p->work_pairs < fast_work_pairs(p->D) || p->work_stride < fast_work_words(p->D)))
     return -1;   // pass 2 stages its outputs in the workspace
   // 4 waves per workgroup (16 waves per CU at <= 128 VGPRs)
@@ -396,5 +396,8 @@ extern "C" int svoc_fast_round_bf16_reg(const FastParams* p, hipStream_t stream)
   if (p->N <= 128) return launch_reg<2, 4>(*p, stream);
   if (p->N <= 256) return launch_reg<4, 4>(*p, stream);
   if (p->N <= 512) return launch_reg<8, 4>(*p, stream);
-  return launch_reg<16, 4>(*p, stream);
+  if (p->N <= 1024) return launch_reg<16, 4>(*p, stream);
+  // N > 1024: 32 / 64 lanes per column pair (two / one pair per wave), the same cross-lane bitonic sort
+  if (p->N <= 2048) return launch_reg<32, 4>(*p, stream);
+  return launch_reg<64, 4>(*p, stream);
 }

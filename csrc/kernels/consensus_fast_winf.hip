@@ -34,6 +34,7 @@
 
 #include "svoc/bufload.hpp"
 #include "svoc/launch.hpp"
+#include "svoc/slabdma.hpp"
 #include "svoc/sortnet.hpp"
 #include "svoc/status.hpp"
 
@@ -79,14 +80,6 @@ SVOC_DEV bool moments_from_sums_d(double n, double t1, double t2, double t3, dou
   ku = (float)((n * mu4 / (mu2 * mu2) * k4a - k4b) / k4c);
   return true;
 }
-
-// The lane's 64 raw rows as two 32-wide vectors (one SSA value each): a plain array is split by SROA into
-// a promoted part and a scratch part when several code paths read it.
-typedef uint32_t u32x32_t __attribute__((ext_vector_type(32)));
-struct RawRows {
-  u32x32_t lo, hi;   // rows 0..31, 32..63
-  SVOC_DEV uint32_t at(int i) const { return i < 32 ? lo[i] : hi[i - 32]; }
-};
 
 // qr partials: every lane accumulates (x - c1)^2 of its 64 rows (rows m, m + 32 as one packed pair)
 // over all the columns it visits in phase A, with the column's power sums of d = x - c1 on the way
@@ -144,42 +137,6 @@ SVOC_DEV void qr_keep(const f32x2 (&a)[32], int lane, float (&keep)[64 / P], boo
 #pragma unroll
   for (int i = 0; i < 64 / P; ++i) keep[i] = add ? keep[i] + part[i] : part[i];
 }
-
-// Phase-A streaming by LDS-DMA (buffer_load_dwordx4 ... lds: no VGPR destination).  Every wave owns a
-// 16-KiB LDS region holding its next slab -- its P columns x the NPAD rows -- so a wave waits for its
-// own pieces only (no workgroup barrier in phase A).  Region layout: LDS row q = NSEG * (r % 64) + r / 64
-// of global row r, P words per row: the NSEG rows a reader instruction touches (r, r + 64, ...; one per
-// lane-group segment) are adjacent, i.e. on 64 distinct banks.  One DMA instruction (piece) writes 1 KiB
-// lane-linearly = RPI consecutive LDS rows; 16 pieces fill the region.
-template <int NSEG>
-struct SlabDma {
-  static constexpr int P = 64 / NSEG, CPR = P / 4, RPI = 64 / CPR;
-  int vlane;   // this lane's part of every piece's voffset
-  SVOC_DEV SlabDma(int lane, int rowb) {
-    const int j = lane / CPR;   // LDS row of the piece this lane fills
-    vlane = ((j % NSEG) * 64 + j / NSEG) * rowb + (lane % CPR) * 16;
-  }
-  // issue this wave's 16 pieces of the slab whose first column (of this wave) is col0.  Inline asm: the
-  // __builtin_amdgcn_raw_ptr_buffer_load_lds form crashes ROCm 7.2's instruction selection in this
-  // kernel; M0 is saved and restored around the piece (the compiler reserves it).
-  SVOC_DEV void issue(const BufDesc& rs, uint32_t* region, int rowb, int col0) const {
-    const int vo = vlane + col0 * 4;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(region + k * 256);
-      int keep;
-      asm volatile(
-          "s_mov_b32 %0, m0\n\t"
-          "s_mov_b32 m0, %3\n\t"
-          "s_nop 0\n\t"
-          "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
-          "s_mov_b32 m0, %0"
-          : "=&s"(keep)
-          : "v"(vo), "s"(rs.w), "s"(lds), "s"(k * (RPI / NSEG) * rowb)
-          : "memory");
-    }
-  }
-};
 
 // One workgroup per instance.  Phase A streams the instance through LDS one WAVES * P-column slab at a
 // time: wait for the slab's DMA + barrier, every lane copies its column's 64 rows (its lane-group
@@ -329,11 +286,13 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       bstore(ws, f2u(t4), col * 4, MOM + 3 * Dc * 4);
     }
   };
-  const int nfull = N == NPAD ? min(D / W, pass1_slabs) : 0;
+  if constexpr (PASS1) {
+    const int nfull = N == NPAD ? min(D / W, pass1_slabs) : 0;
 #pragma nounroll
-  for (int s = 0; s < nfull; ++s) slab_body(std::true_type{}, s);
+    for (int s = 0; s < nfull; ++s) slab_body(std::true_type{}, s);
 #pragma nounroll
-  for (int s = nfull; s < pass1_slabs; ++s) slab_body(std::false_type{}, s);
+    for (int s = nfull; s < pass1_slabs; ++s) slab_body(std::false_type{}, s);
+  }
 
   // ------------------------------------------------------------ qr reduction
   {

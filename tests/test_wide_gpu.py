@@ -1,6 +1,7 @@
-"""N > 256 oracles on the GPU (up to 1024): the register-streaming fast kernel with 8 / 16 lanes per
-column pair (full cross-lane bitonic sort, sortnet.hpp median_group_wide) and the i128 exact kernel
-with 8 / 16 rows per lane.  The reference has no oracle cap beyond gas (contract.cairo:310-329)."""
+"""N > 256 oracles on the GPU: the register-streaming fast kernels (bf16 and fp32 storage) with 8 .. 64
+lanes per column (pair) -- N up to 4096, full cross-lane bitonic sort, sortnet.hpp median_group_wide
+-- and the i128 exact kernel with 8 / 16 rows per lane (N <= 1024).  The reference has no oracle cap
+beyond gas (contract.cairo:310-329)."""
 import pytest
 import torch
 
@@ -11,11 +12,14 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.mark.parametrize("N,D,f,constrained", [(300, 64, 30, True), (512, 256, 64, True), (512, 100, 40, False),
-                                               (1000, 96, 100, True), (1024, 130, 50, True), (777, 33, 200, True)])
-def test_fast_wide_n_vs_torch(N, D, f, constrained):
-    B = 6
-    x, _ = beta_oracles(B, N, D, f, seed=N + D)
+@pytest.mark.parametrize("N,D,f,constrained,storage", [
+    (300, 64, 30, True, "bf16"), (512, 256, 64, True, "bf16"), (512, 100, 40, False, "bf16"),
+    (1000, 96, 100, True, "bf16"), (1024, 130, 50, True, "bf16"), (777, 33, 200, True, "bf16"),
+    (2048, 70, 200, True, "bf16"), (1500, 33, 100, False, "bf16"), (4096, 20, 300, True, "bf16"),
+    (2048, 70, 200, True, "fp32"), (1500, 33, 100, False, "fp32"), (3000, 20, 300, True, "fp32")])
+def test_fast_wide_n_vs_torch(N, D, f, constrained, storage):
+    B = 6 if N <= 1024 else 3
+    x, _ = beta_oracles(B, N, D, f, seed=N + D, dtype=torch.bfloat16 if storage == "bf16" else torch.float32)
     o = run_fast(x.to(DEV), D, f, constrained, 1.0)
     torch.cuda.synchronize()
     r = torch_ref.fast_round(x.to(DEV)[:, :, :D], f, constrained, 1.0)

@@ -6,13 +6,15 @@ set -u
 mkdir -p gpurun_out
 CONFIGS="${AB_CONFIGS:---config c2|--config-file configs/ab_c128.yaml}"
 REPS="${AB_REPS:-3}"
+VARS="${AB_VARIANTS:-old new}"
+TESTV="${AB_TEST_VARIANT:-${VARS##* }}"   # the build the tests run on (default: the last variant)
 if [ "${AB_TESTS:-1}" = "1" ]; then
-  cp ab/_C_new.so svoc/_C.so
+  cp ab/_C_$TESTV.so svoc/_C.so
   timeout -k 10 300 python -u -m pytest ${AB_TEST_FILES:-tests/test_win_gpu.py tests/test_win_gpu_extra.py} -x -q --timeout 120 --timeout-method thread > gpurun_out/win_tests.log 2>&1 || { tail -5 gpurun_out/win_tests.log; exit 1; }; tail -1 gpurun_out/win_tests.log
 fi
 IFS='|' read -ra CFGS <<< "$CONFIGS"
 for rep in $(seq 1 $REPS); do
-  for v in ${AB_VARIANTS:-old new}; do
+  for v in $VARS; do
     cp ab/_C_$v.so svoc/_C.so
     for cfg in "${CFGS[@]}"; do
       tag=$(echo $cfg | tr -cd 'a-z0-9')
@@ -21,4 +23,4 @@ for rep in $(seq 1 $REPS); do
     done
   done
 done
-cp ab/_C_new.so svoc/_C.so
+cp ab/_C_$TESTV.so svoc/_C.so

@@ -17,23 +17,28 @@ d = json.loads(line); d["key"] = sys.argv[1]; print(json.dumps(d))
 PY
   tail -1 $OUT | cut -c1-160
 }
-run c3 300 --config c3 --steps 20 --warmup 3 &&
+run c3 400 --config c3 --steps 20 --warmup 3 &&
+run c3_bf16 300 --config c3 --storage bf16 --steps 20 --warmup 3 &&
 run c2 300 --config c2 --steps 20 --warmup 3 &&
+run c2_fp32 300 --config c2 --storage fp32 --steps 20 --warmup 3 &&
 run c5 300 --config c5 --steps 50 --warmup 3 &&
 run c4 300 --config c4 --steps 10 --warmup 2 &&
-run c2_fp32 300 --config c2 --storage fp32 --steps 20 --warmup 3 &&
-run c3_fp32 300 --config c3 --storage fp32 --steps 20 --warmup 3 &&
 run c2_exact 300 --config c2 --mode exact --steps 10 --warmup 2 &&
 run c2_exact_int64 300 --config c2 --mode exact --storage int64 --steps 10 --warmup 2 &&
 run c5_exact 300 --config-file configs/c5_exact_rounds.yaml --steps 20 --warmup 2 &&
 run c3_exact 300 --config-file configs/c3_exact_rounds.yaml --steps 10 --warmup 2 &&
+run c5_exact_stream 300 --config-file configs/c5_exact_stream.yaml --steps 20 --warmup 2 &&
+run c3_exact_stream 400 --config-file configs/c3_exact_stream.yaml --steps 3 --warmup 1 &&
 run wide512 300 --config-file configs/wide512.yaml --steps 10 --warmup 2 &&
 run wide512_fp32 300 --config-file configs/wide512.yaml --storage fp32 --steps 10 --warmup 2 &&
+run wide2048 300 --config-file configs/wide2048.yaml --steps 5 --warmup 1 &&
+run wide2048_fp32 300 --config-file configs/wide2048.yaml --storage fp32 --steps 5 --warmup 1 &&
 run c1 300 --config c1 --steps 50 --warmup 3 || exit 1
-for cfg in c3 c2 c4; do
+for spec in "c3:--storage fp32" "c2:--storage bf16" "c4:"; do   # one storage per trace (no alt run)
+  cfg=${spec%%:*}; extra=${spec#*:}
   echo "=== rocprof $cfg ($(date +%T))"
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d $R/gpurun_out/prof_$cfg -o run -- python3 $R/bench.py --config $cfg --steps 6 --warmup 1 --graph 0 \
+      -d $R/gpurun_out/prof_$cfg -o run -- python3 $R/bench.py --config $cfg --steps 6 --warmup 1 --graph 0 $extra \
       > $R/gpurun_out/prof_$cfg.log 2>&1) || exit 1
 done
 echo "=== done"
