@@ -140,6 +140,7 @@ def measure(args, c, storage, dev, rank, world, dshard):
     if dshard or mode != "fast" or dev.type != "cuda":
         pipeline = 1
     extra["pipeline_chunks"] = pipeline
+    extra["pipeline_overlap"] = bool(args.overlap) and pipeline > 1
 
     def run_round():
         if dshard:
@@ -157,7 +158,9 @@ def measure(args, c, storage, dev, rank, world, dshard):
             if transactional:   # exact: every update its own transaction (store + round, revert on failure)
                 eng.step(inst, orc, vals, updates_per_instance=U_per_inst)
             elif pipeline > 1:   # the stream has distinct (instance, oracle), grouped by instance
-                eng.step_pipelined(inst, orc, vals, U_per_inst, chunks=pipeline)
+                # consecutive steps overlap too (range 0's update beside the previous step's last
+                # round); anything reading the state joins the streams first (engine.pipeline_join)
+                eng.step_pipelined(inst, orc, vals, U_per_inst, chunks=pipeline, overlap=bool(args.overlap))
             else:
                 eng.apply_updates(inst, orc, vals, unique=True)
                 run_round()
@@ -187,13 +190,14 @@ def measure(args, c, storage, dev, rank, world, dshard):
         # the stream cycles with period `pool`: capture one period and replay it
         period = 1
         for k in (stream.pool if stream is not None else 1, len(gov_batches) if gov is not None else 1,
-                  2 if pipe is not None else 1):
-            period = period * k // math.gcd(period, k)
+                  2 if pipe is not None else 1, 4 if pipeline > 1 else 1):   # (pipelined: 3 of 4 step
+            period = period * k // math.gcd(period, k)                        # boundaries overlap)
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for i in range(period):
                 step(i)
+            eng.pipeline_join()
         torch.cuda.current_stream(dev).wait_stream(s)
         sync()
         try:
@@ -201,6 +205,7 @@ def measure(args, c, storage, dev, rank, world, dshard):
             with torch.cuda.graph(graph):
                 for i in range(period):
                     step(i)
+                eng.pipeline_join()   # every forked stream rejoins the capture stream
             graph_period = period
         except Exception as e:  # graph capture is an optimisation; eager stays correct
             if rank == 0:
@@ -225,6 +230,7 @@ def measure(args, c, storage, dev, rank, world, dshard):
             step(i)
             step_metrics()
     flush()                        # (D-shard) the last round's commit: inside the timed region
+    eng.pipeline_join()
     sync()
     if world > 1:
         dist.barrier()
@@ -259,6 +265,9 @@ def main():
                     help="streaming configs: overlap the update scatter of one instance range with the round "
                          "of the previous one over K ranges (ConsensusEngine.step_pipelined); 1 = serial, "
                          "-1 = the config's default")
+    ap.add_argument("--overlap", type=int, default=1,
+                    help="pipelined steps: overlap consecutive steps too (ConsensusEngine.step_pipelined "
+                         "overlap=True); 0 = join the streams at the end of every step")
     ap.add_argument("--mode", default=None, choices=["fast", "exact"],
                     help="override the config's engine mode (exact = bit-exact wsad int64 path)")
     ap.add_argument("--storage", default=None, choices=["bf16", "fp32", "int64", "int32"],

@@ -122,13 +122,15 @@ class ConsensusEngine:
         return vals.to(self.device, self.vdtype).contiguous()
 
     def apply_updates(self, inst: torch.Tensor, oracle: torch.Tensor, vals: torch.Tensor,
-                      unique: bool = False) -> torch.Tensor:
+                      unique: bool = False, _joined: bool = False) -> torch.Tensor:
         """Store a batch of predictions (no consensus). Returns the per-update status [U] (device).
 
         ``unique=True``: the caller guarantees distinct (instance, oracle) pairs in the batch, so the GPU
         validates and stores in one pass (no last-writer resolution)."""
         inst = torch.as_tensor(inst, dtype=torch.int64, device=self.device).contiguous()
         oracle = torch.as_tensor(oracle, dtype=torch.int64, device=self.device).contiguous()
+        if not _joined:
+            self.pipeline_join()
         vals = self._as_storage(torch.as_tensor(vals))
         if vals.dim() != 2 or vals.shape[1] != self.D:
             raise ValueError(f"predictions must be [U, {self.D}]")
@@ -144,6 +146,7 @@ class ConsensusEngine:
         Three launches: the prologue selects the instances (n_active == N, touched), the fused
         round kernel, and the epilogue commits consensus_active, clears touched and folds the
         round's health counters into :attr:`metrics_fx` (integers: deterministic sums)."""
+        self.pipeline_join()
         self._ops.round_prologue(self.n_active, self.touched, self.N, bool(only_touched), self._active)
         mx = self.cfg.unconstrained_max_spread
         if self.mode == "fast":
@@ -175,17 +178,25 @@ class ConsensusEngine:
                                  self.touched[sl], self.metrics_fx)
 
     def step_pipelined(self, inst: torch.Tensor, oracle: torch.Tensor, vals: torch.Tensor,
-                       updates_per_instance: int, chunks: int = 2) -> None:
+                       updates_per_instance: int, chunks: int = 2, overlap: bool = False) -> None:
         """apply_updates(unique=True) + run_round, pipelined over ``chunks`` instance ranges on HIP streams.
 
-        The update scatter is HBM-bound and the round kernel is latency-bound, so they overlap: the
-        updates of range k+1 (one update stream, in order) run while the round of range k runs on its
-        own stream.  The batch must be grouped by instance, ``updates_per_instance`` distinct oracles
-        per instance in instance order (SyntheticUpdateStream's layout).  Same results as
-        ``apply_updates(..., unique=True); run_round()`` (ranges are disjoint instances).  GPU fast mode
-        only; graph-capturable (fork/join through stream waits)."""
+        The update scatter is HBM-bound and the round kernel VALU-bound, so they overlap: the updates of
+        range k+1 (one update stream, in order) run while the round of range k runs on its own stream.
+        The batch must be grouped by instance, ``updates_per_instance`` distinct oracles per instance in
+        instance order (SyntheticUpdateStream's layout).  Same results as ``apply_updates(...,
+        unique=True); run_round()`` (ranges are disjoint instances).  GPU fast mode only;
+        graph-capturable (fork/join through stream waits / events).
+
+        ``overlap=True`` also overlaps consecutive steps: every range runs on its own stream (its update,
+        then its round), the streams are not joined back at the end, so the next call's update of range
+        k queues behind this call's round of range k (the one kernel that reads those rows) and runs
+        beside the other ranges' rounds.  The engine is then "open": :meth:`pipeline_join` (called by
+        every other engine method) joins the streams into the current stream before anything else
+        touches the state."""
         U = int(updates_per_instance)
         if self.mode != "fast" or self.device.type != "cuda" or chunks <= 1:
+            self.pipeline_join()
             self.apply_updates(inst, oracle, vals, unique=True)
             self.run_round()
             return
@@ -193,22 +204,49 @@ class ConsensusEngine:
             raise ValueError("step_pipelined: expects updates_per_instance updates for every instance")
         cur = torch.cuda.current_stream(self.device)
         if getattr(self, "_pipe_streams", None) is None or len(self._pipe_streams) != chunks + 1:
+            self.pipeline_join()
             self._pipe_streams = [torch.cuda.Stream(self.device) for _ in range(chunks + 1)]
         su, sc = self._pipe_streams[0], self._pipe_streams[1:]
-        su.wait_stream(cur)
         step = (self.B + chunks - 1) // chunks
-        for k in range(chunks):
-            b0, b1 = k * step, min(self.B, (k + 1) * step)
-            if b0 >= b1:
-                break
+        ranges = [(k * step, min(self.B, (k + 1) * step)) for k in range(chunks) if k * step < self.B]
+        if overlap:
+            # range k lives on stream sc[k] alone (update, then round; the next step's update of range k
+            # queues behind this round on the same stream: no cross-stream waits).  The streams start
+            # staggered by one update (sc[k] waits for range k-1's update once, after a join), so each
+            # range's update runs beside another range's round, also across steps.
+            fresh = not getattr(self, "_pipe_open", False)
+            for k, (b0, b1) in enumerate(ranges):
+                sc[k].wait_stream(cur)
+                if fresh and k > 0:
+                    sc[k].wait_stream(sc[k - 1])     # holds only range k-1's update at this point
+                with torch.cuda.stream(sc[k]):
+                    self.apply_updates(inst[b0 * U:b1 * U], oracle[b0 * U:b1 * U], vals[b0 * U:b1 * U],
+                                       unique=True, _joined=True)
+            for k, (b0, b1) in enumerate(ranges):
+                with torch.cuda.stream(sc[k]):
+                    self._run_round_range(b0, b1)
+            self.rounds += 1
+            self._pipe_open = True
+            return
+        su.wait_stream(cur)
+        for k, (b0, b1) in enumerate(ranges):
             with torch.cuda.stream(su):
-                self.apply_updates(inst[b0 * U:b1 * U], oracle[b0 * U:b1 * U], vals[b0 * U:b1 * U], unique=True)
+                self.apply_updates(inst[b0 * U:b1 * U], oracle[b0 * U:b1 * U], vals[b0 * U:b1 * U], unique=True,
+                                   _joined=True)
             sc[k].wait_stream(su)
             with torch.cuda.stream(sc[k]):
                 self._run_round_range(b0, b1)
+        self.rounds += 1
         for s in self._pipe_streams:
             cur.wait_stream(s)
-        self.rounds += 1
+
+    def pipeline_join(self) -> None:
+        """Join the streams of an open (``overlap=True``) pipelined step into the current stream."""
+        if getattr(self, "_pipe_open", False):
+            cur = torch.cuda.current_stream(self.device)
+            for s in self._pipe_streams:
+                cur.wait_stream(s)
+            self._pipe_open = False
 
     def work(self) -> Optional[torch.Tensor]:
         """Workspace of the one-network window kernel (34 window keys + 8 power sums + 2 cleanup
@@ -225,6 +263,7 @@ class ConsensusEngine:
 
     def metrics(self) -> torch.Tensor:
         """[sum rel2 of committed rounds, committed, processed, reverted] as float64 (device)."""
+        self.pipeline_join()
         m = self.metrics_fx.double()
         m[0] *= (2.0 ** -32) if self.mode == "fast" else 1e-6
         return m
@@ -239,6 +278,7 @@ class ConsensusEngine:
         the transaction waves are strided views: no host synchronisation at all (graph-capturable).
         That layout is trusted, as in :meth:`step_pipelined` (an instance twice in one wave breaks the
         sequential order); any other batch goes through the general device-side grouping."""
+        self.pipeline_join()
         if self.mode == "fast":
             st = self.apply_updates(inst, oracle, vals)
             self.run_round()
@@ -326,6 +366,7 @@ class ConsensusEngine:
     # ------------------------------------------------------------------ synthetic data
     def randomize(self, seed: int = 0, a: float = 20.0, failing_low: float = 0.0) -> None:
         """Fill every oracle of every instance (Beta(a,a) honest, U(0,1) failing), all enabled."""
+        self.pipeline_join()
         from .models.oracle_gen import beta_failing_oracles
         g = torch.Generator(device=self.device).manual_seed(seed)
         x = beta_failing_oracles(self.B, self.N, self.D, self.cfg.n_failing_oracles, a, g, self.device)
@@ -339,28 +380,36 @@ class ConsensusEngine:
 
     # ------------------------------------------------------------------ getters (contract ABI names)
     def get_consensus_value(self, i: Optional[int] = None) -> torch.Tensor:
+        self.pipeline_join()
         return self.consensus if i is None else self.consensus[i]
 
     def get_first_pass_consensus_reliability(self, i: Optional[int] = None):
+        self.pipeline_join()
         return self.rel[:, 0] if i is None else self.rel[i, 0]
 
     def get_second_pass_consensus_reliability(self, i: Optional[int] = None):
+        self.pipeline_join()
         return self.rel[:, 1] if i is None else self.rel[i, 1]
 
     def get_skewness(self, i: Optional[int] = None):
+        self.pipeline_join()
         return self.skew if i is None else self.skew[i]
 
     def get_kurtosis(self, i: Optional[int] = None):
+        self.pipeline_join()
         return self.kurt if i is None else self.kurt[i]
 
     def get_reliability(self) -> torch.Tensor:
         """North-star alias: [B, 2] (first pass, second pass)."""
+        self.pipeline_join()
         return self.rel
 
     get_consensus = get_consensus_value
 
     def get_predictions_dimension(self) -> int:
+        self.pipeline_join()
         return self.D
 
     def get_oracle_value_list(self, i: int):
+        self.pipeline_join()
         return (self.values[i, :, : self.D], self.enabled[i].bool(), self.reliable[i].bool())

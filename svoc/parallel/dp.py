@@ -47,6 +47,7 @@ class DataParallelConsensus:
         """One all-reduce of the integer counters (RCCL on GPU), then float64 metrics:
         [sum rel2 of committed rounds, committed, processed, reverted]."""
         e = self.engine
+        e.pipeline_join()
         self._fx.copy_(e.metrics_fx)
         if self.world > 1:
             dist.all_reduce(self._fx, op=dist.ReduceOp.SUM, group=self.group)
@@ -70,6 +71,7 @@ class DataParallelConsensus:
     def all_gather_summaries(self, k: int = 4) -> Optional[Dict[str, torch.Tensor]]:
         """Gather [world*B] summaries (first k consensus components, rel, status) to every rank."""
         e = self.engine
+        e.pipeline_join()
         local = torch.cat([e.consensus[:, :k].double(), e.rel.double(), e.status[:, None].double()], dim=1)
         if self.world == 1:
             full = local

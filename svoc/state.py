@@ -22,6 +22,7 @@ FORMAT = "svoc-state/1"
 
 def save(svc, path: str) -> None:
     e, g = svc.engine, svc.gov
+    e.pipeline_join()
     D = e.D
     exact = e.mode == "exact"
     num = "i128" if exact else ""

@@ -69,3 +69,46 @@ def test_step_pipelined_rejects_ungrouped_batch():
     with pytest.raises(ValueError):
         a.step_pipelined(torch.zeros(3, dtype=torch.long, device=DEV), torch.zeros(3, dtype=torch.long, device=DEV),
                          torch.zeros(3, 128, device=DEV), 2, chunks=2)
+
+
+@pytest.mark.parametrize("chunks", [2, 3])
+def test_step_pipelined_overlap_matches_serial(chunks):
+    """overlap=True: consecutive steps overlap (range 0's update beside the previous step's last round;
+    each range's update waits only for the previous step's round of that range) -- same state."""
+    N, D, f, B, U = 256, 512, 32, 9, 64
+    a, b = _pair(N, D, f, B)
+    st = SyntheticUpdateStream(B, N, D, U, f, pool=2, device=DEV, seed=7)
+    for i in range(4):
+        a.step_pipelined(*st.batch(i), U, chunks=chunks, overlap=True)
+        b.apply_updates(*st.batch(i), unique=True)
+        b.run_round()
+    m = a.metrics()            # joins the open pipeline before reading
+    assert not a._pipe_open
+    _same(a, b)
+    assert torch.equal(m, b.metrics())
+
+
+def test_step_pipelined_overlap_in_graph():
+    """Four overlapped steps captured in one graph (joined at the end of the capture), replayed twice."""
+    N, D, f, B, U = 256, 640, 32, 8, 64
+    a, b = _pair(N, D, f, B)
+    st = SyntheticUpdateStream(B, N, D, U, f, pool=2, device=DEV, seed=11)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):   # warm-up outside capture (allocations, stream creation)
+        a.step_pipelined(*st.batch(0), U, chunks=2, overlap=True)
+        a.pipeline_join()
+    torch.cuda.current_stream().wait_stream(s)
+    b.apply_updates(*st.batch(0), unique=True)
+    b.run_round()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(4):
+            a.step_pipelined(*st.batch(i + 1), U, chunks=2, overlap=True)
+        a.pipeline_join()
+    for _ in range(2):
+        g.replay()
+        for i in range(4):
+            b.apply_updates(*st.batch(i + 1), unique=True)
+            b.run_round()
+    _same(a, b)
