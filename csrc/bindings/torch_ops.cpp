@@ -180,12 +180,10 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
   p.work_pairs = (int)fast_work_pairs(D);
   p.work_stride = words;
   auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
+  // (mode 0: the kernel, or its dispatcher, commits the staged c1 into c1_out)
+  p.c1_out = mode == 0 ? c1.data_ptr<float>() : nullptr;
   const int rc = f32 ? svoc_fast_round_f32(&p, stream) : svoc_fast_round_bf16(&p, stream);
   TORCH_CHECK(rc == 0, f32 ? "svoc_fast_round_f32" : "svoc_fast_round_bf16", " launch failed: ", rc);
-  if (mode == 0) {
-    const int rc2 = svoc_commit_rows(c1_stage.data_ptr(), c1.data_ptr(), p.status, p.active, B, D, stream);
-    TORCH_CHECK(rc2 == 0, "svoc_commit_rows failed: ", rc2);
-  }
 }
 
 // -------------------------------------------------------------------------------------- exact

@@ -32,6 +32,10 @@ struct FastParams {
   int64_t work_stride;      // u32 words per instance in `work`
   float win_cancel;         // window kernel: max all-row / reliable power-sum ratio trusted (else cleanup)
   int work_fresh;           // the workspace holds no pass-1 state (mode 2 must not use the window kernel)
+  // mode 0: c1 above is the round's staging row; c1_out [B, D] receives it only where the round
+  // succeeded (the window kernels write it in their commit phase, the dispatchers commit it for the
+  // others with svoc_commit_rows).  Null: the caller commits (or mode 1 / 2: c1 is the output itself).
+  float* c1_out;
 };
 
 // Workspace per instance of the LDS-free fast kernels, in u32 words (Dp = fast_work_pairs(D)).

@@ -49,29 +49,36 @@ __global__ __launch_bounds__(256) void round_epilogue_kernel(RoundBook r) {
 
 // Commit of staged per-instance rows (the round's c1): row b of src -> dst when instance b ran a round
 // (active, or every instance when active is null) and it succeeded.  A reverted round leaves dst
-// untouched, like every other output (contract.cairo:588-603).  Flat over B * words 4-byte words.
+// untouched, like every other output (contract.cairo:588-603).  One workgroup per row (grid-strided
+// over rows): the row's status is read once and the words move as 16-B vectors when rows allow it.
 __global__ __launch_bounds__(256) void commit_rows_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                                          const int32_t* __restrict__ status,
                                                          const uint8_t* __restrict__ active, uint32_t words,
-                                                         uint32_t total) {
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
-    const uint32_t b = i / words;
-    if (status[b] == ST_OK && (!active || active[b])) dst[i] = src[i];
+                                                         uint32_t rows, int vec) {
+  for (uint32_t b = blockIdx.x; b < rows; b += gridDim.x) {
+    if (status[b] != ST_OK || (active && !active[b])) continue;   // uniform over the workgroup
+    const uint64_t o = (uint64_t)b * words;
+    if (vec) {
+      const uint4* s4 = (const uint4*)(src + o);
+      uint4* d4 = (uint4*)(dst + o);
+      for (uint32_t i = threadIdx.x; i < words / 4; i += 256) d4[i] = s4[i];
+    } else {
+      for (uint32_t i = threadIdx.x; i < words; i += 256) dst[o + i] = src[o + i];
+    }
   }
 }
-
 }  // namespace svoc
 
 using namespace svoc;
 
 extern "C" int svoc_commit_rows(const void* src, void* dst, const int32_t* status, const uint8_t* active, int64_t B,
                                 int64_t words, hipStream_t stream) {
-  const int64_t total = B * words;
-  if (total <= 0) return 0;
-  if (total >= (1ll << 32) || words <= 0) return -1;
-  const int64_t blocks = (total + 255) / 256;
-  hipLaunchKernelGGL(commit_rows_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, stream,
-                     (const uint32_t*)src, (uint32_t*)dst, status, active, (uint32_t)words, (uint32_t)total);
+  if (B <= 0 || words <= 0) return B <= 0 ? 0 : -1;
+  if (B * words >= (1ll << 32) || B >= (1ll << 31)) return -1;
+  const int vec = (words % 4 == 0) && (((uintptr_t)src | (uintptr_t)dst) % 16 == 0);
+  const int64_t blocks = B < 8192 ? B : 8192;
+  hipLaunchKernelGGL(commit_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (const uint32_t*)src,
+                     (uint32_t*)dst, status, active, (uint32_t)words, (uint32_t)B, vec);
   return (int)hipGetLastError();
 }
 

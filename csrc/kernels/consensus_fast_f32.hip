@@ -521,12 +521,17 @@ extern "C" int svoc_fast_round_f32(const FastParams* p, hipStream_t stream) {
     const int rc = svoc_fast_round_f32_win(p, stream);
     if (rc != -2) return rc;
   }
-  if (p->N <= 64) return launch_f32<1>(*p, stream);
-  if (p->N <= 128) return launch_f32<2>(*p, stream);
-  if (p->N <= 256) return launch_f32<4>(*p, stream);
-  if (p->N <= 512) return launch_f32<8>(*p, stream);
-  if (p->N <= 1024) return launch_f32<16>(*p, stream);
+  int rc;
+  if (p->N <= 64) rc = launch_f32<1>(*p, stream);
+  else if (p->N <= 128) rc = launch_f32<2>(*p, stream);
+  else if (p->N <= 256) rc = launch_f32<4>(*p, stream);
+  else if (p->N <= 512) rc = launch_f32<8>(*p, stream);
+  else if (p->N <= 1024) rc = launch_f32<16>(*p, stream);
   // N > 1024: 32 / 64 lanes per column (two / one column per wave), the same cross-lane bitonic sort
-  if (p->N <= 2048) return launch_f32<32>(*p, stream);
-  return launch_f32<64>(*p, stream);
+  else if (p->N <= 2048) rc = launch_f32<32>(*p, stream);
+  else rc = launch_f32<64>(*p, stream);
+  // c1 (mode 0 with c1_out): the window kernel commits it itself, this kernel stages it
+  if (rc == 0 && p->mode == 0 && p->c1_out)
+    rc = svoc_commit_rows(p->c1, p->c1_out, p->status, p->active, p->B, p->D, stream);
+  return rc;
 }

@@ -632,7 +632,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
       // within 2 sigma of the shift c1 (moments about a far shift cancel like (dl^2 / mu2)^2)
       const float rdl = (h ? t1.y : t1.x) / n, rmu2 = r2 / n - rdl * rdl;
       const bool good = r2 > 0.f && a2 <= p.win_cancel * r2 && a4 <= p.win_cancel * r4 && rdl * rdl <= 4.f * rmu2;
-      if (CONS) p.consensus[ob + col] = h ? 0.5f * (bf16_hi(medw) + bf16_hi(mhw)) : 0.5f * (bf16_lo(medw) + bf16_lo(mhw));
+      if (CONS) {
+        p.consensus[ob + col] = h ? 0.5f * (bf16_hi(medw) + bf16_hi(mhw)) : 0.5f * (bf16_lo(medw) + bf16_lo(mhw));
+        if (MODE == 0 && p.c1_out) p.c1_out[ob + col] = h ? c1B : c1A;   // (no revert after the pre-check)
+      }
       if (good) {
         float dl, sk, ku;
         const bool nz = moments_from_sums(n, h ? t1.y : t1.x, r2, h ? t3.y : t3.x, r4, dl, sk, ku);
@@ -718,6 +721,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
       return;
     }
     commit_staged<NT>(ws, STG, D2, D, tid, p.consensus + ob, p.skew + ob, p.kurt + ob);
+    if (MODE == 0 && p.c1_out)
+      for (int c = tid; c < D; c += NT) p.c1_out[ob + c] = p.c1[ob + c];
     for (int t = tid; t < N; t += NT) {
       p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
       p.qr[(int64_t)b * N + t] = qr_lds[t];
@@ -793,12 +798,20 @@ extern "C" int svoc_fast_round_bf16_small(const FastParams* p, hipStream_t strea
 //   default: this one-network window kernel where it applies (workspace given, f <= 32, N <= 256);
 //   otherwise, and for wave_hint -7 (tests: the cross-check), the two-network register-streaming kernel
 //     (consensus_fast_reg.hip).
+//   c1 (mode 0 with c1_out): the window kernel commits it itself; after the others, commit_rows does.
 extern "C" int svoc_fast_round_bf16(const FastParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
-  if (p->wave_hint == 0 && p->mode == 0 && p->N <= 16 && p->D <= 128) return svoc_fast_round_bf16_small(p, stream);
-  if (p->wave_hint != -7) {
-    const int rc = svoc_fast_round_bf16_win(p, stream);
-    if (rc != -2) return rc;
+  int rc;
+  if (p->wave_hint == 0 && p->mode == 0 && p->N <= 16 && p->D <= 128) {
+    rc = svoc_fast_round_bf16_small(p, stream);
+  } else {
+    if (p->wave_hint != -7) {
+      rc = svoc_fast_round_bf16_win(p, stream);
+      if (rc != -2) return rc;
+    }
+    rc = svoc_fast_round_bf16_reg(p, stream);
   }
-  return svoc_fast_round_bf16_reg(p, stream);
+  if (rc == 0 && p->mode == 0 && p->c1_out)
+    rc = svoc_commit_rows(p->c1, p->c1_out, p->status, p->active, p->B, p->D, stream);
+  return rc;
 }

@@ -523,7 +523,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       const double rdl = r1 / n, rmu2 = r2 / n - rdl * rdl;
       const double wc = (double)p.win_cancel;
       const bool good = r2 > 0.0 && a2 <= wc * r2 && a4 <= wc * r4 && rdl * rdl <= 4.0 * rmu2;
-      if (CONS) p.consensus[ob + col] = cons_v;
+      if (CONS) {
+        p.consensus[ob + col] = cons_v;
+        if (MODE == 0 && p.c1_out) p.c1_out[ob + col] = c1c;   // (no revert after the pre-check)
+      }
       if (good) {
         double dl;
         float sk, ku;
@@ -611,6 +614,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       return;
     }
     commit_staged<NT>(ws, STG, Dc, D, tid, p.consensus + ob, p.skew + ob, p.kurt + ob);
+    if (MODE == 0 && p.c1_out)
+      for (int c = tid; c < D; c += NT) p.c1_out[ob + c] = p.c1[ob + c];
     for (int t = tid; t < N; t += NT) {
       p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
       p.qr[(int64_t)b * N + t] = qr_lds[t];

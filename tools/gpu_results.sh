@@ -17,6 +17,7 @@ d = json.loads(line); d["key"] = sys.argv[1]; print(json.dumps(d))
 PY
   tail -1 $OUT | cut -c1-160
 }
+if [ -z "${PART2:-}" ]; then
 run c3 400 --config c3 --steps 20 --warmup 3 &&
 run c3_bf16 300 --config c3 --storage bf16 --steps 20 --warmup 3 &&
 run c2 300 --config c2 --steps 20 --warmup 3 &&
@@ -28,7 +29,8 @@ run c2_exact_int64 300 --config c2 --mode exact --storage int64 --steps 10 --war
 run c5_exact 300 --config-file configs/c5_exact_rounds.yaml --steps 20 --warmup 2 &&
 run c3_exact 300 --config-file configs/c3_exact_rounds.yaml --steps 10 --warmup 2 &&
 run c5_exact_stream 300 --config-file configs/c5_exact_stream.yaml --steps 20 --warmup 2 &&
-run c3_exact_stream 400 --config-file configs/c3_exact_stream.yaml --steps 3 --warmup 1 &&
+true || exit 1
+fi
 run wide512 300 --config-file configs/wide512.yaml --steps 10 --warmup 2 &&
 run wide512_fp32 300 --config-file configs/wide512.yaml --storage fp32 --steps 10 --warmup 2 &&
 run wide2048 300 --config-file configs/wide2048.yaml --steps 5 --warmup 1 &&
@@ -41,4 +43,6 @@ for spec in "c3:--storage fp32" "c2:--storage bf16" "c4:"; do   # one storage pe
       -d $R/gpurun_out/prof_$cfg -o run -- python3 $R/bench.py --config $cfg --steps 6 --warmup 1 --graph 0 $extra \
       > $R/gpurun_out/prof_$cfg.log 2>&1) || exit 1
 done
+# last: 64 exact transactions per instance per step (a 64-instance batch keeps it short)
+run c3_exact_stream 150 --config-file configs/c3_exact_stream.yaml --batch 64 --steps 2 --warmup 1 || exit 1
 echo "=== done"
