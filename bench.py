@@ -117,7 +117,10 @@ def measure(args, c, storage, dev, rank, world, dshard):
         # D-sharding: every rank streams the same updates (same seed), its own column slice of them
         stream = SyntheticUpdateStream(B, c["N"], D_local, U_per_inst, c["f"], pool=2, device=dev,
                                        seed=(0 if dshard else rank),
-                                       dtype=torch.int64 if mode == "exact" else eng.vdtype)
+                                       dtype=torch.int64 if mode == "exact" else eng.vdtype,
+                                       # the state's failing oracles stay the failing ones (D-shard:
+                                       # every rank's slice of the same rows, so the stream's own set)
+                                       failing=None if dshard else eng.failing_mask)
     if args.config == "c5":
         from svoc.codec import address_to_limbs
         from svoc.governance import Governance

@@ -88,6 +88,7 @@ class ConsensusEngine:
         self._active = torch.zeros(B, dtype=torch.uint8, device=dev)
         self.wave_hint = 0
         self.rounds = 0
+        self.failing_mask: Optional[torch.Tensor] = None   # [B, N] set by randomize()
         self._work = None   # window-kernel workspace (GPU fast mode), allocated on first use
         # health counters folded in by every round's epilogue: [rel2 sum (2^-32 units fast / wsad
         # exact), committed, processed, reverted]
@@ -365,11 +366,14 @@ class ConsensusEngine:
 
     # ------------------------------------------------------------------ synthetic data
     def randomize(self, seed: int = 0, a: float = 20.0, failing_low: float = 0.0) -> None:
-        """Fill every oracle of every instance (Beta(a,a) honest, U(0,1) failing), all enabled."""
+        """Fill every oracle of every instance (Beta(a,a) honest, U(0,1) failing), all enabled.  The
+        [B, N] failing set is kept in :attr:`failing_mask` (a synthetic update stream that keeps the same
+        oracles failing: SyntheticUpdateStream(failing=...))."""
         self.pipeline_join()
         from .models.oracle_gen import beta_failing_oracles
         g = torch.Generator(device=self.device).manual_seed(seed)
-        x = beta_failing_oracles(self.B, self.N, self.D, self.cfg.n_failing_oracles, a, g, self.device)
+        x, self.failing_mask = beta_failing_oracles(self.B, self.N, self.D, self.cfg.n_failing_oracles, a, g,
+                                                    self.device, return_mask=True)
         if self.mode == "exact":
             self.values[:, :, : self.D] = (x.double() * WSAD).to(torch.int64).to(self.vdtype)
         else:

@@ -19,11 +19,14 @@ from .models.oracle_gen import failing_mask
 
 class SyntheticUpdateStream:
     def __init__(self, B: int, N: int, D: int, U: int, f: int, pool: int = 2, device="cuda", seed: int = 0,
-                 a: float = 20.0, dtype=torch.bfloat16):
+                 a: float = 20.0, dtype=torch.bfloat16, failing: Optional[torch.Tensor] = None):
         self.B, self.N, self.D, self.U, self.pool = B, N, D, U, pool
         dev = torch.device(device)
         g = torch.Generator(device=dev).manual_seed(seed)
-        self.failing = failing_mask(B, N, f, g, dev)            # [B, N] fixed per instance
+        # [B, N] fixed per instance: the engine's own failing set (ConsensusEngine.failing_mask) when given,
+        # so a state and its stream agree on which f oracles fail (an extra noisy oracle per update would
+        # stay among the reliable rows)
+        self.failing = (failing.to(dev, torch.bool) if failing is not None else failing_mask(B, N, f, g, dev))
         self.batches: List[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = []
         inst = torch.arange(B, device=dev).repeat_interleave(U)
         for _ in range(pool):
