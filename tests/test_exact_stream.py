@@ -146,3 +146,27 @@ def test_strided_layout_must_divide():
 @pytest.mark.gpu
 def test_exact_stream_gpu():
     _covers_reverts(_run_general("cuda"), _run_strided("cuda"))
+
+
+def test_synthetic_stream_keeps_engine_failing_set():
+    """bench.py's update stream draws its U(0,1) rows for the engine's own failing oracles
+    (ConsensusEngine.failing_mask): an honest oracle never receives a uniform row, so no instance ends
+    up with more than f noisy oracles (which the exact column kernel hands to the i128 kernel)."""
+    from svoc.engine import ConsensusEngine
+    from svoc.stream import SyntheticUpdateStream
+    B, n, d, f, U = 3, 16, 40, 3, 8
+    cfg = ConsensusConfig(n_oracles=n, dimension=d, n_failing_oracles=f, constrained=True)
+    eng = ConsensusEngine(cfg, batch=B, device="cpu", mode="exact")
+    eng.randomize(seed=4)
+    m = eng.failing_mask
+    assert m.shape == (B, n) and (m.sum(1) == f).all()
+    s = SyntheticUpdateStream(B, n, d, U, f, pool=2, device="cpu", seed=1, dtype=torch.int64, failing=m)
+    assert torch.equal(s.failing, m)
+    for k in range(2):
+        inst, orc, vals = s.batch(k)
+        # honest rows are Beta(20, 20): none is near 0 or 1 in every column, uniform rows spread out
+        spread = (vals.double() / 1e6).std(dim=1)
+        fail = m[inst, orc]
+        assert (spread[~fail] < 0.15).all() and (spread[fail] > 0.15).all()
+    eng.step(*s.batch(0), updates_per_instance=U)
+    assert (eng.status == int(Status.OK)).all()

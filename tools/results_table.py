@@ -21,7 +21,9 @@ RESULTS = os.path.join(ROOT, "profiles", "results.jsonl")
 ROWS = [
     ("c1", "c1: 4 oracles × 2 dims, one exact round, CPU (plumbing)", "2,518/s Python emulator (7×2)"),
     ("c2", "c2: 64 × 1024, 10k batched instances, bf16", "≈93/s numpy fp64"),
-    ("c3", "c3: 256 × 4096 streaming, failing-oracle masking (headline)", "≈6/s numpy fp64"),
+    ("c3", "c3: 256 × 4096 streaming, failing-oracle masking, fp32 storage (headline: reference resolution)",
+     "≈6/s numpy fp64"),
+    ("c3_bf16", "c3 shape, fast mode over bf16 storage", "≈6/s numpy fp64"),
     ("c4", "c4: BERT-base sentiment oracles → consensus", "—"),
     ("c5", "c5: governance + reliability stream, 1M instances (7 × 6)", "≈127,900/s numpy fp64 (7×6)"),
     ("c2_fp32", "c2 shape, fast mode over fp32 storage (reference resolution)", "≈93/s numpy fp64"),
@@ -30,8 +32,14 @@ ROWS = [
     ("c2_exact_int64", "c2 shape, exact wsad, int64 storage", "0.61/s exact Python emulator"),
     ("c3_exact", "c3 shape (256 × 4096), exact wsad, int32 storage", "≈6/s numpy fp64 (non-exact)"),
     ("c5_exact", "c5 shape (7 × 6), exact wsad, 1M instances", "939/s exact Python emulator"),
+    ("c5_exact_stream", "c5 shape, exact transactional update stream (store + round + revert per update)",
+     "939/s exact Python emulator"),
+    ("c3_exact_stream", "c3 shape, exact transactional update stream, 64 instances × 64 transactions/step",
+     "0.61/s exact Python emulator (64 × 1024)"),
     ("wide512", "512 oracles × 2048 dims, 1024 instances (N > 256)", "—"),
     ("wide512_fp32", "512 × 2048, fast mode over fp32 storage", "—"),
+    ("wide2048", "2048 oracles × 512 dims (N > 1024)", "—"),
+    ("wide2048_fp32", "2048 × 512, fast mode over fp32 storage", "—"),
 ]
 
 
