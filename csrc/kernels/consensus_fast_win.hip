@@ -95,10 +95,18 @@ SVOC_DEV float qr_tree(const QrCtx& c, const uint32_t (&wv)[64], f32x2& s1, f32x
     constexpr int msk = P >> L;
     const float lo_v = qr_tree<L - 1, I, P, MASKROWS>(c, wv, s1, s2, s3, s4);
     const float hi_v = qr_tree<L - 1, I + (64 >> L), P, MASKROWS>(c, wv, s1, s2, s3, s4);
-    const bool up = (c.lane & msk) != 0;
-    const float send = up ? lo_v : hi_v;
-    const float keep = up ? hi_v : lo_v;
-    return keep + xor_lane<msk>(send);
+    if constexpr (msk == 32 || msk == 16) {
+      // one v_permlane{32,16}_swap: the lower lane ends with (own lo, partner's lo), the upper lane with
+      // (partner's hi, own hi) -- the same sums as the select form below, no selects
+      uint32_t x = __builtin_bit_cast(uint32_t, lo_v), y = __builtin_bit_cast(uint32_t, hi_v);
+      xswap<msk>(x, y);
+      return __builtin_bit_cast(float, x) + __builtin_bit_cast(float, y);
+    } else {
+      const bool up = (c.lane & msk) != 0;
+      const float send = up ? lo_v : hi_v;
+      const float keep = up ? hi_v : lo_v;
+      return keep + xor_lane<msk>(send);
+    }
   }
 }
 // One butterfly tree (final slot I): its 64/KEEP rows I, I + KEEP, ... are loaded together (all in
