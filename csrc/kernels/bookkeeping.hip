@@ -49,8 +49,9 @@ __global__ __launch_bounds__(256) void round_epilogue_kernel(RoundBook r) {
 
 // Commit of staged per-instance rows (the round's c1): row b of src -> dst when instance b ran a round
 // (active, or every instance when active is null) and it succeeded.  A reverted round leaves dst
-// untouched, like every other output (contract.cairo:588-603).  One workgroup per row (grid-strided
-// over rows): the row's status is read once and the words move as 16-B vectors when rows allow it.
+// untouched, like every other output (contract.cairo:588-603).  Wide rows (>= 256 words): one
+// workgroup per row (grid-strided), the status read once, 16-B vectors when the rows allow it; narrow
+// rows (the deployed 7 x 6: 6 words): flat over B * words, one word per thread.
 __global__ __launch_bounds__(256) void commit_rows_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
                                                          const int32_t* __restrict__ status,
                                                          const uint8_t* __restrict__ active, uint32_t words,
@@ -67,6 +68,15 @@ __global__ __launch_bounds__(256) void commit_rows_kernel(const uint32_t* __rest
     }
   }
 }
+__global__ __launch_bounds__(256) void commit_words_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                          const int32_t* __restrict__ status,
+                                                          const uint8_t* __restrict__ active, uint32_t words,
+                                                          uint32_t total) {
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const uint32_t b = i / words;
+    if (status[b] == ST_OK && (!active || active[b])) dst[i] = src[i];
+  }
+}
 }  // namespace svoc
 
 using namespace svoc;
@@ -75,6 +85,12 @@ extern "C" int svoc_commit_rows(const void* src, void* dst, const int32_t* statu
                                 int64_t words, hipStream_t stream) {
   if (B <= 0 || words <= 0) return B <= 0 ? 0 : -1;
   if (B * words >= (1ll << 32) || B >= (1ll << 31)) return -1;
+  if (words < 256) {
+    const int64_t blocks = (B * words + 255) / 256;
+    hipLaunchKernelGGL(commit_words_kernel, dim3((unsigned)(blocks < 8192 ? blocks : 8192)), dim3(256), 0, stream,
+                       (const uint32_t*)src, (uint32_t*)dst, status, active, (uint32_t)words, (uint32_t)(B * words));
+    return (int)hipGetLastError();
+  }
   const int vec = (words % 4 == 0) && (((uintptr_t)src | (uintptr_t)dst) % 16 == 0);
   const int64_t blocks = B < 8192 ? B : 8192;
   hipLaunchKernelGGL(commit_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, (const uint32_t*)src,
