@@ -38,6 +38,13 @@
 #include "svoc/sortnet.hpp"
 #include "svoc/status.hpp"
 
+// Diagnostic builds only (SVOC_HIPCC_FLAGS=-DSVOC_WINF_PROBE=n, tools/winf_probe.py; wrong results):
+// 1 = phase A without the window network, 2 = phase A without the HBM stream (no DMA, stale LDS),
+// 3 = the full kernel, workgroup phase end times (s_memrealtime ticks since its start) in skew[b, 0..5].
+#ifndef SVOC_WINF_PROBE
+#define SVOC_WINF_PROBE 0
+#endif
+
 namespace svoc {
 
 // Constrained keys: values validated to [0, 1] (sign bit clear, or -0.0: key 0, just below +0.0) ->
@@ -158,13 +165,17 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
   __shared__ int urow[32];      // removed rows, index order
   __shared__ float misc_f[2];
   __shared__ int misc_i[3];     // status, zero-variance flag, cleanup list length
+  __shared__ uint32_t redo[128];   // constrained, D <= 4096: the cleanup columns as a bit mask
 
   const int b = blockIdx.x;
   if (p.active && !p.active[b]) return;
+  uint64_t stamp[6] = {0, 0, 0, 0, 0, 0};
+  if constexpr (SVOC_WINF_PROBE == 3) stamp[0] = __builtin_amdgcn_s_memrealtime();
   // (wave made explicitly uniform: it feeds the DMA's M0 and SGPR row offsets)
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid < 32) urow[tid] = 0;  // f < 32: unused slots still name a valid row
   if (tid == 0) misc_i[2] = 0;
+  if (tid < 128) redo[tid] = 0u;
   const int seg = lane / P, cw = lane % P;
   const int N = p.N, D = p.D;
   const int rowb = p.ld * 4;
@@ -202,7 +213,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
   uint32_t* const region = slab + (PASS1 ? wave * 64 * 64 : 0);
   // this lane's words: global row seg * 64 + i at LDS row NSEG * i + seg, i.e. word 64 i + seg P + cw
   const uint32_t* const mine = region + (PASS1 ? seg * P + cw : 0);
-  if (pass1_slabs > 0) dma.issue(rsd, region, rowb, wave * P);
+  if (pass1_slabs > 0 && SVOC_WINF_PROBE != 2) dma.issue(rsd, region, rowb, wave * P);
   // One slab of phase A.  FULL: every column of the slab is < D and N = NPAD, so no masks at all; the
   // masked form serves the tail slab and padded N.  (One body per loop: reading the raw rows in two
   // branches of one loop makes the compiler demote them to scratch.)
@@ -222,7 +233,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       xs.hi[i] = mine[(i + 32) * 64];
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0): the region is read, the next slab may land
-    if (s + 1 < pass1_slabs) dma.issue(rsd, region, rowb, (s + 1) * W + wave * P);
+    if (s + 1 < pass1_slabs && SVOC_WINF_PROBE != 2) dma.issue(rsd, region, rowb, (s + 1) * W + wave * P);
     {
       uint32_t r[64];
       if (FULL || N == NPAD) {
@@ -240,7 +251,14 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       uint32_t klo, khi;
       if constexpr (CONS) {
         uint32_t wk[NSEG == 1 ? 2 * H : H];
-        window_group<NSEG, P, H>(r, seg, lane, wk, klo, khi);
+        if constexpr (SVOC_WINF_PROBE == 1) {
+#pragma unroll
+          for (int m = 0; m < (NSEG == 1 ? 2 * H : H); ++m) wk[m] = r[m];
+          klo = r[31];
+          khi = r[32];
+        } else {
+          window_group<NSEG, P, H>(r, seg, lane, wk, klo, khi);
+        }
         if constexpr (NSEG == 1) {
 #pragma unroll
           for (int m = 0; m < H; ++m) {
@@ -294,6 +312,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     for (int s = nfull; s < pass1_slabs; ++s) slab_body(std::false_type{}, s);
   }
 
+  if constexpr (SVOC_WINF_PROBE == 3) stamp[1] = __builtin_amdgcn_s_memrealtime();
   // ------------------------------------------------------------ qr reduction
   {
     if constexpr (ACC64) qr_keep<P>(acc, lane, keep, false);
@@ -399,6 +418,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     return;
   }
 
+  if constexpr (SVOC_WINF_PROBE == 3) stamp[2] = __builtin_amdgcn_s_memrealtime();
   // ------------------------------------------------------------ zero-variance pre-check (constrained)
   // A reliable column of zero variance reverts the round (math.cairo:322,331; contract.cairo:588-603).
   // The R equal values would form a sorted run covering positions [f, N - f - 1]; when f + H <= N/2 that
@@ -443,39 +463,69 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     }
   }
 
+  if constexpr (SVOC_WINF_PROBE == 3) stamp[3] = __builtin_amdgcn_s_memrealtime();
   // ------------------------------------------------------------ phase B: pass 2 (contract.cairo:476-500)
-  // one lane per column: the removed keys are sorted once and ranked against the window
+  // one lane per column: the removed keys are sorted once and ranked against the window.
+  // Constrained rounds with D <= 4096 (LDSO): the outputs are staged in the idle slab region and the
+  // cleanup columns in an LDS bit mask, so the loop issues no global store -- and with loads only in
+  // flight, the next column's words (removed rows, window, power sums, c1) are loaded while this one is
+  // computed (in-order vmcnt waits).  Otherwise one column per iteration, outputs stored directly.
   const double n = (double)R;
   const int sh = H - 1 - (N / 2 - R / 2);   // -inf sentinels in front of the removed keys
   const int64_t ob = (int64_t)b * D;
   bool zv = false;
-#pragma nounroll
-  for (int base = wave * 64; base < D; base += WAVES * 64) {
+  constexpr int NS = CONS ? 2 * H : 32;
+  constexpr int NW = CONS ? H : 1;
+  struct PBWords {
+    uint32_t uw[NS];          // removed rows (constrained: the 2H network slots)
+    uint32_t wl[NW], wu[NW];  // window halves (constrained)
+    uint32_t am[4];           // all-row power sums (phase A)
+    float c1c;
+  };
+  auto pb_load = [&](int base, PBWords& q) __attribute__((always_inline)) {
     const int col = base + lane;
     const int pc = col < D ? col : D - 1;
     const int vo = pc * 4;
-    const float c1c = p.c1[ob + pc];
     // opaque per-iteration copies: otherwise LICM hoists the 2H slot offsets / masks out of the loop
     int shl = sh, fl = f;
     asm volatile("" : "+s"(shl), "+s"(fl));
-    constexpr int NS = CONS ? 2 * H : 32;
     const int s0 = CONS ? shl : 0;
     const uint64_t realm = ((fl >= 64 ? ~0ull : (1ull << fl) - 1)) << s0;
-    const uint64_t lowm = (1ull << s0) - 1;
-    uint32_t uw[NS];
+    q.c1c = p.c1[ob + pc];
 #pragma unroll
     for (int t = 0; t < NS; ++t) {
       const int row = t - s0;
       const bool real = (realm >> t) & 1;
-      uw[t] = 0u;
-      if (CONS || real) uw[t] = bload(rs, vo, __builtin_amdgcn_readfirstlane(urow[real ? row : 0]) * rowb);
+      q.uw[t] = 0u;
+      if (CONS || real) q.uw[t] = bload(rs, vo, __builtin_amdgcn_readfirstlane(urow[real ? row : 0]) * rowb);
     }
+    if constexpr (CONS) {
+#pragma unroll
+      for (int m = 0; m < H; ++m) {
+        q.wl[m] = bload(ws, pc * 4, 2 * m * Dc * 4);
+        q.wu[m] = ~bload(ws, (Dc + pc) * 4, 2 * m * Dc * 4);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q.am[k] = bload(ws, pc * 4, MOM + k * Dc * 4);
+  };
+  float* const o_lds = reinterpret_cast<float*>(slab);   // [consensus | skew | kurt | c1] x D
+  const bool ldso = CONS && PASS1 && D <= 4096;         // (4 D floats fit the WAVES x 16 KiB region)
+  auto pb_col = [&](auto ldso_c, int base, const PBWords& cur) __attribute__((always_inline)) {
+    constexpr bool LDSO = decltype(ldso_c)::value;
+    const int col = base + lane;
+    const float c1c = cur.c1c;
+    int shl = sh, fl = f;
+    asm volatile("" : "+s"(shl), "+s"(fl));
+    const int s0 = CONS ? shl : 0;
+    const uint64_t realm = ((fl >= 64 ? ~0ull : (1ull << fl) - 1)) << s0;
+    const uint64_t lowm = (1ull << s0) - 1;
     // removed rows' power sums of d = x - c1
     float u1 = 0.f, u2 = 0.f, u3 = 0.f, u4 = 0.f;
 #pragma unroll
     for (int t = 0; t < NS; ++t) {
       if ((realm >> t) & 1) {   // uniform
-        const float y = u2f(uw[t]) - c1c;
+        const float y = u2f(cur.uw[t]) - c1c;
         const float q = y * y;
         u1 += y;
         u2 += q;
@@ -492,7 +542,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
         if (t < 2 * H) {
           const uint32_t mreal = 0u - (uint32_t)((realm >> t) & 1);
           const uint32_t kx = (0x80000000u & mreal) | (~mreal & (0u - (uint32_t)(((~lowm) >> t) & 1)));
-          z[t] = (uw[t] & mreal) ^ kx;
+          z[t] = (cur.uw[t] & mreal) ^ kx;
         } else {
           z[t] = ~0u;
         }
@@ -503,8 +553,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       uint32_t clo = ~0u, chi = ~0u;
 #pragma unroll
       for (int m = 0; m < H; ++m) {
-        const uint32_t wl = bload(ws, pc * 4, 2 * m * Dc * 4);
-        const uint32_t wu = ~bload(ws, (Dc + pc) * 4, 2 * m * Dc * 4);
+        const uint32_t wl = cur.wl[m], wu = cur.wu[m];
         clo = kmin(clo, winf_cand(wl, z[m]));
         if (m) chi = kmin(chi, winf_cand(wl, z[m - 1]));
         clo = kmin(clo, winf_cand(wu, z[2 * H - 1 - m]));
@@ -512,10 +561,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       }
       cons_v = 0.5f * (fkey_val<true>(clo) + fkey_val<true>(chi));
     }
-
     // reliable rows' power sums = all-row sums (phase A) - removed rows' sums
-    const double a1 = (double)u2f(bload(ws, pc * 4, MOM)), a2 = (double)u2f(bload(ws, pc * 4, MOM + Dc * 4));
-    const double a3 = (double)u2f(bload(ws, pc * 4, MOM + 2 * Dc * 4)), a4 = (double)u2f(bload(ws, pc * 4, MOM + 3 * Dc * 4));
+    const double a1 = (double)u2f(cur.am[0]), a2 = (double)u2f(cur.am[1]);
+    const double a3 = (double)u2f(cur.am[2]), a4 = (double)u2f(cur.am[3]);
     const double r1 = a1 - (double)u1, r2 = a2 - (double)u2, r3 = a3 - (double)u3, r4 = a4 - (double)u4;
     if (col < D) {
       // trusted: no deep cancellation in the all-minus-removed difference, and the reliable mean within
@@ -523,7 +571,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       const double rdl = r1 / n, rmu2 = r2 / n - rdl * rdl;
       const double wc = (double)p.win_cancel;
       const bool good = r2 > 0.0 && a2 <= wc * r2 && a4 <= wc * r4 && rdl * rdl <= 4.0 * rmu2;
-      if (CONS) {
+      if constexpr (LDSO) {
+        o_lds[col] = cons_v;
+        o_lds[3 * D + col] = c1c;
+      } else if (CONS) {
         p.consensus[ob + col] = cons_v;
         if (MODE == 0 && p.c1_out) p.c1_out[ob + col] = c1c;   // (no revert after the pre-check)
       }
@@ -531,7 +582,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
         double dl;
         float sk, ku;
         const bool nz = moments_from_sums_d(n, r1, r2, r3, r4, dl, sk, ku);
-        if (CONS) {
+        if constexpr (LDSO) {
+          o_lds[D + col] = p.legacy ? 0.f : sk;
+          o_lds[2 * D + col] = p.legacy ? 0.f : ku;
+        } else if (CONS) {
           p.skew[ob + col] = p.legacy ? 0.f : sk;
           p.kurt[ob + col] = p.legacy ? 0.f : ku;
         } else {
@@ -540,22 +594,44 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
           stage_out(ws, STG, Dc, 2, col, p.legacy ? 0.f : ku);
           zv |= !nz;
         }
+      } else if constexpr (LDSO) {
+        atomicOr(&redo[col >> 5], 1u << (col & 31));   // exact recomputation below
       } else {
         // exact recomputation over the reliable rows below (each column listed once)
         const int k = atomicAdd(&misc_i[2], 1);
         bstore(ws, (uint32_t)col, k * 4, LST);
       }
     }
+  };
+  if (ldso) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): no store in flight into the load-only loop
+    PBWords cur;
+    pb_load(wave * 64, cur);
+#pragma nounroll
+    for (int base = wave * 64; base < D; base += WAVES * 64) {
+      PBWords nxt;
+      if (base + WAVES * 64 < D) pb_load(base + WAVES * 64, nxt);   // uniform
+      // compiler barrier: the next column's loads are issued here, not sunk to their first use after the
+      // compute (the scheduler moves loads down to shorten live ranges)
+      asm volatile("" ::: "memory");
+      pb_col(std::true_type{}, base, cur);
+      cur = nxt;
+    }
+  } else {
+#pragma nounroll
+    for (int base = wave * 64; base < D; base += WAVES * 64) {
+      PBWords cur;
+      pb_load(base, cur);
+      pb_col(std::false_type{}, base, cur);
+    }
   }
+  if constexpr (SVOC_WINF_PROBE == 3) stamp[4] = __builtin_amdgcn_s_memrealtime();
   if (!CONS && zv && !p.legacy) misc_i[1] = 1;
   __syncthreads();
   // cleanup: one wave per listed column, lanes stride the rows, two-pass wave reductions
   // (math.cairo:320-363): the reliable mean first, then the power sums about it (no cancellation)
-  const int nredo = misc_i[2];
-  if (nredo) {
-    for (int k = wave; k < nredo; k += WAVES) {
-      // (sc0: read through the vL1D -- the entry was written by another wave of this workgroup)
-      const int col = (int)__builtin_amdgcn_readfirstlane(__builtin_amdgcn_raw_buffer_load_b32(ws, 0, LST + k * 4, 1));
+  // (ldso: the columns of the LDS bit mask in index order, dealt round-robin to the waves)
+  auto cleanup_col = [&](int col) __attribute__((always_inline)) {
       const float cc = p.c1[ob + col];
       const float* xc = inst + col;
       float y[NSEG];
@@ -592,7 +668,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
         double dl;
         float sk, ku;
         const bool nz = moments_from_sums_d(n, c1s, t2, t3, t4, dl, sk, ku);
-        if (CONS) {
+        if (CONS && ldso) {
+          o_lds[D + col] = p.legacy ? 0.f : sk;
+          o_lds[2 * D + col] = p.legacy ? 0.f : ku;
+        } else if (CONS) {
           p.skew[ob + col] = p.legacy ? 0.f : sk;
           p.kurt[ob + col] = p.legacy ? 0.f : ku;
         } else {
@@ -602,8 +681,46 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
           if (!nz && !p.legacy) misc_i[1] = 1;
         }
       }
+  };
+  if (ldso) {
+    int k = 0;
+    for (int w32 = 0; w32 < (D + 31) / 32; ++w32) {
+      uint32_t bits = redo[w32];   // uniform
+      while (bits) {
+        const int c = __builtin_ctz(bits);
+        bits &= bits - 1;
+        if (k % WAVES == wave) cleanup_col(w32 * 32 + c);
+        ++k;
+      }
     }
     __syncthreads();
+    // staged outputs -> global (16-B vectors when the rows allow it)
+    const bool c1o = MODE == 0 && p.c1_out;
+    if ((D & 3) == 0) {
+      for (int i = tid; i < D / 4; i += NT) {
+        const float4* o4 = reinterpret_cast<const float4*>(o_lds);
+        reinterpret_cast<float4*>(p.consensus + ob)[i] = o4[i];
+        reinterpret_cast<float4*>(p.skew + ob)[i] = o4[D / 4 + i];
+        reinterpret_cast<float4*>(p.kurt + ob)[i] = o4[2 * (D / 4) + i];
+        if (c1o) reinterpret_cast<float4*>(p.c1_out + ob)[i] = o4[3 * (D / 4) + i];
+      }
+    } else {
+      for (int i = tid; i < D; i += NT) {
+        p.consensus[ob + i] = o_lds[i];
+        p.skew[ob + i] = o_lds[D + i];
+        p.kurt[ob + i] = o_lds[2 * D + i];
+        if (c1o) p.c1_out[ob + i] = o_lds[3 * D + i];
+      }
+    }
+  } else {
+    const int nredo = misc_i[2];
+    if (nredo) {
+      for (int k = wave; k < nredo; k += WAVES) {
+        // (sc0: read through the vL1D -- the entry was written by another wave of this workgroup)
+        cleanup_col((int)__builtin_amdgcn_readfirstlane(__builtin_amdgcn_raw_buffer_load_b32(ws, 0, LST + k * 4, 1)));
+      }
+      __syncthreads();
+    }
   }
   // ------------------------------------------------------------ commit
   // (constrained: written in place -- the pre-check ruled out every revert; unconstrained: copied from
@@ -620,6 +737,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
       p.qr[(int64_t)b * N + t] = qr_lds[t];
     }
+  }
+  if constexpr (SVOC_WINF_PROBE == 3) {
+    __syncthreads();
+    stamp[5] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0)
+      for (int k = 1; k < 6; ++k) p.skew[(int64_t)b * D + k] = (float)(stamp[k] - stamp[0]);
   }
   if (tid == 0) {
     p.rel[2 * (int64_t)b] = misc_f[0];
