@@ -9,7 +9,7 @@
 #include "svoc/ops.hpp"
 
 extern "C" int svoc_add_layernorm_bf16(const void* x, const void* y, const void* w, const void* b, void* out,
-                                       int64_t rows, int H, float eps, hipStream_t stream);
+                                       int64_t rows, int H, float eps, int64_t y_stride, hipStream_t stream);
 extern "C" int svoc_embed_layernorm_bf16(const int64_t* ids, const int64_t* pos_ids, const void* tok, const void* pos,
                                          const void* typ, const void* w, const void* b, void* out, int64_t rows, int H,
                                          float eps, hipStream_t stream);
@@ -33,8 +33,9 @@ bool hip_supported(int64_t H) { return H == 256 || H == 512 || H == 768 || H == 
 
 at::Tensor add_layernorm_hip(const at::Tensor& x, const at::Tensor& y, const at::Tensor& w, const at::Tensor& b,
                              double eps) {
-  TORCH_CHECK(x.sizes() == y.sizes(), "add_layernorm: x and y shapes differ");
   const int64_t H = x.size(-1);
+  const bool y_row = y.dim() == 1 && y.numel() == H;   // one [H] row broadcast over x's rows
+  TORCH_CHECK(y_row || x.sizes() == y.sizes(), "add_layernorm: y must have x's shape or be one [H] row");
   TORCH_CHECK(w.numel() == H && b.numel() == H, "add_layernorm: weight/bias must have H elements");
   const bool fast = x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 &&
                     w.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && hip_supported(H);
@@ -42,7 +43,7 @@ at::Tensor add_layernorm_hip(const at::Tensor& x, const at::Tensor& y, const at:
   auto xc = x.contiguous(), yc = y.contiguous(), wc = w.contiguous(), bc = b.contiguous();
   auto out = at::empty_like(xc);
   const int rc = svoc_add_layernorm_bf16(xc.data_ptr(), yc.data_ptr(), wc.data_ptr(), bc.data_ptr(), out.data_ptr(),
-                                         xc.numel() / H, (int)H, (float)eps,
+                                         xc.numel() / H, (int)H, (float)eps, y_row ? 0 : H,
                                          c10::hip::getCurrentHIPStream(x.device().index()).stream());
   TORCH_CHECK(rc == 0, "svoc_add_layernorm_bf16 failed: ", rc);
   return out;

@@ -28,14 +28,15 @@ __global__ __launch_bounds__(256) void add_layernorm_kernel(const uint16_t* __re
                                                             const uint16_t* __restrict__ y,
                                                             const uint16_t* __restrict__ w,
                                                             const uint16_t* __restrict__ bias,
-                                                            uint16_t* __restrict__ out, int64_t rows, float eps) {
+                                                            uint16_t* __restrict__ out, int64_t rows, float eps,
+                                                            int64_t y_stride) {
   constexpr int H = 64 * EPL;
   constexpr int V = EPL / 4;  // 8-byte vectors per lane
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const uint2* xr = (const uint2*)(x + row * H);
-  const uint2* yr = (const uint2*)(y + row * H);
+  const uint2* yr = (const uint2*)(y + row * y_stride);  // y_stride 0: one [H] row for all
   float v[EPL];
   float s = 0.f;
 #pragma unroll
@@ -196,8 +197,10 @@ __global__ __launch_bounds__(256) void segment_mean_kernel(const uint16_t* __res
 }  // namespace svoc
 
 // Returns 0 on success, -1 if the hidden size is not supported (caller falls back to ATen).
+// y_stride: H (y is [rows, H]) or 0 (y is one [H] row added to every row, e.g. a GEMM bias when the
+// residual was accumulated into the GEMM output).
 extern "C" int svoc_add_layernorm_bf16(const void* x, const void* y, const void* w, const void* b, void* out,
-                                       int64_t rows, int H, float eps, hipStream_t stream) {
+                                       int64_t rows, int H, float eps, int64_t y_stride, hipStream_t stream) {
   if (rows <= 0) return 0;
   const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
   const auto* X = (const uint16_t*)x;
@@ -206,10 +209,10 @@ extern "C" int svoc_add_layernorm_bf16(const void* x, const void* y, const void*
   const auto* B = (const uint16_t*)b;
   auto* O = (uint16_t*)out;
   switch (H) {
-    case 256: hipLaunchKernelGGL(add_layernorm_kernel<4>, grid, block, 0, stream, X, Y, W, B, O, rows, eps); break;
-    case 512: hipLaunchKernelGGL(add_layernorm_kernel<8>, grid, block, 0, stream, X, Y, W, B, O, rows, eps); break;
-    case 768: hipLaunchKernelGGL(add_layernorm_kernel<12>, grid, block, 0, stream, X, Y, W, B, O, rows, eps); break;
-    case 1024: hipLaunchKernelGGL(add_layernorm_kernel<16>, grid, block, 0, stream, X, Y, W, B, O, rows, eps); break;
+    case 256: hipLaunchKernelGGL(add_layernorm_kernel<4>, grid, block, 0, stream, X, Y, W, B, O, rows, eps, y_stride); break;
+    case 512: hipLaunchKernelGGL(add_layernorm_kernel<8>, grid, block, 0, stream, X, Y, W, B, O, rows, eps, y_stride); break;
+    case 768: hipLaunchKernelGGL(add_layernorm_kernel<12>, grid, block, 0, stream, X, Y, W, B, O, rows, eps, y_stride); break;
+    case 1024: hipLaunchKernelGGL(add_layernorm_kernel<16>, grid, block, 0, stream, X, Y, W, B, O, rows, eps, y_stride); break;
     default: return -1;
   }
   return (int)hipGetLastError();

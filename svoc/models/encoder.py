@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import dataclasses
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -79,8 +80,8 @@ class Layer(nn.Module):
         """x: [T, H] real tokens only (sequence b = rows [cu[b], cu[b+1]))."""
         from .. import ops as svops
         a = svops.ops().attention_varlen(self.qkv(x), plan.cu, plan.max_len, self.heads)
-        x = _add_ln(x, self.out(a), self.ln1)
-        return _add_ln(x, self.fc2(_linear_gelu(x, self.fc1)), self.ln2)
+        x = _res_linear_ln(x, a, self.out, self.ln1)
+        return _res_linear_ln(x, _linear_gelu(x, self.fc1), self.fc2, self.ln2)
 
 
 @dataclasses.dataclass
@@ -104,6 +105,21 @@ def _linear_gelu(x: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
         y = torch._addmm_activation(fc.bias, x.reshape(-1, x.shape[-1]), fc.weight.t(), use_gelu=True)
         return y.view(*x.shape[:-1], -1)
     return F.gelu(fc(x))
+
+
+# residual accumulated into the out-projection / FC2 GEMMs (A/B switch, docs/PERF.md "Encoder (c4)")
+_RESGEMM = os.environ.get("SVOC_ENC_RESGEMM", "0") == "1"
+
+
+def _res_linear_ln(x: torch.Tensor, inp: torch.Tensor, fc: nn.Linear, ln: nn.LayerNorm) -> torch.Tensor:
+    """LayerNorm(x + fc(inp)) for the packed path, which owns x (it is consumed here).  On the GPU
+    (inference) the residual is accumulated into the GEMM in place (x += inp @ W^T, beta = 1: the GEMM
+    reads x in its epilogue) and the LayerNorm kernel adds the bias as one broadcast [H] row, so it
+    reads one [T, H] operand instead of two."""
+    if _RESGEMM and x.is_cuda and not torch.is_grad_enabled() and x.is_contiguous():
+        x.view(-1, x.shape[-1]).addmm_(inp.reshape(-1, inp.shape[-1]), fc.weight.t())
+        return _add_ln(x, fc.bias, ln)
+    return _add_ln(x, fc(inp), ln)
 
 
 def _add_ln(x: torch.Tensor, y: torch.Tensor, ln: nn.LayerNorm) -> torch.Tensor:

@@ -23,6 +23,36 @@ def test_add_layernorm_bf16(rows, H):
     assert (out.float() - ref.to(torch.bfloat16).float()).abs().max().item() <= 0.0625
 
 
+@pytest.mark.parametrize("H", [768, 256])
+def test_add_layernorm_broadcast_row(H):
+    """y as one [H] row (the GEMM bias when the residual was accumulated into the GEMM output)."""
+    g = torch.Generator(device="cuda").manual_seed(H)
+    x = torch.randn(333, H, device="cuda", generator=g).to(torch.bfloat16)
+    y = (0.3 * torch.randn(H, device="cuda", generator=g)).to(torch.bfloat16)
+    w = (1 + 0.1 * torch.randn(H, device="cuda", generator=g)).to(torch.bfloat16)
+    b = (0.1 * torch.randn(H, device="cuda", generator=g)).to(torch.bfloat16)
+    out = svops.ops().add_layernorm(x, y, w, b, 1e-5)
+    ref = F.layer_norm(x.float() + y.float()[None], (H,), w.float(), b.float(), 1e-5)
+    assert (out.float() - ref.to(torch.bfloat16).float()).abs().max().item() <= 0.0625
+
+
+def test_encoder_residual_gemm_matches_default(monkeypatch):
+    """Packed path with the residual accumulated into the out-projection / FC2 GEMMs (x += inp @ W^T,
+    bias added by the LayerNorm kernel) vs the default (GEMM + bias, then add + LayerNorm)."""
+    from svoc.models import encoder as E
+    cfg = E.EncoderConfig(vocab_size=500, hidden=768, layers=2, heads=12, ffn=3072, max_positions=130)
+    enc = E.build("cuda", torch.bfloat16, seed=5, cfg=cfg)
+    g = torch.Generator().manual_seed(3)
+    ids = torch.randint(3, 500, (7, 128), generator=g).cuda()
+    mask = (torch.arange(128)[None] < torch.tensor([128, 40, 77, 1, 9, 100, 64])[:, None]).to(torch.int64).cuda()
+    with torch.no_grad():
+        monkeypatch.setattr(E, "_RESGEMM", False)
+        a = enc(ids, mask)
+        monkeypatch.setattr(E, "_RESGEMM", True)
+        b = enc(ids, mask)
+    torch.testing.assert_close(a, b, rtol=0, atol=0.03)
+
+
 def test_add_layernorm_3d_and_fallback_width():
     x = torch.randn(2, 7, 64, device="cuda", dtype=torch.bfloat16)
     y = torch.randn(2, 7, 64, device="cuda", dtype=torch.bfloat16)
