@@ -4,7 +4,7 @@
 set -u
 mkdir -p gpurun_out
 bash tools/gpu_quick3.sh || exit 1
-bash tools/gpu_resgemm_ab.sh || exit 1
+bash tools/gpu_c4_ab.sh || exit 1
 bash tools/gpu_exact_stream.sh || exit 1
 timeout -k 10 200 python -u tools/probe_gemm_shapes.py > gpurun_out/gemm_shapes.log 2>&1 || { tail -5 gpurun_out/gemm_shapes.log; exit 1; }
 cat gpurun_out/gemm_shapes.log

@@ -43,6 +43,6 @@ for spec in "c3:--storage fp32" "c2:--storage bf16" "c4:"; do   # one storage pe
       -d $R/gpurun_out/prof_$cfg -o run -- python3 $R/bench.py --config $cfg --steps 6 --warmup 1 --graph 0 $extra \
       > $R/gpurun_out/prof_$cfg.log 2>&1) || exit 1
 done
-# last: 64 exact transactions per instance per step (a 64-instance batch keeps it short)
-run c3_exact_stream 150 --config-file configs/c3_exact_stream.yaml --batch 64 --steps 2 --warmup 1 || exit 1
+# last: 64 exact transactions per instance per step at the YAML batch (1024 instances)
+run c3_exact_stream 150 --config-file configs/c3_exact_stream.yaml --steps 2 --warmup 1 || exit 1
 echo "=== done"

@@ -34,7 +34,7 @@ ROWS = [
     ("c5_exact", "c5 shape (7 × 6), exact wsad, 1M instances", "939/s exact Python emulator"),
     ("c5_exact_stream", "c5 shape, exact transactional update stream (store + round + revert per update)",
      "939/s exact Python emulator"),
-    ("c3_exact_stream", "c3 shape, exact transactional update stream, 64 instances × 64 transactions/step",
+    ("c3_exact_stream", "c3 shape, exact transactional update stream, 1024 instances × 64 transactions/step",
      "0.61/s exact Python emulator (64 × 1024)"),
     ("wide512", "512 oracles × 2048 dims, 1024 instances (N > 256)", "—"),
     ("wide512_fp32", "512 × 2048, fast mode over fp32 storage", "—"),
