@@ -16,7 +16,6 @@ from __future__ import annotations
 
 import dataclasses
 import math
-import os
 from typing import List, Optional
 
 import torch
@@ -71,7 +70,7 @@ class Layer(nn.Module):
         from .. import ops as svops
         # attention straight from the fused QKV projection [B, S, 3, heads, 64] into [B, S, H]
         # (MFMA kernel for S <= 128 on the GPU, encoder_ops.hip; ATen otherwise)
-        a = svops.ops().attention_qkv(_qkv(x, self.qkv), key_mask, self.heads)
+        a = svops.ops().attention_qkv(self.qkv(x), key_mask, self.heads)
         # post-LN (BERT/RoBERTa): residual add + LayerNorm fused in one HIP kernel (encoder_ops.hip)
         x = _add_ln(x, self.out(a), self.ln1)
         return _add_ln(x, self.fc2(_linear_gelu(x, self.fc1)), self.ln2)
@@ -79,7 +78,7 @@ class Layer(nn.Module):
     def forward_packed(self, x: torch.Tensor, plan: "PackPlan") -> torch.Tensor:
         """x: [T, H] real tokens only (sequence b = rows [cu[b], cu[b+1]))."""
         from .. import ops as svops
-        a = svops.ops().attention_varlen(_qkv(x, self.qkv), plan.cu, plan.max_len, self.heads)
+        a = svops.ops().attention_varlen(self.qkv(x), plan.cu, plan.max_len, self.heads)
         x = _add_ln(x, self.out(a), self.ln1)
         return _add_ln(x, self.fc2(_linear_gelu(x, self.fc1)), self.ln2)
 
@@ -105,24 +104,6 @@ def _linear_gelu(x: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
         y = torch._addmm_activation(fc.bias, x.reshape(-1, x.shape[-1]), fc.weight.t(), use_gelu=True)
         return y.view(*x.shape[:-1], -1)
     return F.gelu(fc(x))
-
-
-# QKV projection on rocBLAS (A/B switch, docs/PERF.md "Encoder (c4)")
-_QKV_ROCBLAS = os.environ.get("SVOC_ENC_QKV_ROCBLAS", "0") == "1"
-
-
-def _qkv(x: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
-    """The fused QKV projection.  At K = 768, N = 2304 rocBLAS's kernel measured 0.81 ms vs hipBLASLt's
-    heuristic pick 0.96 ms on 245,760 tokens (tools/probe_gemm_shapes.py); the other three encoder GEMMs
-    are equal under both libraries, so only this call switches (host-side library selection)."""
-    if _QKV_ROCBLAS and x.is_cuda:
-        prev = torch.backends.cuda.preferred_blas_library()
-        torch.backends.cuda.preferred_blas_library("cublas")   # = rocBLAS on ROCm
-        try:
-            return fc(x)
-        finally:
-            torch.backends.cuda.preferred_blas_library(prev)
-    return fc(x)
 
 
 def _add_ln(x: torch.Tensor, y: torch.Tensor, ln: nn.LayerNorm) -> torch.Tensor:

@@ -36,24 +36,6 @@ def test_add_layernorm_broadcast_row(H):
     assert (out.float() - ref.to(torch.bfloat16).float()).abs().max().item() <= 0.0625
 
 
-def test_encoder_qkv_rocblas_matches_default(monkeypatch):
-    """QKV projection on rocBLAS vs the default library: same encoder scores."""
-    from svoc.models import encoder as E
-    cfg = E.EncoderConfig(vocab_size=500, hidden=768, layers=2, heads=12, ffn=3072, max_positions=130)
-    enc = E.build("cuda", torch.bfloat16, seed=5, cfg=cfg)
-    g = torch.Generator().manual_seed(3)
-    ids = torch.randint(3, 500, (7, 128), generator=g).cuda()
-    mask = (torch.arange(128)[None] < torch.tensor([128, 40, 77, 1, 9, 100, 64])[:, None]).to(torch.int64).cuda()
-    lib = torch.backends.cuda.preferred_blas_library()
-    with torch.no_grad():
-        monkeypatch.setattr(E, "_QKV_ROCBLAS", False)
-        a = enc(ids, mask)
-        monkeypatch.setattr(E, "_QKV_ROCBLAS", True)
-        b = enc(ids, mask)
-    torch.testing.assert_close(a, b, rtol=0, atol=0.03)
-    assert torch.backends.cuda.preferred_blas_library() == lib    # the switch is scoped to the QKV call
-
-
 def test_add_layernorm_3d_and_fallback_width():
     x = torch.randn(2, 7, 64, device="cuda", dtype=torch.bfloat16)
     y = torch.randn(2, 7, 64, device="cuda", dtype=torch.bfloat16)
