@@ -143,7 +143,6 @@ def measure(args, c, storage, dev, rank, world, dshard):
     if dshard or mode != "fast" or dev.type != "cuda":
         pipeline = 1
     extra["pipeline_chunks"] = pipeline
-    extra["pipeline_overlap"] = bool(args.overlap) and pipeline > 1
 
     def run_round():
         if dshard:
@@ -215,6 +214,9 @@ def measure(args, c, storage, dev, rank, world, dshard):
                 print(f"[bench] graph capture failed ({e}); running eager", file=sys.stderr)
             graph = None
 
+    # cross-step overlap happens only under graph replay: eager steps reduce the metrics every step, and
+    # that joins the pipeline streams (engine.pipeline_join)
+    extra["pipeline_overlap"] = bool(args.overlap) and pipeline > 1 and graph is not None
     fx0 = eng.metrics_fx.clone()   # this rank's round outcome counters before the timed steps
     if world > 1:
         dist.barrier()

@@ -123,19 +123,6 @@ void apply_updates_hip(at::Tensor values, at::Tensor enabled, at::Tensor n_activ
   TORCH_CHECK(rc == 0, "svoc_apply_updates failed: ", rc);
 }
 
-// quadratic-risk probe (csrc/kernels/qr_probe.hip): VALU vs MFMA formulation of the qr pass
-void qr_probe_hip(const at::Tensor& values, const at::Tensor& c1, at::Tensor qr, int64_t variant) {
-  TORCH_CHECK(values.dim() == 3 && values.scalar_type() == at::kBFloat16 && values.is_contiguous(),
-              "values: contiguous bf16 [B, N, ld]");
-  const int64_t B = values.size(0), N = values.size(1), ld = values.size(2), D = c1.size(1);
-  TORCH_CHECK(c1.scalar_type() == at::kFloat && c1.is_contiguous() && c1.size(0) == B, "c1: fp32 [B, D]");
-  TORCH_CHECK(qr.scalar_type() == at::kFloat && qr.is_contiguous() && qr.numel() == B * N, "qr: fp32 [B, N]");
-  auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
-  const int rc = svoc_qr_probe((const uint16_t*)values.data_ptr(), c1.data_ptr<float>(), qr.data_ptr<float>(),
-                               (int)B, (int)N, (int)D, (int)ld, (int)variant, stream);
-  TORCH_CHECK(rc == 0, "svoc_qr_probe failed: ", rc);
-}
-
 }  // namespace
 
 void register_extra_defs(torch::Library& m) {
@@ -147,7 +134,6 @@ void register_extra_defs(torch::Library& m) {
   register_io_defs(m);
   register_bookkeeping_defs(m);
   register_encoder_defs(m);
-  m.def("qr_probe(Tensor values, Tensor c1, Tensor(a!) qr, int variant) -> ()");
 }
 
 void register_extra_cpu(torch::Library& m) {
@@ -160,7 +146,6 @@ void register_extra_cpu(torch::Library& m) {
 
 void register_extra_hip(torch::Library& m) {
   m.impl("apply_updates", &apply_updates_hip);
-  m.impl("qr_probe", &qr_probe_hip);
   register_governance_hip(m);
   register_generator_hip(m);
   register_bookkeeping_hip(m);

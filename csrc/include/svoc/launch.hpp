@@ -138,5 +138,3 @@ extern "C" int svoc_apply_updates(const svoc::UpdateParams* p, hipStream_t strea
 extern "C" int svoc_commit_rows(const void* src, void* dst, const int32_t* status, const uint8_t* active, int64_t B,
                                 int64_t words, hipStream_t stream);
 
-extern "C" int svoc_qr_probe(const uint16_t* X, const float* C, float* qr, int B, int N, int D, int ld, int variant,
-                             hipStream_t stream);

@@ -38,13 +38,6 @@
 #include "svoc/sortnet.hpp"
 #include "svoc/status.hpp"
 
-// Diagnostic builds only (SVOC_HIPCC_FLAGS=-DSVOC_WINF_PROBE=n, tools/winf_probe.py; wrong results):
-// 1 = phase A without the window network, 2 = phase A without the HBM stream (no DMA, stale LDS),
-// 3 = the full kernel, workgroup phase end times (s_memrealtime ticks since its start) in skew[b, 0..5].
-#ifndef SVOC_WINF_PROBE
-#define SVOC_WINF_PROBE 0
-#endif
-
 namespace svoc {
 
 // Constrained keys: values validated to [0, 1] (sign bit clear, or -0.0: key 0, just below +0.0) ->
@@ -169,8 +162,6 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
 
   const int b = blockIdx.x;
   if (p.active && !p.active[b]) return;
-  uint64_t stamp[6] = {0, 0, 0, 0, 0, 0};
-  if constexpr (SVOC_WINF_PROBE == 3) stamp[0] = __builtin_amdgcn_s_memrealtime();
   // (wave made explicitly uniform: it feeds the DMA's M0 and SGPR row offsets)
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid < 32) urow[tid] = 0;  // f < 32: unused slots still name a valid row
@@ -213,7 +204,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
   uint32_t* const region = slab + (PASS1 ? wave * 64 * 64 : 0);
   // this lane's words: global row seg * 64 + i at LDS row NSEG * i + seg, i.e. word 64 i + seg P + cw
   const uint32_t* const mine = region + (PASS1 ? seg * P + cw : 0);
-  if (pass1_slabs > 0 && SVOC_WINF_PROBE != 2) dma.issue(rsd, region, rowb, wave * P);
+  if (pass1_slabs > 0) dma.issue(rsd, region, rowb, wave * P);
   // One slab of phase A.  FULL: every column of the slab is < D and N = NPAD, so no masks at all; the
   // masked form serves the tail slab and padded N.  (One body per loop: reading the raw rows in two
   // branches of one loop makes the compiler demote them to scratch.)
@@ -233,7 +224,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       xs.hi[i] = mine[(i + 32) * 64];
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0): the region is read, the next slab may land
-    if (s + 1 < pass1_slabs && SVOC_WINF_PROBE != 2) dma.issue(rsd, region, rowb, (s + 1) * W + wave * P);
+    if (s + 1 < pass1_slabs) dma.issue(rsd, region, rowb, (s + 1) * W + wave * P);
     {
       uint32_t r[64];
       if (FULL || N == NPAD) {
@@ -251,14 +242,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       uint32_t klo, khi;
       if constexpr (CONS) {
         uint32_t wk[NSEG == 1 ? 2 * H : H];
-        if constexpr (SVOC_WINF_PROBE == 1) {
-#pragma unroll
-          for (int m = 0; m < (NSEG == 1 ? 2 * H : H); ++m) wk[m] = r[m];
-          klo = r[31];
-          khi = r[32];
-        } else {
-          window_group<NSEG, P, H>(r, seg, lane, wk, klo, khi);
-        }
+        window_group<NSEG, P, H>(r, seg, lane, wk, klo, khi);
         if constexpr (NSEG == 1) {
 #pragma unroll
           for (int m = 0; m < H; ++m) {
@@ -312,7 +296,6 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     for (int s = nfull; s < pass1_slabs; ++s) slab_body(std::false_type{}, s);
   }
 
-  if constexpr (SVOC_WINF_PROBE == 3) stamp[1] = __builtin_amdgcn_s_memrealtime();
   // ------------------------------------------------------------ qr reduction
   {
     if constexpr (ACC64) qr_keep<P>(acc, lane, keep, false);
@@ -418,7 +401,6 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     return;
   }
 
-  if constexpr (SVOC_WINF_PROBE == 3) stamp[2] = __builtin_amdgcn_s_memrealtime();
   // ------------------------------------------------------------ zero-variance pre-check (constrained)
   // A reliable column of zero variance reverts the round (math.cairo:322,331; contract.cairo:588-603).
   // The R equal values would form a sorted run covering positions [f, N - f - 1]; when f + H <= N/2 that
@@ -463,7 +445,6 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     }
   }
 
-  if constexpr (SVOC_WINF_PROBE == 3) stamp[3] = __builtin_amdgcn_s_memrealtime();
   // ------------------------------------------------------------ phase B: pass 2 (contract.cairo:476-500)
   // one lane per column: the removed keys are sorted once and ranked against the window.
   // Constrained rounds with D <= 4096 (LDSO): the outputs are staged in the idle slab region and the
@@ -625,7 +606,6 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       pb_col(std::false_type{}, base, cur);
     }
   }
-  if constexpr (SVOC_WINF_PROBE == 3) stamp[4] = __builtin_amdgcn_s_memrealtime();
   if (!CONS && zv && !p.legacy) misc_i[1] = 1;
   __syncthreads();
   // cleanup: one wave per listed column, lanes stride the rows, two-pass wave reductions
@@ -737,12 +717,6 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       p.reliable[(int64_t)b * N + t] = (relmask[t >> 6] >> (t & 63)) & 1;
       p.qr[(int64_t)b * N + t] = qr_lds[t];
     }
-  }
-  if constexpr (SVOC_WINF_PROBE == 3) {
-    __syncthreads();
-    stamp[5] = __builtin_amdgcn_s_memrealtime();
-    if (tid == 0)
-      for (int k = 1; k < 6; ++k) p.skew[(int64_t)b * D + k] = (float)(stamp[k] - stamp[0]);
   }
   if (tid == 0) {
     p.rel[2 * (int64_t)b] = misc_f[0];

@@ -131,7 +131,9 @@ class ConsensusEngine:
         inst = torch.as_tensor(inst, dtype=torch.int64, device=self.device).contiguous()
         oracle = torch.as_tensor(oracle, dtype=torch.int64, device=self.device).contiguous()
         if not _joined:
-            self.pipeline_join()
+            # (streams only: a pending D-shard round's commit writes outputs, not the stored rows, and
+            # its pass 2 has already read them -- updates may land before it)
+            self._join_streams()
         vals = self._as_storage(torch.as_tensor(vals))
         if vals.dim() != 2 or vals.shape[1] != self.D:
             raise ValueError(f"predictions must be [U, {self.D}]")
@@ -226,6 +228,12 @@ class ConsensusEngine:
             for k, (b0, b1) in enumerate(ranges):
                 with torch.cuda.stream(sc[k]):
                     self._run_round_range(b0, b1)
+            # the side streams still read the caller's batch after this returns: hold it until the join
+            # (after which the current stream is ordered behind every read, so the caching allocator may
+            # hand its blocks out again)
+            held = getattr(self, "_pipe_held", None) or []
+            held.append((inst, oracle, vals))
+            self._pipe_held = held
             self.rounds += 1
             self._pipe_open = True
             return
@@ -242,12 +250,23 @@ class ConsensusEngine:
             cur.wait_stream(s)
 
     def pipeline_join(self) -> None:
-        """Join the streams of an open (``overlap=True``) pipelined step into the current stream."""
+        """Join the streams of an open (``overlap=True``) pipelined step into the current stream, and
+        commit a deferred D-sharded round (svoc.parallel.dshard, ``defer=True``): every reader of the
+        state (getters, metrics, checkpoints, the next update) goes through here.  With a D-shard round
+        pending this is a collective (one status all-reduce): every rank of the shard group must read."""
+        self._join_streams()
+        if getattr(self, "_dshard_pending", None) is not None:
+            from .parallel.dshard import flush_sharded
+            group, world = self._dshard_ctx
+            flush_sharded(self, group=group, world=world)
+
+    def _join_streams(self) -> None:
         if getattr(self, "_pipe_open", False):
             cur = torch.cuda.current_stream(self.device)
             for s in self._pipe_streams:
                 cur.wait_stream(s)
             self._pipe_open = False
+            self._pipe_held = None
 
     def work(self) -> Optional[torch.Tensor]:
         """Workspace of the one-network window kernel (34 window keys + 8 power sums + 2 cleanup
@@ -325,6 +344,16 @@ class ConsensusEngine:
         if K:
             if U % K:
                 raise ValueError("_exact_transactions: updates_per_instance must divide the batch")
+            if U > self.B * K:
+                raise ValueError("_exact_transactions: more than updates_per_instance updates per instance")
+            capturing = self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
+            if not capturing:
+                # outside graph capture the b * K + k layout is checked (one host sync); a batch that does
+                # not follow it (an instance twice in a wave) takes the general device-side grouping
+                okl = (inst >= 0) & (inst < self.B) & (oracle >= 0) & (oracle < self.N)
+                lay = inst == torch.arange(U, device=self.device) // K
+                if not bool((lay | ~okl).all()):
+                    K = 0
             waves = [torch.arange(k, U, K, device=self.device) for k in range(K)]
         else:
             order, bounds = self._transaction_waves(inst, oracle)

@@ -137,6 +137,7 @@ def run_round_sharded(engine, d_global: int, group=None, world: int = 1, defer: 
     if defer and world > 1:
         # (active, local pass-2 status, global qr, c1): pass 1 of the next round rewrites the qr / c1 shadows
         e._dshard_pending = (e._active.clone(), e.status.clone(), sh.qr.clone(), sh.c1.clone())
+        e._dshard_ctx = (group, world)   # engine.pipeline_join (every state reader) commits it
         e.touched.zero_()
         e.rounds += 1
         return

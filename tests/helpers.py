@@ -46,7 +46,10 @@ def run_exact(values, n_failing, constrained, max_spread=0, active=None, legacy=
 def beta_oracles(B, N, D, f, a=20.0, seed=0, device="cpu", dtype=torch.bfloat16, ld=None):
     """Honest oracles ~ Beta(a, a) per component, f failing ~ U(0,1), shuffled (notebook cell 3)."""
     g = torch.Generator().manual_seed(seed)
-    honest = torch.distributions.Beta(torch.tensor(a), torch.tensor(a)).sample((B, N, D))
+    # Beta(a, a) as Ga / (Ga + Gb), both gamma draws from g: a parametrisation is reproducible alone
+    ga = torch._standard_gamma(torch.full((B, N, D), float(a)), generator=g)
+    gb = torch._standard_gamma(torch.full((B, N, D), float(a)), generator=g)
+    honest = ga / (ga + gb)
     fail = torch.rand(B, N, D, generator=g)
     is_fail = torch.zeros(B, N, dtype=torch.bool)
     for b in range(B):

@@ -174,7 +174,8 @@ def _ds_defer_worker(rank, world, port, outdir, xs, cfgd, mode):
     cfg = ConsensusConfig(**cfgd)
     lo, hi = dshard.shard_bounds(cfg.dimension, rank, world)
     lcfg = ConsensusConfig(**{**cfgd, "dimension": hi - lo})
-    engines = [ConsensusEngine(lcfg, xs[0].shape[0], device="cpu", mode=mode) for _ in range(2)]
+    # 0: eager commits; 1: deferred, flushed explicitly; 2: deferred, committed by a state reader (getter)
+    engines = [ConsensusEngine(lcfg, xs[0].shape[0], device="cpu", mode=mode) for _ in range(3)]
     calls = []
     real = dist.all_reduce
 
@@ -189,10 +190,14 @@ def _ds_defer_worker(rank, world, port, outdir, xs, cfgd, mode):
             for x in xs:
                 e.values[:, :, : hi - lo] = x[:, :, lo:hi]
                 e.enabled.fill_(1); e.n_active.fill_(cfg.n_oracles); e.touched.fill_(1)
-                dshard.run_round_sharded(e, cfg.dimension, world=world, defer=(j == 1))
+                dshard.run_round_sharded(e, cfg.dimension, world=world, defer=(j >= 1))
                 if j == 1:
                     calls.append("round")
-            dshard.flush_sharded(e, world=world)
+            if j == 2:
+                e.get_consensus_value()          # engine.pipeline_join commits the pending round
+                assert getattr(e, "_dshard_pending", None) is None
+            else:
+                dshard.flush_sharded(e, world=world)
         finally:
             dist.all_reduce = real
         out.append({k: getattr(e, k).clone() for k in ("consensus", "rel", "reliable", "qr", "skew", "kurt", "c1",
@@ -222,9 +227,10 @@ def test_dsharding_deferred_commit_one_collective_per_round(mode):
         mp.spawn(_ds_defer_worker, args=(world, _free_port(), d, xs, cfgd, mode), nprocs=world, join=True)
         r = [torch.load(os.path.join(d, f"dd{i}.pt"), weights_only=True) for i in range(world)]
     for s in r:
-        eager, deferred = s["out"]
+        eager, deferred, via_getter = s["out"]
         for k in eager:
             assert torch.equal(eager[k], deferred[k]), k
+            assert torch.equal(eager[k], via_getter[k]), k
         assert eager["status"].tolist()[1] == 0 and eager["status"].tolist()[3] != 0
         # one collective per round, the packed [B, N + 2 * world] buffer; the flush's status MAX last
         assert s["calls"] == [(B, N + 2 * world), "round"] * 3 + [(B,)], s["calls"]

@@ -127,27 +127,6 @@ def test_engine_exact_int32_storage_gpu():
         assert torch.equal(getattr(e32, k), getattr(e64, k)), k
 
 
-def test_qr_probe_mfma_vs_valu_precision():
-    """The MFMA formulation of the qr pass (csrc/kernels/qr_probe.hip) against fp64: within the
-    fast-mode qr tolerance on Beta data, but measurably worse than the VALU form (cancellation)."""
-    from helpers import beta_oracles as bo
-    B, N, D, f = 16, 256, 1024, 32
-    x, _ = bo(B, N, D, f, seed=3, ld=1024)
-    xg = x.to(DEV)
-    xs = xg[:, :, :D].float()
-    srt = torch.sort(xs, dim=1).values
-    c1 = (0.5 * (srt[:, N // 2 - 1] + srt[:, N // 2])).contiguous()
-    ref = ((xs.double() - c1[:, None].double()) ** 2).sum(-1)
-    err = {}
-    for v in (0, 1):
-        qr = torch.empty(B, N, dtype=torch.float32, device=DEV)
-        svops.ops().qr_probe(xg, c1, qr, v)
-        torch.cuda.synchronize()
-        err[v] = ((qr.double() - ref).abs() / ref).max().item()
-    assert err[0] < 2e-5 and err[1] < 2e-3, err
-    assert err[1] > err[0]
-
-
 @pytest.mark.parametrize("N,D,f", [(64, 1024, 8), (256, 512, 32)])
 def test_fast_bf16_agrees_with_exact_on_shared_grid(N, D, f):
     """Fast (bf16 storage, fp32 math) vs exact (wsad) on data both represent exactly (x = j / 64, i.e.

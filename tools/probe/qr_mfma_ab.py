@@ -1,4 +1,4 @@
-"""A/B of the quadratic-risk pass on the VALU vs the matrix cores (csrc/kernels/qr_probe.hip), on
+"""A/B of the quadratic-risk pass on the VALU vs the matrix cores (tools/probe/qr_probe.hip), on
 the c2 and c3 shapes: kernel time (HIP events) and precision against fp64 -- max relative error of
 qr and the number of instances whose (qr asc, idx desc) rank mask differs from the fp64 one
 (contract.cairo:345-363).
@@ -14,9 +14,11 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+sys.path.insert(0, HERE)
 
-from svoc import ops as svops  # noqa: E402
+from build import qr_probe  # noqa: E402  (tools/probe/build.py)
 from svoc.models.oracle_gen import beta_failing_oracles  # noqa: E402
 
 
@@ -51,7 +53,7 @@ def case(name, B, N, D, f, reps=20):
     ref_mask = rank_mask(ref, N - f)
     for v, vn in ((0, "valu"), (1, "mfma")):
         qr = torch.empty(B, N, dtype=torch.float32, device=dev)
-        op = svops.ops().qr_probe
+        op = qr_probe
         op(x, c1, qr, v)
         torch.cuda.synchronize()
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
