@@ -42,7 +42,7 @@ CONFIGS = {
     "c2": dict(model="svoc-consensus N=64 D=1024 batched (f=8, constrained)", N=64, D=1024, f=8,
                batch=10000, update_frac=0.0, storage="bf16", alt_storage="fp32"),
     "c4": dict(model="sentiment oracles: BERT-base (12x768, bf16) on 30-comment windows -> 7 oracles x 6 dims",
-               N=7, D=6, f=2, batch=64, update_frac=1.0, seq_len=128),
+               N=7, D=6, f=2, batch=64, update_frac=1.0, seq_len=128, alt_precision="fp32"),
     "c5": dict(model="deployed config 7 oracles x 6 dims, governance + reliability stream (1% instances vote/step)",
                N=7, D=6, f=2, batch=1 << 20, update_frac=1 / 7, gov_frac=0.01),
 }
@@ -65,13 +65,39 @@ def _launch_ranks(n: int) -> int:
     return subprocess.call(cmd)
 
 
+def _collectives_capturable(dev) -> bool:
+    """Whether an all-reduce of this process group can be captured in a HIP graph (collective: every rank
+    runs it; the verdict is agreed by a MIN all-reduce so all ranks take the same path)."""
+    ok = True
+    buf = torch.ones(16, device=dev)
+    try:
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            dist.all_reduce(buf)                  # warm the communicator on the capture stream
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            dist.all_reduce(buf)
+        g.replay()
+        torch.cuda.synchronize(dev)
+        del g
+    except Exception as e:  # capture is an optimisation; eager stays correct
+        print(f"[bench] collective capture unavailable ({e}); D-shard steps run eagerly", file=sys.stderr)
+        ok = False
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return bool(flag.item())
+
+
 def _dtype_name(mode: str, storage: str, c: dict) -> str:
     if mode == "exact":
         return f"{storage}-wsad"
     return {"fp32": "fp32", "bf16": "bf16"}.get(storage, c.get("dtype", "bf16"))
 
 
-def measure(args, c, storage, dev, rank, world, dshard):
+def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
     """Build the engine + update source for one storage dtype, warm up, time exactly args.steps steps
     (barrier + device sync on both sides) and gather every rank's time and round outcomes."""
     from svoc.config import ConsensusConfig
@@ -92,6 +118,9 @@ def measure(args, c, storage, dev, rank, world, dshard):
     mode = args.mode or c.get("mode", "fast")
     eng = ConsensusEngine(cfg, batch=B, device=dev, mode=mode, storage=storage)
     eng.wave_hint = args.wave_hint
+    if mode == "fast":
+        # transactional steps (default): a reverted round restores its instance's pre-batch rows
+        eng.transactional = bool(args.transactional)
     dp = DataParallelConsensus(eng, rank=rank, world=world)
     eng.randomize(seed=1000 + (0 if dshard else rank))
 
@@ -102,7 +131,14 @@ def measure(args, c, storage, dev, rank, world, dshard):
     if args.config == "c4":
         from svoc.models import corpus
         from svoc.models.sentiment_oracle import SentimentOraclePipeline
-        pipe = SentimentOraclePipeline(eng, seed=0)
+        enc = None
+        if enc_dtype is not None:
+            # the reference's precision (HF pipeline, fp32 weights: oracle_scheduler.py:23-25): fp32 GEMMs and
+            # the padded path (ATen attention; the MFMA attention kernel is bf16)
+            from svoc.models.encoder import build as build_encoder
+            enc = build_encoder(dev, enc_dtype, 0)
+            enc.packed = False
+        pipe = SentimentOraclePipeline(eng, encoder=enc, seed=0)
         g = torch.Generator(device=dev).manual_seed(rank)
         toks = [corpus.synthetic_token_batch(B * 30, c["seq_len"], 50265, g, dev) for _ in range(2)]
         from svoc.models.encoder import flops_for_lengths
@@ -139,6 +175,8 @@ def measure(args, c, storage, dev, rank, world, dshard):
     if transactional and mode != "exact":
         raise SystemExit("transactional streaming is the exact engine's per-update replay (mode: exact)")
     extra["transactional"] = transactional
+    if mode == "fast" and stream is not None:
+        extra["fast_transactional"] = eng.transactional
     pipeline = args.pipeline if args.pipeline >= 0 else c.get("pipeline", 1)
     if dshard or mode != "fast" or dev.type != "cuda":
         pipeline = 1
@@ -188,7 +226,13 @@ def measure(args, c, storage, dev, rank, world, dshard):
 
     graph = None
     graph_period = 1
-    if args.graph and dev.type == "cuda" and not (dshard and world > 1):   # (no collectives in a graph)
+    graph_ok = args.graph and dev.type == "cuda"
+    if graph_ok and dshard and world > 1:
+        # the D-shard round's RCCL all-reduce goes into the graph too (RCCL kernels are stream-capturable):
+        # probe one captured all-reduce first, so a backend that cannot capture collectives runs eagerly
+        graph_ok = _collectives_capturable(dev)
+    extra["graph_collectives"] = bool(graph_ok and dshard and world > 1)
+    if graph_ok:
         # the stream cycles with period `pool`: capture one period and replay it
         period = 1
         for k in (stream.pool if stream is not None else 1, len(gov_batches) if gov is not None else 1,
@@ -196,10 +240,13 @@ def measure(args, c, storage, dev, rank, world, dshard):
             period = period * k // math.gcd(period, k)                        # boundaries overlap)
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
+        # (D-shard at world > 1: the streams only -- pipeline_join would commit the deferred round with a
+        # collective; the graph's next round commits it from the engine's persistent pending buffers)
+        join = eng._join_streams if (dshard and world > 1) else eng.pipeline_join
         with torch.cuda.stream(s):
             for i in range(period):
                 step(i)
-            eng.pipeline_join()
+            join()
         torch.cuda.current_stream(dev).wait_stream(s)
         sync()
         try:
@@ -207,7 +254,7 @@ def measure(args, c, storage, dev, rank, world, dshard):
             with torch.cuda.graph(graph):
                 for i in range(period):
                     step(i)
-                eng.pipeline_join()   # every forked stream rejoins the capture stream
+                join()   # every forked stream rejoins the capture stream
             graph_period = period
         except Exception as e:  # graph capture is an optimisation; eager stays correct
             if rank == 0:
@@ -241,6 +288,11 @@ def measure(args, c, storage, dev, rank, world, dshard):
         dist.barrier()
     t1 = time.perf_counter()
     fx = (eng.metrics_fx - fx0).double()
+    ns = eng.net_stats() if mode == "fast" else {"slab_networks": 0}
+    if ns["slab_networks"]:
+        # pruned window network (fp32, N = 256): share of slab networks whose exact check failed and reran
+        # the full network (whole run, warm-up included)
+        extra["pruned_net_fallback_rate"] = ns["fallbacks"] / ns["slab_networks"]
     ok_local = float(fx[1] / fx[2]) if float(fx[2]) > 0 else 0.0
     mine = torch.tensor([t1 - t0, ok_local], dtype=torch.float64, device=dev)
     if world > 1:
@@ -273,6 +325,9 @@ def main():
     ap.add_argument("--overlap", type=int, default=1,
                     help="pipelined steps: overlap consecutive steps too (ConsensusEngine.step_pipelined "
                          "overlap=True); 0 = join the streams at the end of every step")
+    ap.add_argument("--transactional", type=int, default=1,
+                    help="fast streaming: save the rows each update overwrites and restore them for instances "
+                         "whose round reverts (the reference's per-transaction atomicity); 0 = coalesced rows stay")
     ap.add_argument("--mode", default=None, choices=["fast", "exact"],
                     help="override the config's engine mode (exact = bit-exact wsad int64 path)")
     ap.add_argument("--storage", default=None, choices=["bf16", "fp32", "int64", "int32"],
@@ -361,6 +416,17 @@ def main():
             "hbm_gbps_min_traffic": min_gbps(ra, ra["eng"].values.element_size()),
             "rank_ms_spread": [min(ra["rank_ms"]), max(ra["rank_ms"])]}
         log_eng, log_step = ra["eng"], ra["step"]
+    if c.get("alt_precision") == "fp32" and dev.type == "cuda":
+        # c4 at the reference's precision: the same step with fp32 encoder weights / activations
+        del r, eng
+        log_eng = log_step = None
+        torch.cuda.empty_cache()
+        rp = measure(args, c, storage, dev, rank, world, dshard, enc_dtype=torch.float32)
+        out["config"]["alt_precision"] = {
+            "encoder_dtype": "fp32", "value": rp["B"] * scale * args.steps / rp["elapsed"],
+            "ms_per_step": 1e3 * rp["elapsed"] / args.steps, "ok_fraction": rp["ok"],
+            "path": "padded tokens, fp32 GEMMs (hipBLASLt), ATen attention"}
+        log_eng, log_step = rp["eng"], rp["step"]
     if rank == 0:
         print(json.dumps(out))
         if args.log:

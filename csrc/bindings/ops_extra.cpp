@@ -72,12 +72,30 @@ bool in_range_cpu(const UpdateParams& p, int64_t u, int d) {
   return v >= 0 && v <= 1000000;
 }
 
+// transactional streaming buffers (optional): saved [U, D] in the values' dtype, saved_en uint8 [U]
+void set_saved(UpdateParams& p, const c10::optional<at::Tensor>& saved, const c10::optional<at::Tensor>& saved_en,
+               const at::Tensor& upd) {
+  p.saved = nullptr;
+  p.saved_en = nullptr;
+  if (!saved.has_value() || !saved->defined()) return;
+  TORCH_CHECK(saved_en.has_value() && saved_en->defined(), "saved and saved_en go together");
+  TORCH_CHECK(saved->scalar_type() == upd.scalar_type() && saved->is_contiguous() && saved->dim() == 2 &&
+                  saved->size(0) == upd.size(0) && saved->size(1) == upd.size(1),
+              "saved: contiguous [U, D] in the values' dtype");
+  TORCH_CHECK(saved_en->scalar_type() == at::kByte && saved_en->is_contiguous() && saved_en->numel() == upd.size(0),
+              "saved_en: uint8 [U]");
+  p.saved = saved->data_ptr();
+  p.saved_en = saved_en->data_ptr<uint8_t>();
+}
+
 void apply_updates_cpu(at::Tensor values, at::Tensor enabled, at::Tensor n_active, at::Tensor touched,
                        at::Tensor winner, const at::Tensor& inst, const at::Tensor& oracle, const at::Tensor& upd,
-                       bool constrained, at::Tensor upd_status, bool unique) {
+                       bool constrained, at::Tensor upd_status, bool unique, const c10::optional<at::Tensor>& saved,
+                       const c10::optional<at::Tensor>& saved_en) {
   (void)winner;
   (void)unique;  // sequential CPU loop: last writer wins either way
   UpdateParams p = make_update_params(values, enabled, n_active, touched, inst, oracle, upd, constrained, upd_status);
+  set_saved(p, saved, saved_en, upd);
   const int64_t row_bytes = (int64_t)p.D * p.elem_bytes;
   for (int64_t u = 0; u < p.U; ++u) {  // sequential = last writer wins
     const int64_t b = p.inst[u], o = p.oracle[u];
@@ -99,9 +117,16 @@ void apply_updates_cpu(at::Tensor values, at::Tensor enabled, at::Tensor n_activ
       }
     if (st == ST_OK && (b < 0 || b >= p.B || o < 0 || o >= p.N)) st = ST_NOT_ORACLE;
     p.upd_status[u] = st;
+    if (p.saved_en) p.saved_en[u] = kNotSaved;
     if (st != ST_OK) continue;
-    std::memcpy((unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes,
-                (const unsigned char*)p.upd + u * row_bytes, row_bytes);
+    unsigned char* dst = (unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes;
+    if (p.saved) {
+      // sequential: an earlier update of the same slot in this batch is superseded (coalesced); the
+      // restore runs in reverse batch order, so every saved row is the one its update overwrote
+      std::memcpy((unsigned char*)p.saved + u * row_bytes, dst, row_bytes);
+      p.saved_en[u] = p.enabled[b * p.N + o];
+    }
+    std::memcpy(dst, (const unsigned char*)p.upd + u * row_bytes, row_bytes);
     if (!p.enabled[b * p.N + o]) {
       p.enabled[b * p.N + o] = 1;
       p.n_active[b] += 1;
@@ -112,8 +137,10 @@ void apply_updates_cpu(at::Tensor values, at::Tensor enabled, at::Tensor n_activ
 
 void apply_updates_hip(at::Tensor values, at::Tensor enabled, at::Tensor n_active, at::Tensor touched,
                        at::Tensor winner, const at::Tensor& inst, const at::Tensor& oracle, const at::Tensor& upd,
-                       bool constrained, at::Tensor upd_status, bool unique) {
+                       bool constrained, at::Tensor upd_status, bool unique, const c10::optional<at::Tensor>& saved,
+                       const c10::optional<at::Tensor>& saved_en) {
   UpdateParams p = make_update_params(values, enabled, n_active, touched, inst, oracle, upd, constrained, upd_status);
+  set_saved(p, saved, saved_en, upd);
   p.unique = unique ? 1 : 0;
   TORCH_CHECK(winner.scalar_type() == at::kInt && winner.numel() == (int64_t)p.B * p.N && winner.is_contiguous(),
               "winner workspace: int32 [B, N] filled with -1");
@@ -123,12 +150,82 @@ void apply_updates_hip(at::Tensor values, at::Tensor enabled, at::Tensor n_activ
   TORCH_CHECK(rc == 0, "svoc_apply_updates failed: ", rc);
 }
 
+RestoreParams make_restore_params(at::Tensor& values, at::Tensor& enabled, at::Tensor& n_active, const at::Tensor& inst,
+                                  const at::Tensor& oracle, at::Tensor& upd_status, const at::Tensor& saved,
+                                  const at::Tensor& saved_en, const at::Tensor& status, const at::Tensor& active) {
+  TORCH_CHECK(values.dim() == 3 && values.stride(2) == 1 && values.stride(1) == values.size(2),
+              "values: [B, N, ld] with dense rows");
+  const int64_t B = values.size(0), N = values.size(1), U = inst.numel();
+  TORCH_CHECK(inst.scalar_type() == at::kLong && oracle.scalar_type() == at::kLong && oracle.numel() == U &&
+                  inst.is_contiguous() && oracle.is_contiguous(), "inst/oracle: contiguous int64 [U]");
+  TORCH_CHECK(upd_status.scalar_type() == at::kInt && upd_status.numel() == U, "upd_status: int32 [U]");
+  TORCH_CHECK(saved.scalar_type() == values.scalar_type() && saved.is_contiguous() && saved.dim() == 2 &&
+                  saved.size(0) == U && saved.size(1) <= values.size(2), "saved: contiguous [U, D]");
+  TORCH_CHECK(saved_en.scalar_type() == at::kByte && saved_en.numel() == U, "saved_en: uint8 [U]");
+  TORCH_CHECK(status.scalar_type() == at::kInt && status.numel() == B && status.is_contiguous(), "status: int32 [B]");
+  TORCH_CHECK(active.scalar_type() == at::kByte && active.numel() == B && active.is_contiguous(), "active: uint8 [B]");
+  TORCH_CHECK(enabled.scalar_type() == at::kByte && enabled.numel() == B * N && n_active.scalar_type() == at::kInt &&
+                  n_active.numel() == B, "enabled uint8 [B, N], n_active int32 [B]");
+  RestoreParams p{};
+  p.values = values.data_ptr();
+  p.enabled = enabled.data_ptr<uint8_t>();
+  p.n_active = n_active.data_ptr<int32_t>();
+  p.inst = inst.data_ptr<int64_t>();
+  p.oracle = oracle.data_ptr<int64_t>();
+  p.upd_status = upd_status.data_ptr<int32_t>();
+  p.saved = saved.data_ptr();
+  p.saved_en = saved_en.data_ptr<uint8_t>();
+  p.status = status.data_ptr<int32_t>();
+  p.active = active.data_ptr<uint8_t>();
+  p.inst_stride = values.stride(0);
+  p.B = (int)B; p.N = (int)N; p.D = (int)saved.size(1); p.ld = (int)values.size(2); p.U = (int)U;
+  p.elem_bytes = (int)values.element_size();
+  return p;
+}
+
+void restore_updates_cpu(at::Tensor values, at::Tensor enabled, at::Tensor n_active, const at::Tensor& inst,
+                         const at::Tensor& oracle, at::Tensor upd_status, const at::Tensor& saved,
+                         const at::Tensor& saved_en, const at::Tensor& status, const at::Tensor& active) {
+  RestoreParams p = make_restore_params(values, enabled, n_active, inst, oracle, upd_status, saved, saved_en, status,
+                                        active);
+  const int64_t row_bytes = (int64_t)p.D * p.elem_bytes;
+  for (int64_t u = p.U - 1; u >= 0; --u) {   // reverse batch order (a slot updated twice: see apply)
+    if (p.upd_status[u] != ST_OK) continue;
+    const int64_t b = p.inst[u], o = p.oracle[u];
+    if (b < 0 || b >= p.B || o < 0 || o >= p.N || !p.active[b] || p.status[b] == ST_OK) continue;
+    const uint8_t was = p.saved_en[u];
+    if (was != kNotSaved) {
+      std::memcpy((unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes,
+                  (const unsigned char*)p.saved + u * row_bytes, row_bytes);
+      if (was == 0) {
+        p.enabled[b * p.N + o] = 0;
+        p.n_active[b] -= 1;
+      }
+    }
+    p.upd_status[u] = p.status[b];
+  }
+}
+
+void restore_updates_hip(at::Tensor values, at::Tensor enabled, at::Tensor n_active, const at::Tensor& inst,
+                         const at::Tensor& oracle, at::Tensor upd_status, const at::Tensor& saved,
+                         const at::Tensor& saved_en, const at::Tensor& status, const at::Tensor& active) {
+  RestoreParams p = make_restore_params(values, enabled, n_active, inst, oracle, upd_status, saved, saved_en, status,
+                                        active);
+  auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
+  const int rc = svoc_restore_updates(&p, stream);
+  TORCH_CHECK(rc == 0, "svoc_restore_updates failed: ", rc);
+}
+
 }  // namespace
 
 void register_extra_defs(torch::Library& m) {
   m.def(
       "apply_updates(Tensor(a!) values, Tensor(b!) enabled, Tensor(c!) n_active, Tensor(d!) touched, "
-      "Tensor(e!) winner, Tensor inst, Tensor oracle, Tensor upd, bool constrained, Tensor(f!) upd_status, bool unique=False) -> ()");
+      "Tensor(e!) winner, Tensor inst, Tensor oracle, Tensor upd, bool constrained, Tensor(f!) upd_status, bool unique=False, "
+      "Tensor(g!)? saved=None, Tensor(h!)? saved_en=None) -> ()");
+  m.def(
+      "restore_updates(Tensor(a!) values, Tensor(b!) enabled, Tensor(c!) n_active, Tensor inst, Tensor oracle, "
+      "Tensor(d!) upd_status, Tensor saved, Tensor saved_en, Tensor status, Tensor active) -> ()");
   register_governance_defs(m);
   register_generator_defs(m);
   register_io_defs(m);
@@ -138,6 +235,7 @@ void register_extra_defs(torch::Library& m) {
 
 void register_extra_cpu(torch::Library& m) {
   m.impl("apply_updates", &apply_updates_cpu);
+  m.impl("restore_updates", &restore_updates_cpu);
   register_governance_cpu(m);
   register_generator_cpu(m);
   register_bookkeeping_cpu(m);
@@ -146,6 +244,7 @@ void register_extra_cpu(torch::Library& m) {
 
 void register_extra_hip(torch::Library& m) {
   m.impl("apply_updates", &apply_updates_hip);
+  m.impl("restore_updates", &restore_updates_hip);
   register_governance_hip(m);
   register_generator_hip(m);
   register_bookkeeping_hip(m);

@@ -63,9 +63,10 @@ void fast_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& a
                     int64_t n_failing, bool constrained, double max_spread, at::Tensor c1, at::Tensor cons,
                     at::Tensor skew, at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable,
                     at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim, bool legacy,
-                    const c10::optional<at::Tensor>& work) {
+                    const c10::optional<at::Tensor>& work, const c10::optional<at::Tensor>& stats) {
   (void)wave_hint;
   (void)work;
+  (void)stats;   // (GPU pruned-network counter; the CPU twin runs full sorts)
   fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
   const int64_t B = values.size(0), N = values.size(1), ld = values.size(2), is = values.stride(0);
   TORCH_CHECK(values.scalar_type() == at::kBFloat16 || values.scalar_type() == at::kFloat,
@@ -110,7 +111,7 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
                     int64_t n_failing, bool constrained, double max_spread, at::Tensor c1, at::Tensor cons,
                     at::Tensor skew, at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable,
                     at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim, bool legacy,
-                    const c10::optional<at::Tensor>& work) {
+                    const c10::optional<at::Tensor>& work, const c10::optional<at::Tensor>& stats) {
   fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
   TORCH_CHECK(values.scalar_type() == at::kBFloat16 || values.scalar_type() == at::kFloat,
               "GPU fast path stores values in bf16 or fp32");
@@ -182,6 +183,11 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
   auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
   // (mode 0: the kernel, or its dispatcher, commits the staged c1 into c1_out)
   p.c1_out = mode == 0 ? c1.data_ptr<float>() : nullptr;
+  if (stats.has_value() && stats->defined()) {
+    TORCH_CHECK(stats->scalar_type() == at::kInt && stats->numel() >= 1 && stats->device() == values.device(),
+                "stats: int32 [>= 1] on the values' device ([0] += pruned-network fallbacks)");
+    p.net_fallbacks = (unsigned int*)stats->data_ptr();
+  }
   const int rc = f32 ? svoc_fast_round_f32(&p, stream) : svoc_fast_round_bf16(&p, stream);
   TORCH_CHECK(rc == 0, f32 ? "svoc_fast_round_f32" : "svoc_fast_round_bf16", " launch failed: ", rc);
 }
@@ -301,7 +307,7 @@ TORCH_LIBRARY(svoc, m) {
       "fast_round(Tensor values, Tensor? active, int D, int n_failing, bool constrained, float max_spread, "
       "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "
       "Tensor(g!) reliable, Tensor(h!) status, int wave_hint=0, int mode=0, int rel_dim=0, bool legacy=False, "
-      "Tensor? work=None) -> ()");
+      "Tensor? work=None, Tensor(i!)? stats=None) -> ()");
   m.def(
       "exact_round(Tensor values, Tensor? active, int n_failing, bool constrained, int max_spread, "
       "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "

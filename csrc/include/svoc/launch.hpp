@@ -36,6 +36,9 @@ struct FastParams {
   // succeeded (the window kernels write it in their commit phase, the dispatchers commit it for the
   // others with svoc_commit_rows).  Null: the caller commits (or mode 1 / 2: c1 is the output itself).
   float* c1_out;
+  // optional counter: slab networks of the pruned window path (N = 256) that failed their exact check and
+  // reran the full network (consensus_fast_winf.hip); null = not counted
+  unsigned int* net_fallbacks;
 };
 
 // Workspace per instance of the LDS-free fast kernels, in u32 words (Dp = fast_work_pairs(D)).
@@ -129,11 +132,36 @@ struct UpdateParams {
   int dtype;                // 0 bf16, 1 fp32, 2 int64 wsad, 3 int32 wsad
   int constrained;
   int unique;               // caller guarantees distinct (instance, oracle) pairs: one fused pass
+  // transactional fast streaming (optional, null = off): every applied update first copies the row it
+  // overwrites to saved[u] ([U, D], the values' dtype) and its old `enabled` flag to saved_en[u]
+  // (kNotSaved when the update did not store), so a reverted round can restore the pre-batch state
+  void* saved;
+  uint8_t* saved_en;
+};
+constexpr uint8_t kNotSaved = 0xFF;
+
+// Roll back the applied updates of the instances whose round ran and reverted (active[b] set, status[b]
+// not OK): rows from saved, enabled from saved_en, n_active decremented for first commits, and the
+// update's transaction status set to the round's code (contract.cairo:588-603: the whole tx reverts).
+struct RestoreParams {
+  void* values;
+  uint8_t* enabled;
+  int32_t* n_active;
+  const int64_t* inst;
+  const int64_t* oracle;
+  int32_t* upd_status;
+  const void* saved;
+  const uint8_t* saved_en;
+  const int32_t* status;    // [B] round status
+  const uint8_t* active;    // [B] the round ran
+  int64_t inst_stride;
+  int B, N, D, ld, U, elem_bytes;
 };
 
 }  // namespace svoc
 
 extern "C" int svoc_apply_updates(const svoc::UpdateParams* p, hipStream_t stream);
+extern "C" int svoc_restore_updates(const svoc::RestoreParams* p, hipStream_t stream);
 // row b of src -> dst (words 4-byte words per row) where status[b] == OK and (active null or set)
 extern "C" int svoc_commit_rows(const void* src, void* dst, const int32_t* status, const uint8_t* active, int64_t B,
                                 int64_t words, hipStream_t stream);

@@ -138,11 +138,25 @@ SVOC_DEV void qr_keep(const f32x2 (&a)[32], int lane, float (&keep)[64 / P], boo
   for (int i = 0; i < 64 / P; ++i) keep[i] = add ? keep[i] + part[i] : part[i];
 }
 
+// window_group_pruned for N = 256 (H = 17, one window part of H keys per lane); `wk` sized by the
+// caller's instantiation (the template parameter keeps the call dependent, so other widths compile)
+template <int P, int H, int WN>
+SVOC_DEV bool try_pruned(uint32_t (&r)[64], int seg, int lane, uint32_t (&w)[WN], uint32_t& lo, uint32_t& hi) {
+  if constexpr (WN == H && H == 17) {
+    bool ok;
+    window_group_pruned<P, H>(r, seg, lane, w, lo, hi, ok);
+    return ok;
+  } else {
+    return false;
+  }
+}
+
 // One workgroup per instance.  Phase A streams the instance through LDS one WAVES * P-column slab at a
 // time: wait for the slab's DMA + barrier, every lane copies its column's 64 rows (its lane-group
 // segment) into registers (raw values and sort keys), barrier, the next slab's DMA is issued, and the
 // network, window, c1 and qr pass run on the registers while it lands.  2 waves per SIMD (<= 256
 // VGPRs: 64 keys + 64 raw rows + the window), LDS = WAVES x 16 KiB.
+
 template <int NSEG, int WAVES, int H, bool CONS, int MODE>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2))) void consensus_fast_winf_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // columns per wave (phase A)
@@ -197,6 +211,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
   float keep[KEEP];
 #pragma unroll
   for (int i = 0; i < KEEP; ++i) keep[i] = 0.f;
+  int net_fallbacks = 0;   // slabs whose pruned network failed its check (wave-uniform)
 
   // ------------------------------------------------------------ phase A: pass 1 (contract.cairo:455-463)
   const int pass1_slabs = PASS1 ? nslab : 0;
@@ -227,22 +242,43 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     if (s + 1 < pass1_slabs) dma.issue(rsd, region, rowb, (s + 1) * W + wave * P);
     {
       uint32_t r[64];
-      if (FULL || N == NPAD) {
+      auto build_keys = [&](uint32_t kpx) __attribute__((always_inline)) {
+        if (FULL || N == NPAD) {
 #pragma unroll
-        for (int i = 0; i < 64; ++i) r[i] = CONS ? xs.at(i) ^ kp : fkey<CONS>(xs.at(i)) ^ pol;
-      } else {
+          for (int i = 0; i < 64; ++i) r[i] = CONS ? xs.at(i) ^ kpx : fkey<CONS>(xs.at(i)) ^ pol;
+        } else {
 #pragma unroll
-        for (int i = 0; i < 64; ++i) {
-          // real rows -> key; rows >= N (read as 0) -> 0 (the first lo1) / ~0 sentinels, so the middle of
-          // the padded sort is the middle of the real rows
-          const uint32_t hi_m = ~lt_mask(i, nll);
-          r[i] = ((fkey<CONS>(xs.at(i)) & (lt_mask(i, nvl) | hi_m)) | hi_m) ^ pol;
+          for (int i = 0; i < 64; ++i) {
+            // real rows -> key; rows >= N (read as 0) -> 0 (the first lo1) / ~0 sentinels, so the middle of
+            // the padded sort is the middle of the real rows
+            const uint32_t hi_m = ~lt_mask(i, nll);
+            r[i] = ((fkey<CONS>(xs.at(i)) & (lt_mask(i, nvl) | hi_m)) | hi_m) ^ pol;
+          }
         }
-      }
+      };
+      build_keys(kp);
       uint32_t klo, khi;
       if constexpr (CONS) {
         uint32_t wk[NSEG == 1 ? 2 * H : H];
-        window_group<NSEG, P, H>(r, seg, lane, wk, klo, khi);
+        auto pruned_net = [&](auto full_c2) __attribute__((always_inline)) {
+          if constexpr (NSEG == 4 && H == 17 && decltype(full_c2)::value) {
+            // N = 256: the pruned network (middle 32 keys of every lane) + its exact check; a wave with any
+            // failing column reruns the full network from the raw rows (sortnet.hpp window_group_pruned)
+            const bool ok = try_pruned<P, H>(r, seg, lane, wk, klo, khi);
+            if (__ballot(!ok) != 0) {
+              ++net_fallbacks;
+              // an opaque copy of the key XOR: otherwise CSE keeps the first 64 keys alive across the
+              // pruned network to reuse them here (+64 VGPRs: spills)
+              uint32_t kpo = kp;
+              asm volatile("" : "+v"(kpo));
+              build_keys(kpo);
+              window_group<NSEG, P, H>(r, seg, lane, wk, klo, khi);
+            }
+          } else {
+            window_group<NSEG, P, H>(r, seg, lane, wk, klo, khi);
+          }
+        };
+        pruned_net(full_c);
         if constexpr (NSEG == 1) {
 #pragma unroll
           for (int m = 0; m < H; ++m) {
@@ -296,6 +332,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     for (int s = nfull; s < pass1_slabs; ++s) slab_body(std::false_type{}, s);
   }
 
+  if (net_fallbacks && lane == 0 && p.net_fallbacks) atomicAdd(p.net_fallbacks, (unsigned)net_fallbacks);
   // ------------------------------------------------------------ qr reduction
   {
     if constexpr (ACC64) qr_keep<P>(acc, lane, keep, false);
@@ -733,7 +770,9 @@ static void launch_winf_w(const FastParams& p, hipStream_t stream) {
 }
 
 // 4-wave workgroups: 64 KiB of LDS slab each, two workgroups per CU (2 waves per SIMD) -- one's
-// barriers and slab-0 load overlap the other's compute.
+// barriers and slab-0 load overlap the other's compute.  (A 2-wave form with two DMA regions per wave,
+// one wave per SIMD, measured slower: c3 fp32 rounds 1944 vs 1796 us per 1024 instances, c2 fp32
+// 8.1 M vs 10.1 M rounds/s -- profiles/r4_winf_dbuf_ab.txt.)
 template <int NSEG, int H, bool CONS>
 static void launch_winf_c(const FastParams& p, hipStream_t stream) {
   launch_winf_w<NSEG, 4, H, CONS>(p, stream);

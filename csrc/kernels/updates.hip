@@ -92,8 +92,47 @@ __global__ __launch_bounds__(256) void upd_validate_kernel(UpdateParams p) {
   if (in && sub == 0) {
     const int st = row_status(ok, fin, bad);
     p.upd_status[u] = st;
+    if (p.saved_en) p.saved_en[u] = kNotSaved;   // the winner's apply overwrites it
     if (st == ST_OK) atomicMax(&p.winner[b * p.N + o], (int)u);
   }
+}
+
+// Row copy src -> dst by the L lanes of an update (16-B vectors when aligned); with `sv` (transactional
+// streaming) every chunk of dst is first copied to sv -- loaded before the chunk is overwritten by the
+// same lane, so the saved row is the pre-update one.
+template <int L>
+__device__ __forceinline__ void copy_row(unsigned char* dst, const unsigned char* src, unsigned char* sv,
+                                         int64_t row_bytes, int sub) {
+  if (((uintptr_t)dst & 15) == 0 && ((uintptr_t)src & 15) == 0 && (!sv || ((uintptr_t)sv & 15) == 0) &&
+      (row_bytes & 15) == 0) {
+    for (int64_t i = sub; i < row_bytes / 16; i += L) {
+      if (sv) ((uint4*)sv)[i] = ((const uint4*)dst)[i];
+      ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    }
+  } else if (((uintptr_t)dst & 3) == 0 && ((uintptr_t)src & 3) == 0 && (!sv || ((uintptr_t)sv & 3) == 0) &&
+             (row_bytes & 3) == 0) {
+    for (int64_t i = sub; i < row_bytes / 4; i += L) {
+      if (sv) ((uint32_t*)sv)[i] = ((const uint32_t*)dst)[i];
+      ((uint32_t*)dst)[i] = ((const uint32_t*)src)[i];
+    }
+  } else {
+    for (int64_t i = sub; i < row_bytes; i += L) {
+      if (sv) sv[i] = dst[i];
+      dst[i] = src[i];
+    }
+  }
+}
+
+// first commit of an (instance, oracle) slot: enabled + n_active (contract.cairo:331-343); the old flag
+// goes to saved_en (transactional streaming)
+__device__ __forceinline__ void commit_flags(const UpdateParams& p, int64_t u, int64_t b, int64_t o) {
+  const uint8_t was = p.enabled[b * p.N + o];
+  if (p.saved_en) p.saved_en[u] = was;
+  if (!was) {
+    p.enabled[b * p.N + o] = 1;
+    atomicAdd(&p.n_active[b], 1);
+  }
+  p.touched[b] = 1;
 }
 
 // the winner of each slot copies its row (16-B vectors when aligned), flips `enabled`, bumps
@@ -108,20 +147,9 @@ __global__ __launch_bounds__(256) void upd_apply_kernel(UpdateParams p) {
   const int64_t row_bytes = (int64_t)p.D * p.elem_bytes;
   unsigned char* dst = (unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes;
   const unsigned char* src = (const unsigned char*)p.upd + u * row_bytes;
-  if (((uintptr_t)dst & 15) == 0 && ((uintptr_t)src & 15) == 0 && (row_bytes & 15) == 0) {
-    for (int64_t i = sub; i < row_bytes / 16; i += L) ((uint4*)dst)[i] = ((const uint4*)src)[i];
-  } else if (((uintptr_t)dst & 3) == 0 && ((uintptr_t)src & 3) == 0 && (row_bytes & 3) == 0) {
-    for (int64_t i = sub; i < row_bytes / 4; i += L) ((uint32_t*)dst)[i] = ((const uint32_t*)src)[i];
-  } else {
-    for (int64_t i = sub; i < row_bytes; i += L) dst[i] = src[i];
-  }
-  if (sub == 0) {
-    if (!p.enabled[b * p.N + o]) {
-      p.enabled[b * p.N + o] = 1;
-      atomicAdd(&p.n_active[b], 1);
-    }
-    p.touched[b] = 1;
-  }
+  unsigned char* sv = p.saved ? (unsigned char*)p.saved + u * row_bytes : nullptr;
+  copy_row<L>(dst, src, sv, row_bytes, sub);
+  if (sub == 0) commit_flags(p, u, b, o);
 }
 
 // unique (instance, oracle) pairs (e.g. a synthetic stream, one bootstrap batch per window): no
@@ -150,14 +178,18 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
   const int64_t nch = row_bytes / 16;
   if (p.dtype <= 1 && vec && nch <= (int64_t)RB * L) {  // uniform over the launch
     uint4 v[RB];
+    u32x4 old[RB];   // transactional: the row being overwritten, loaded in the same batch (one round trip)
     bool ok = true, fin = true;
     const bool live = in;
+    const bool sv_on = p.saved != nullptr;   // uniform
 #pragma unroll
     for (int k = 0; k < RB; ++k) {
       const int64_t i = sub + (int64_t)k * L;
       u32x4 t = {0u, 0u, 0u, 0u};
       if (live && i < nch) t = __builtin_nontemporal_load((const u32x4*)src + i);
       v[k] = uint4{t.x, t.y, t.z, t.w};
+      old[k] = u32x4{0u, 0u, 0u, 0u};
+      if (sv_on && live && !bad && i < nch) old[k] = ((const u32x4*)dst)[i];
     }
 #pragma unroll
     for (int k = 0; k < RB; ++k) {
@@ -177,8 +209,19 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
     fin = group_all<L>(fin);
     if (!in) return;
     const int st = row_status(ok, fin, bad);
-    if (sub == 0) p.upd_status[u] = st;
+    if (sub == 0) {
+      p.upd_status[u] = st;
+      if (st != ST_OK && p.saved_en) p.saved_en[u] = kNotSaved;
+    }
     if (st != ST_OK) return;
+    if (sv_on) {   // (uniform) the old row, saved beside the update
+      u32x4* sv = (u32x4*)((unsigned char*)p.saved + u * row_bytes);
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        const int64_t i = sub + (int64_t)k * L;
+        if (i < nch) __builtin_nontemporal_store(old[k], sv + i);   // read back only on a revert
+      }
+    }
 #pragma unroll
     for (int k = 0; k < RB; ++k) {
       const int64_t i = sub + (int64_t)k * L;
@@ -203,7 +246,16 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
     if (!in) return;
     const int st = row_status(ok, fin, bad);
     p.upd_status[u] = st;
-    if (st != ST_OK) return;
+    if (st != ST_OK) {
+      if (p.saved_en) p.saved_en[u] = kNotSaved;
+      return;
+    }
+    if (p.saved) {
+      uint32_t* sv = (uint32_t*)((unsigned char*)p.saved + u * row_bytes);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < nw) sv[k] = ((const uint32_t*)dst)[k];
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (k < nw) ((uint32_t*)dst)[k] = w[k];
@@ -231,23 +283,45 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
     fin = group_all<L>(fin);
     if (!in) return;
     const int st = row_status(ok, fin, bad);
-    if (sub == 0) p.upd_status[u] = st;
+    if (sub == 0) {
+      p.upd_status[u] = st;
+      if (st != ST_OK && p.saved_en) p.saved_en[u] = kNotSaved;
+    }
     if (st != ST_OK) return;
     // the row was just read by these lanes: the copy re-reads it from L2
-    if (vec) {
-      for (int64_t i = sub; i < nch; i += L) ((uint4*)dst)[i] = ((const uint4*)src)[i];
-    } else if (((uintptr_t)dst & 3) == 0 && ((uintptr_t)src & 3) == 0 && (row_bytes & 3) == 0) {
-      for (int64_t i = sub; i < row_bytes / 4; i += L) ((uint32_t*)dst)[i] = ((const uint32_t*)src)[i];
-    } else {
-      for (int64_t i = sub; i < row_bytes; i += L) dst[i] = src[i];
-    }
+    copy_row<L>(dst, src, p.saved ? (unsigned char*)p.saved + u * row_bytes : nullptr, row_bytes, sub);
   }
-  if (sub == 0) {
-    if (!p.enabled[b * p.N + o]) {
-      p.enabled[b * p.N + o] = 1;
-      atomicAdd(&p.n_active[b], 1);
+  if (sub == 0) commit_flags(p, u, b, o);
+}
+
+// Roll back the reverted instances' updates (RestoreParams).  One thread per update, grid-stride over a
+// small grid: the check is a few loads per update and reverts are rare, so the kernel must not need many
+// workgroup slots -- it runs right after its range's round, beside the other range's round kernel, which
+// holds every slot it can get (a one-wave-per-update form took ~85 us there, on the step's critical path).
+// A reverted update's row is copied back by its own thread (16-B vectors when aligned).
+__global__ __launch_bounds__(256) void upd_restore_kernel(RestoreParams p) {
+  const int64_t row_bytes = (int64_t)p.D * p.elem_bytes;
+  for (int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x; u < p.U; u += (int64_t)gridDim.x * 256) {
+    if (p.upd_status[u] != ST_OK) continue;
+    const int64_t b = p.inst[u], o = p.oracle[u];
+    if (b < 0 || b >= p.B || o < 0 || o >= p.N) continue;
+    const int rst = p.status[b];
+    if (!p.active[b] || rst == ST_OK) continue;
+    const uint8_t was = p.saved_en[u];
+    if (was != kNotSaved) {
+      unsigned char* dst = (unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes;
+      const unsigned char* sv = (const unsigned char*)p.saved + u * row_bytes;
+      if (((uintptr_t)dst & 15) == 0 && ((uintptr_t)sv & 15) == 0 && (row_bytes & 15) == 0) {
+        for (int64_t i = 0; i < row_bytes / 16; ++i) ((uint4*)dst)[i] = ((const uint4*)sv)[i];
+      } else {
+        for (int64_t i = 0; i < row_bytes; ++i) dst[i] = sv[i];
+      }
+      if (was == 0) {
+        p.enabled[b * p.N + o] = 0;
+        atomicSub(&p.n_active[b], 1);
+      }
     }
-    p.touched[b] = 1;
+    p.upd_status[u] = rst;   // the transaction reverted with the round's code
   }
 }
 
@@ -275,6 +349,13 @@ static int launch_updates(const UpdateParams& p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+static int launch_restore(const RestoreParams& p, hipStream_t stream) {
+  int64_t blocks = ((int64_t)p.U + 255) / 256;
+  if (blocks > 64) blocks = 64;
+  hipLaunchKernelGGL(upd_restore_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p);
+  return (int)hipGetLastError();
+}
+
 }  // namespace svoc
 
 using namespace svoc;
@@ -290,4 +371,9 @@ extern "C" int svoc_apply_updates(const UpdateParams* p, hipStream_t stream) {
   if (chunks <= 16) return launch_updates<16>(*p, stream);
   if (chunks <= 32) return launch_updates<32>(*p, stream);
   return launch_updates<64>(*p, stream);
+}
+
+extern "C" int svoc_restore_updates(const RestoreParams* p, hipStream_t stream) {
+  if (p->U <= 0) return 0;
+  return launch_restore(*p, stream);
 }

@@ -20,8 +20,13 @@ Two numeric modes share one semantics:
 * ``fast``: fp32 math over bf16 storage (the fused kernels csrc/kernels/consensus_fast_*.hip) or fp32
   storage (``storage="fp32"``: reference resolution, csrc/kernels/consensus_fast_f32.hip).
   Updates inside one step are coalesced (last writer wins) -- exact for the reference because a
-  round is a pure function of the current values (survey §2.8-13); a reverted round keeps the stored
-  values but leaves every consensus output untouched.
+  round is a pure function of the current values (survey §2.8-13).  Steps are transactional per
+  instance (``transactional=True``, the default): the update kernels save every row they overwrite, and
+  a round that reverts restores that instance's rows, ``enabled`` flags and ``n_active`` to their
+  pre-batch state and reports the round's code as the status of each of its updates
+  (contract.cairo:588-603: the reverted transaction leaves no trace); its consensus outputs stay
+  untouched as well.  (Coalescing differs from the reference's one-transaction-per-update replay only
+  when a revert happens: the whole batch of that instance reverts.)
 
 Steady-state steps issue no host synchronisation, so they can be captured in a HIP graph.
 """
@@ -90,6 +95,14 @@ class ConsensusEngine:
         self.rounds = 0
         self.failing_mask: Optional[torch.Tensor] = None   # [B, N] set by randomize()
         self._work = None   # window-kernel workspace (GPU fast mode), allocated on first use
+        # transactional fast steps: the rows each apply_updates call overwrote, restored by the next round
+        # for the instances whose round reverts (engine docstring)
+        self.transactional = mode == "fast"
+        # pruned window network (fp32, N = 256): slab networks that failed the exact check and reran the
+        # full network, counted by the kernel (net_stats)
+        self._net_fb = torch.zeros(1, dtype=torch.int32, device=dev) if (mode == "fast" and dev.type == "cuda") else None
+        self._pending_restore = []
+        self._save_bufs: Dict[tuple, tuple] = {}
         # health counters folded in by every round's epilogue: [rel2 sum (2^-32 units fast / wsad
         # exact), committed, processed, reverted]
         self.metrics_fx = torch.zeros(4, dtype=torch.int64, device=dev)
@@ -123,7 +136,7 @@ class ConsensusEngine:
         return vals.to(self.device, self.vdtype).contiguous()
 
     def apply_updates(self, inst: torch.Tensor, oracle: torch.Tensor, vals: torch.Tensor,
-                      unique: bool = False, _joined: bool = False) -> torch.Tensor:
+                      unique: bool = False, _joined: bool = False, save=None) -> torch.Tensor:
         """Store a batch of predictions (no consensus). Returns the per-update status [U] (device).
 
         ``unique=True``: the caller guarantees distinct (instance, oracle) pairs in the batch, so the GPU
@@ -137,10 +150,40 @@ class ConsensusEngine:
         vals = self._as_storage(torch.as_tensor(vals))
         if vals.dim() != 2 or vals.shape[1] != self.D:
             raise ValueError(f"predictions must be [U, {self.D}]")
-        st = torch.empty(inst.numel(), dtype=torch.int32, device=self.device)
+        saved = saved_en = None
+        if save is not None:      # (saved rows, saved enabled flags, status out) of step_pipelined
+            saved, saved_en, st = save
+        else:
+            st = torch.empty(inst.numel(), dtype=torch.int32, device=self.device)
+            if self.transactional:
+                saved, saved_en, _ = self._save_buffer(("pending", len(self._pending_restore)), inst.numel())
+                self._pending_restore.append((inst, oracle, st, saved, saved_en))
         self._ops.apply_updates(self.values, self.enabled, self.n_active, self.touched, self._winner,
-                                inst, oracle, vals, self.cfg.constrained, st, bool(unique))
+                                inst, oracle, vals, self.cfg.constrained, st, bool(unique), saved, saved_en)
         return st
+
+    def _save_buffer(self, key, U: int):
+        """Reusable [U, D] / [U] save buffers of the transactional update path (stable across steps, so
+        a captured HIP graph replays into the same memory)."""
+        buf = self._save_bufs.get(key)
+        if buf is None or buf[0].shape[0] < U:
+            buf = (torch.empty(U, self.D, dtype=self.vdtype, device=self.device),
+                   torch.empty(U, dtype=torch.uint8, device=self.device),
+                   torch.empty(U, dtype=torch.int32, device=self.device))
+            self._save_bufs[key] = buf
+        return buf[0][:U], buf[1][:U], buf[2][:U]
+
+    def _restore(self, entries, status=None) -> None:
+        """Roll back the saved updates of the instances whose round ran and reverted (latest batch first)."""
+        status = self.status if status is None else status
+        for inst, oracle, st, saved, saved_en in reversed(entries):
+            self._ops.restore_updates(self.values, self.enabled, self.n_active, inst, oracle, st, saved, saved_en,
+                                      status, self._active)
+
+    def _restore_pending(self, status=None) -> None:
+        if self._pending_restore:
+            self._restore(self._pending_restore, status)
+            self._pending_restore = []
 
     # ------------------------------------------------------------------ rounds
     def run_round(self, only_touched: bool = True) -> None:
@@ -156,7 +199,8 @@ class ConsensusEngine:
             self._ops.fast_round(self.values, self._active, self.D, self.cfg.n_failing_oracles,
                                  self.cfg.constrained, float(mx), self.c1, self.consensus, self.skew,
                                  self.kurt, self.rel, self.qr, self.reliable, self.status, self.wave_hint,
-                                 0, 0, self.cfg.legacy, self.work())
+                                 0, 0, self.cfg.legacy, self.work(), self._net_fb)
+            self._restore_pending()
         else:
             self._ops.exact_round(self.values, self._active, self.cfg.n_failing_oracles, self.cfg.constrained,
                                   self.cfg.max_spread_wsad, self.c1, self.consensus, self.skew, self.kurt,
@@ -165,8 +209,9 @@ class ConsensusEngine:
                                  self.metrics_fx)
         self.rounds += 1
 
-    def _run_round_range(self, b0: int, b1: int, only_touched: bool = True) -> None:
-        """run_round over instances [b0, b1) only (views of the state; fast mode)."""
+    def _run_round_range(self, b0: int, b1: int, only_touched: bool = True, restore=None) -> None:
+        """run_round over instances [b0, b1) only (views of the state; fast mode); ``restore``: the
+        range's saved update batch (inst, oracle, st, saved, saved_en), rolled back where it reverted."""
         sl = slice(b0, b1)
         self._ops.round_prologue(self.n_active[sl], self.touched[sl], self.N, bool(only_touched), self._active[sl])
         w = self.work()
@@ -176,7 +221,10 @@ class ConsensusEngine:
         self._ops.fast_round(self.values[sl], self._active[sl], self.D, self.cfg.n_failing_oracles,
                              self.cfg.constrained, float(self.cfg.unconstrained_max_spread), self.c1[sl],
                              self.consensus[sl], self.skew[sl], self.kurt[sl], self.rel[sl], self.qr[sl],
-                             self.reliable[sl], self.status[sl], self.wave_hint, 0, 0, self.cfg.legacy, w)
+                             self.reliable[sl], self.status[sl], self.wave_hint, 0, 0, self.cfg.legacy, w,
+                             self._net_fb)
+        if restore is not None:
+            self._restore([restore])
         self._ops.round_epilogue(self._active[sl], self.status[sl], self.rel[sl], self.consensus_active[sl],
                                  self.touched[sl], self.metrics_fx)
 
@@ -198,7 +246,8 @@ class ConsensusEngine:
         every other engine method) joins the streams into the current stream before anything else
         touches the state."""
         U = int(updates_per_instance)
-        if self.mode != "fast" or self.device.type != "cuda" or chunks <= 1:
+        # (a lone apply_updates before this step is still awaiting its round: one round must cover both)
+        if self.mode != "fast" or self.device.type != "cuda" or chunks <= 1 or self._pending_restore:
             self.pipeline_join()
             self.apply_updates(inst, oracle, vals, unique=True)
             self.run_round()
@@ -212,6 +261,22 @@ class ConsensusEngine:
         su, sc = self._pipe_streams[0], self._pipe_streams[1:]
         step = (self.B + chunks - 1) // chunks
         ranges = [(k * step, min(self.B, (k + 1) * step)) for k in range(chunks) if k * step < self.B]
+        # per-step buffers live in the engine (the side streams use them after this returns): saved rows,
+        # saved enabled flags and the update statuses, one slice per range
+        sv_all, sen_all, st_all = self._save_buffer(("pipe",), inst.numel()) if self.transactional else (None,) * 3
+
+        def upd(k, b0, b1):
+            sl = slice(b0 * U, b1 * U)
+            if self.transactional:
+                self.apply_updates(inst[sl], oracle[sl], vals[sl], unique=True, _joined=True,
+                                   save=(sv_all[sl], sen_all[sl], st_all[sl]))
+            else:
+                self.apply_updates(inst[sl], oracle[sl], vals[sl], unique=True, _joined=True)
+
+        def rnd(k, b0, b1):
+            sl = slice(b0 * U, b1 * U)
+            rest = (inst[sl], oracle[sl], st_all[sl], sv_all[sl], sen_all[sl]) if self.transactional else None
+            self._run_round_range(b0, b1, restore=rest)
         if overlap:
             # range k lives on stream sc[k] alone (update, then round; the next step's update of range k
             # queues behind this round on the same stream: no cross-stream waits).  The streams start
@@ -223,11 +288,10 @@ class ConsensusEngine:
                 if fresh and k > 0:
                     sc[k].wait_stream(sc[k - 1])     # holds only range k-1's update at this point
                 with torch.cuda.stream(sc[k]):
-                    self.apply_updates(inst[b0 * U:b1 * U], oracle[b0 * U:b1 * U], vals[b0 * U:b1 * U],
-                                       unique=True, _joined=True)
+                    upd(k, b0, b1)
             for k, (b0, b1) in enumerate(ranges):
                 with torch.cuda.stream(sc[k]):
-                    self._run_round_range(b0, b1)
+                    rnd(k, b0, b1)
             # the side streams still read the caller's batch after this returns: hold it until the join
             # (after which the current stream is ordered behind every read, so the caching allocator may
             # hand its blocks out again)
@@ -240,11 +304,10 @@ class ConsensusEngine:
         su.wait_stream(cur)
         for k, (b0, b1) in enumerate(ranges):
             with torch.cuda.stream(su):
-                self.apply_updates(inst[b0 * U:b1 * U], oracle[b0 * U:b1 * U], vals[b0 * U:b1 * U], unique=True,
-                                   _joined=True)
+                upd(k, b0, b1)
             sc[k].wait_stream(su)
             with torch.cuda.stream(sc[k]):
-                self._run_round_range(b0, b1)
+                rnd(k, b0, b1)
         self.rounds += 1
         for s in self._pipe_streams:
             cur.wait_stream(s)
@@ -280,6 +343,17 @@ class ConsensusEngine:
             self._work = torch.empty(svops.fast_work_numel(self.B, self.D), dtype=torch.int32,
                                      device=self.device)
         return self._work
+
+    def net_stats(self) -> Dict[str, int]:
+        """Pruned window network counters (fp32 storage, N = 256; sortnet.hpp window_group_pruned):
+        ``slab_networks`` run so far (processed rounds x full 64-column slab steps x 4 waves) and the
+        ``fallbacks`` among them whose exact check failed (the full network reran for that wave)."""
+        self.pipeline_join()
+        if self._net_fb is None or not svops.pruned_window_applies(self.N, self.cfg.n_failing_oracles,
+                                                                  self.cfg.constrained, self.storage):
+            return {"slab_networks": 0, "fallbacks": 0}
+        processed = int(self.metrics_fx[2].item())
+        return {"slab_networks": processed * (self.D // 64) * 4, "fallbacks": int(self._net_fb.item())}
 
     def metrics(self) -> torch.Tensor:
         """[sum rel2 of committed rounds, committed, processed, reverted] as float64 (device)."""

@@ -76,3 +76,20 @@ def fast_work_applies(N: int, D: int, n_failing: int) -> bool:
     one (N <= 16 and D <= 128) keeps its window state and staged pass-2 outputs there."""
     return N > 16 or D > 128
 
+
+
+def fast_win_h(N: int, f: int) -> int:
+    """Window half-width of the one-network kernels (launch.hpp fast_win_h): 5, 17, or 0 (no window)."""
+    R = N - f
+    a = N // 2 - R // 2
+    if a + 1 <= 5 and f - a + 1 <= 5:
+        return 5
+    if a + 1 <= 17 and f - a + 1 <= 17:
+        return 17
+    return 0
+
+
+def pruned_window_applies(N: int, n_failing: int, constrained: bool, storage: str) -> bool:
+    """The fp32 window kernel's pruned network runs (N = 256, H = 17, constrained; csrc/kernels/
+    consensus_fast_winf.hip + sortnet.hpp window_group_pruned) -- on every full 64-column slab step."""
+    return storage == "fp32" and constrained and N == 256 and 0 <= n_failing <= 32 and fast_win_h(N, n_failing) == 17

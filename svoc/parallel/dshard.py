@@ -53,6 +53,12 @@ class _Shadow:
         self.kurt = torch.zeros_like(e.kurt)
         self.rel = torch.zeros_like(e.rel)
         self.reliable = torch.zeros_like(e.reliable)
+        # a deferred round's (active, local pass-2 status, global qr, c1): persistent buffers, so a HIP graph
+        # that captures a deferred round commits what the previous replay left here
+        self.p_active = torch.zeros_like(e._active)
+        self.p_status = torch.zeros_like(e.status)
+        self.p_qr = torch.zeros_like(e.qr)
+        self.p_c1 = torch.zeros_like(e.c1)
 
 
 def _pack(qr: torch.Tensor, prev: torch.Tensor, cur: torch.Tensor, rank: int, world: int) -> torch.Tensor:
@@ -135,8 +141,15 @@ def run_round_sharded(engine, d_global: int, group=None, world: int = 1, defer: 
     # pass 2 from the global qr on the instances every shard passed, into the shadow outputs
     half(2)
     if defer and world > 1:
-        # (active, local pass-2 status, global qr, c1): pass 1 of the next round rewrites the qr / c1 shadows
-        e._dshard_pending = (e._active.clone(), e.status.clone(), sh.qr.clone(), sh.c1.clone())
+        # (active, local pass-2 status, global qr, c1): pass 1 of the next round rewrites the qr / c1 shadows.
+        # A deferred round's verdict arrives after the next round has read the rows, so the transactional
+        # row restore (engine docstring) does not apply here: its update batches stay coalesced as stored.
+        e._pending_restore = []
+        sh.p_active.copy_(e._active)
+        sh.p_status.copy_(e.status)
+        sh.p_qr.copy_(sh.qr)
+        sh.p_c1.copy_(sh.c1)
+        e._dshard_pending = (sh.p_active, sh.p_status, sh.p_qr, sh.p_c1)
         e._dshard_ctx = (group, world)   # engine.pipeline_join (every state reader) commits it
         e.touched.zero_()
         e.rounds += 1
@@ -144,6 +157,8 @@ def run_round_sharded(engine, d_global: int, group=None, world: int = 1, defer: 
     if world > 1:
         dist.all_reduce(e.status, op=dist.ReduceOp.MAX, group=group)
     _commit(e, sh, e._active, e.status)
+    if e.mode == "fast":
+        e._restore_pending()    # every rank rolls back its column slice of the reverted instances' updates
     e.rounds += 1
 
 

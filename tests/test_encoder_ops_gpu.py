@@ -86,6 +86,42 @@ def test_encoder_fused_matches_cpu_fp32():
     torch.testing.assert_close(sg, sc, rtol=0, atol=0.05)
 
 
+@pytest.mark.parametrize("packed", [True, False])
+def test_encoder_oracle_vectors_match_cpu_fp32_bert_base(packed):
+    """The full BERT-base encoder (12 x 768, bf16 on the GPU: MFMA attention, fused embed / add + LN,
+    hipBLASLt GEMMs) against the fp32 CPU encoder of the same weights, on what the reference consumes:
+    the normalised 6-label oracle vectors (oracle_scheduler.py:20-40).  max |delta| <= 0.01."""
+    from svoc.models.encoder import build, scores_to_oracle_vectors
+    enc_g = build("cuda", torch.bfloat16, seed=11)
+    enc_g.packed = packed
+    enc_c = build("cpu", torch.float32, seed=11)
+    g = torch.Generator().manual_seed(5)
+    lens = torch.tensor([128, 40, 77, 128, 9, 100, 64, 1])
+    ids = torch.randint(3, enc_c.cfg.vocab_size, (8, 128), generator=g)
+    mask = (torch.arange(128)[None] < lens[:, None]).to(torch.int64)
+    with torch.no_grad():
+        vg = scores_to_oracle_vectors(enc_g(ids.cuda(), mask.cuda()).float().cpu())
+        vc = scores_to_oracle_vectors(enc_c(ids, mask))
+    err = (vg - vc).abs().max().item()
+    assert err <= 0.01, err
+
+
+def test_encoder_fp32_gpu_matches_cpu():
+    """The fp32 GPU encoder (bench.py's reference-precision c4 field: the padded path, ATen attention)
+    equals the CPU fp32 encoder to fp32 rounding."""
+    from svoc.models.encoder import build, scores_to_oracle_vectors
+    enc_g = build("cuda", torch.float32, seed=12)
+    enc_g.packed = False
+    enc_c = build("cpu", torch.float32, seed=12)
+    g = torch.Generator().manual_seed(6)
+    ids = torch.randint(3, enc_c.cfg.vocab_size, (4, 128), generator=g)
+    mask = (torch.arange(128)[None] < torch.tensor([128, 50, 3, 90])[:, None]).to(torch.int64)
+    with torch.no_grad():
+        vg = scores_to_oracle_vectors(enc_g(ids.cuda(), mask.cuda()).cpu())
+        vc = scores_to_oracle_vectors(enc_c(ids, mask))
+    assert (vg - vc).abs().max().item() <= 1e-4
+
+
 def test_attention_varlen_mfma():
     heads = 12
     lens = [128, 1, 33, 64, 95, 7, 128, 32]

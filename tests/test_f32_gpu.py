@@ -273,3 +273,70 @@ def test_f32_window_split_modes_match_whole_round():
         assert torch.equal(o["reliable"], whole["reliable"])
     for k in ("c1", "consensus"):
         assert torch.equal(torch.cat([outs[0][k], outs[1][k]], 1), whole[k]), k
+
+
+# ----------------------------------------------------------------------------------------------------
+# N = 256: the pruned window network (middle 32 keys per lane, exact check, full-network fallback per
+# wave: sortnet.hpp window_group_pruned).  Adversarial columns force the fallback; results stay exact.
+
+def _pruned_round(x, D, f):
+    B, N = x.shape[:2]
+    o = alloc_fast_out(B, N, D, DEV)
+    stats = torch.zeros(1, dtype=torch.int32, device=DEV)
+    svops.ops().fast_round(x, None, D, f, True, 1.0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"],
+                           o["qr"], o["reliable"], o["status"], 0, 0, 0, False, None, stats)
+    return o, stats
+
+
+@pytest.mark.parametrize("pattern", ["random", "sorted_rows", "one_lane_low", "ties", "signed_zero", "two_values"])
+def test_f32_pruned_window_exact(pattern):
+    B, N, D, f = 6, 256, 1024, 32
+    x = _f32(B, N, D, f, seed=77)[:, :, :D].contiguous()
+    if pattern == "sorted_rows":        # each column ascending in the row index: lane 0 holds the lowest 64
+        x = torch.sort(x, dim=1).values
+    elif pattern == "one_lane_low":     # rows 0..63 (segment 0) pushed below everything in half the columns
+        x[:, :64, ::2] *= 0.01
+    elif pattern == "ties":             # 9 distinct values per column: the window is full of ties
+        x = torch.round(x * 8) / 8
+    elif pattern == "signed_zero":      # many +0.0 / -0.0 around a low median
+        x = torch.where(x < 0.55, torch.zeros_like(x), x)
+        x[:, ::3] = -x[:, ::3]
+        x = torch.where(x < 0, torch.zeros_like(x), x)        # (-0.0 from the negation of +0.0 stays)
+        x[:, 1::3, 5] = -0.0
+    elif pattern == "two_values":
+        x = torch.where(x < 0.5, torch.full_like(x, 0.25), torch.full_like(x, 0.75))
+    xg = x.to(DEV)
+    o, stats = _pruned_round(xg, D, f)
+    ref = torch_ref.fast_round(xg, f, True, 1.0)
+    full = run_fast(xg, D, f, True, wave_hint=-7)          # the two-network kernel (no pruning)
+    torch.cuda.synchronize()
+    st = o["status"]
+    assert torch.equal(st, full["status"]), (st, full["status"])
+    ok = st == 0
+    if pattern != "two_values":
+        assert ok.all(), st
+    assert torch.equal(o["c1"][ok], ref["c1"].float()[ok])
+    assert torch.equal(o["reliable"][ok].bool(), ref["reliable"][ok])
+    assert torch.equal(o["consensus"][ok], ref["consensus"][ok])
+    assert torch.equal(o["consensus"][ok], full["consensus"][ok])
+    fb = int(stats.item())
+    slabs = B * (D // 64) * 4                                    # (instances x slab steps x waves)
+    if pattern == "random":
+        assert fb <= slabs // 20, (fb, slabs)                    # exchangeable rows: a few percent at most
+    if pattern in ("sorted_rows", "one_lane_low"):
+        assert fb > 0, fb                                        # the check must have caught these
+
+
+def test_f32_pruned_window_engine_counter():
+    """The engine passes its counter; c3-like random data falls back on < 5 % of the slab networks."""
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    cfg = ConsensusConfig(n_oracles=256, dimension=2048, n_failing_oracles=32, constrained=True)
+    e = ConsensusEngine(cfg, batch=16, device=DEV, mode="fast", storage="fp32")
+    e.randomize(seed=2)
+    e.run_round()
+    torch.cuda.synchronize()
+    assert (e.status == 0).all()
+    st = e.net_stats()
+    assert st["slab_networks"] == 16 * (2048 // 64) * 4
+    assert st["fallbacks"] <= 0.05 * st["slab_networks"], st

@@ -1,0 +1,136 @@
+"""Transactional fast streaming: a coalesced batch whose round reverts leaves no trace.
+
+The reference's update_prediction is one transaction -- store the prediction, then the consensus round;
+any failed assert of the round reverts the store too (contract.cairo:588-603 -> :442-503, :331-343).
+The fast engine coalesces a batch per instance, so a reverting round restores that instance's stored
+rows, ``enabled`` flags and ``n_active`` to their pre-batch state (the update kernels saved the rows
+they overwrote), and every update of the batch reports the round's code.  Instances whose round
+succeeds keep their updates.
+"""
+import pytest
+import torch
+
+from svoc.config import ConsensusConfig
+from svoc.engine import ConsensusEngine
+from svoc.status import Status
+
+DEVS = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+def _engine(dev, storage="fp32", N=64, D=256, f=8, B=4):
+    cfg = ConsensusConfig(n_oracles=N, dimension=D, n_failing_oracles=f, constrained=True)
+    return ConsensusEngine(cfg, batch=B, device=dev, mode="fast", storage=storage)
+
+
+def _snap(e):
+    e.pipeline_join()
+    return {k: getattr(e, k).clone() for k in ("values", "enabled", "n_active", "consensus", "rel", "skew", "kurt",
+                                               "reliable", "c1")}
+
+
+@pytest.mark.parametrize("dev", DEVS)
+@pytest.mark.parametrize("storage", ["fp32", "bf16"])
+def test_reverted_batch_restores_rows(dev, storage):
+    e = _engine(dev, storage)
+    e.randomize(seed=5)
+    e.run_round()
+    before = _snap(e)
+    N, D = e.N, e.D
+    # instance 2: every oracle -> one point (zero variance: the round reverts); instance 0: 3 fresh rows
+    inst = torch.tensor([2] * N + [0, 0, 0], device=dev)
+    orc = torch.cat([torch.arange(N), torch.tensor([5, 9, 11])]).to(dev)
+    vals = torch.full((N + 3, D), 0.5, device=dev)
+    vals[N:] = torch.rand(3, D, generator=torch.Generator().manual_seed(1)).to(dev)
+    st = e.step(inst, orc, vals)
+    e.pipeline_join()
+    if dev == "cuda":
+        torch.cuda.synchronize()
+    assert e.status[2].item() == int(Status.ZERO_VARIANCE) and e.status[0].item() == 0
+    assert st[:N].cpu().tolist() == [int(Status.ZERO_VARIANCE)] * N     # the tx status is the round's
+    assert st[N:].cpu().tolist() == [0, 0, 0]
+    after = _snap(e)
+    for k in ("values", "consensus", "rel", "skew", "kurt", "reliable", "c1"):
+        assert torch.equal(after[k][2], before[k][2]), k                # instance 2: no trace
+    assert torch.equal(after["enabled"], before["enabled"]) and torch.equal(after["n_active"], before["n_active"])
+    # instance 0 kept its updates; the untouched instances kept everything
+    assert torch.equal(after["values"][0, [5, 9, 11], :D], vals[N:].to(after["values"].dtype))
+    assert torch.equal(after["values"][1], before["values"][1]) and torch.equal(after["values"][3], before["values"][3])
+
+
+@pytest.mark.parametrize("dev", DEVS)
+def test_reverted_activation_restores_enabled_and_n_active(dev):
+    """The batch that activates an instance (first commit of every oracle) reverts: enabled / n_active
+    go back to zero, the rows to their constructor zeros (contract.cairo:106-120, 331-343)."""
+    e = _engine(dev, B=2)
+    N, D = e.N, e.D
+    inst = torch.zeros(N, dtype=torch.long, device=dev)
+    vals = torch.full((N, D), 0.25, device=dev)
+    st = e.step(inst, torch.arange(N, device=dev), vals)
+    e.pipeline_join()
+    assert e.status[0].item() == int(Status.ZERO_VARIANCE)
+    assert (st.cpu() == int(Status.ZERO_VARIANCE)).all()
+    assert e.n_active.cpu().tolist() == [0, 0] and int(e.enabled.sum()) == 0
+    assert int(e.values.abs().sum()) == 0
+    # an instance that does not become fully active keeps its stored rows (no round, no revert)
+    st2 = e.step(torch.ones(3, dtype=torch.long, device=dev), torch.tensor([0, 1, 2], device=dev),
+                 torch.full((3, D), 0.25, device=dev))
+    e.pipeline_join()
+    assert st2.cpu().tolist() == [0, 0, 0] and e.n_active.cpu().tolist() == [0, 3]
+
+
+@pytest.mark.parametrize("dev", DEVS)
+def test_two_batches_before_one_round(dev):
+    """Two apply_updates calls, one round: the revert restores the state from before the FIRST batch,
+    the same slot overwritten by both batches included."""
+    e = _engine(dev)
+    e.randomize(seed=9)
+    e.run_round()
+    before = _snap(e)
+    N, D = e.N, e.D
+    e.apply_updates(torch.full((N,), 1, device=dev), torch.arange(N, device=dev), torch.full((N, D), 0.75, device=dev))
+    e.apply_updates(torch.tensor([1, 1], device=dev), torch.tensor([3, 4], device=dev),
+                    torch.full((2, D), 0.75, device=dev))
+    e.run_round()
+    e.pipeline_join()
+    assert e.status[1].item() == int(Status.ZERO_VARIANCE)
+    after = _snap(e)
+    for k in before:
+        assert torch.equal(after[k], before[k]), k
+
+
+def test_non_transactional_keeps_rows():
+    """transactional=False: the round-3 behaviour (coalesced rows stay, outputs untouched)."""
+    e = _engine("cpu")
+    e.transactional = False
+    e.randomize(seed=5)
+    e.run_round()
+    N, D = e.N, e.D
+    e.step(torch.full((N,), 2), torch.arange(N), torch.full((N, D), 0.5))
+    assert e.status[2].item() == int(Status.ZERO_VARIANCE)
+    assert bool((e.values[2, :, :D] == 0.5).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("overlap", [False, True])
+def test_pipelined_step_restores_reverted_instances(overlap):
+    """step_pipelined (per-range update + round + restore on side streams) == step() on a batch where
+    some instances revert (eager and overlapped across steps)."""
+    N, D, B = 64, 512, 8
+    U = N                            # every oracle of every instance publishes
+    ref, pipe = _engine("cuda", N=N, D=D, B=B), _engine("cuda", N=N, D=D, B=B)
+    for e in (ref, pipe):
+        e.randomize(seed=3)
+        e.run_round()
+    g = torch.Generator(device="cuda").manual_seed(0)
+    inst = torch.arange(B, device="cuda").repeat_interleave(U)
+    orc = torch.stack([torch.randperm(N, device="cuda", generator=g) for _ in range(B)]).reshape(-1)
+    vals = torch.rand(B * U, D, device="cuda", generator=g)
+    vals[3 * U:4 * U] = 0.5          # instance 3: one point -> zero variance, the round reverts
+    ref.step(inst, orc, vals)
+    pipe.step_pipelined(inst, orc, vals, U, chunks=2, overlap=overlap)
+    pipe.pipeline_join()
+    torch.cuda.synchronize()
+    assert torch.equal(pipe.status, ref.status)
+    assert pipe.status[3].item() == int(Status.ZERO_VARIANCE) and int((pipe.status == 0).sum()) == B - 1
+    for k in ("values", "enabled", "n_active", "consensus", "rel", "c1"):
+        assert torch.equal(getattr(pipe, k), getattr(ref, k)), k

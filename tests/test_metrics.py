@@ -119,6 +119,23 @@ def test_bench_gpus_8_spawns_eight_ranks_gloo(tmp_path):
     assert all(o == 1.0 for o in c["rank_ok_fraction"]) and c["ok_fraction"] == 1.0
 
 
+def test_bench_gpus_8_dshard_gloo(tmp_path):
+    """`bench.py --gpus 8 --dshard` at world 8 on gloo: every rank holds a column slice (D = 64 over 8 ranks)
+    of the same 8 instances, one packed all-reduce per round, deferred commits, strong scaling."""
+    cfg = _cpu_cfg(tmp_path)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config-file", cfg, "--gpus", "8",
+                        "--dshard", "--steps", "3", "--warmup", "1"], capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    c = out["config"]
+    assert out["n_gpus"] == 8 and out["scaling"] == "strong" and c["parallelism"] == "dshard8"
+    assert c["backend_world"] == 8 and c["global_batch"] == 8 and len(c["rank_ms_per_step"]) == 8
+    assert c["ok_fraction"] == 1.0 and all(o == 1.0 for o in c["rank_ok_fraction"])
+    assert c["hip_graph"] is False            # (CPU ranks: no graphs)
+
+
 def test_bench_gpus_world_mismatch_fails(tmp_path):
     cfg = _cpu_cfg(tmp_path)
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
