@@ -216,6 +216,34 @@ void restore_updates_hip(at::Tensor values, at::Tensor enabled, at::Tensor n_act
   TORCH_CHECK(rc == 0, "svoc_restore_updates failed: ", rc);
 }
 
+void commit_updates_hip(const at::Tensor& rows, const at::Tensor& oracle, const at::Tensor& upd_status, at::Tensor values,
+                        int64_t upd_per_inst) {
+  TORCH_CHECK(values.dim() == 3 && values.stride(2) == 1 && values.stride(1) == values.size(2),
+              "values: [B, N, ld] with dense rows");
+  const int64_t n = oracle.numel();
+  TORCH_CHECK(rows.dim() == 2 && rows.size(0) == n && rows.is_contiguous() && rows.scalar_type() == values.scalar_type(),
+              "rows: contiguous [n, D] in the values' dtype");
+  TORCH_CHECK(oracle.scalar_type() == at::kLong && oracle.is_contiguous(), "oracle: contiguous int64 [n]");
+  TORCH_CHECK(upd_status.scalar_type() == at::kInt && upd_status.numel() == n, "upd_status: int32 [n]");
+  TORCH_CHECK(upd_per_inst > 0 && n <= values.size(0) * upd_per_inst, "upd_per_inst: rows b * U .. b * U + U - 1 "
+              "belong to instance b");
+  auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
+  const int rc = svoc_commit_updates(rows.data_ptr(), oracle.data_ptr<int64_t>(), upd_status.data_ptr<int32_t>(),
+                                     values.data_ptr(), values.stride(0), (int)values.size(1), (int)rows.size(1),
+                                     (int)values.size(2), (int)upd_per_inst, n, (int)values.element_size(), stream);
+  TORCH_CHECK(rc == 0, "svoc_commit_updates failed: ", rc);
+}
+
+void commit_updates_cpu(const at::Tensor& rows, const at::Tensor& oracle, const at::Tensor& upd_status, at::Tensor values,
+                        int64_t upd_per_inst) {
+  const int64_t n = oracle.numel(), D = rows.size(1);
+  auto o = oracle.accessor<int64_t, 1>();
+  auto st = upd_status.accessor<int32_t, 1>();
+  for (int64_t u = 0; u < n; ++u)
+    if (st[u] == ST_OK && o[u] >= 0 && o[u] < values.size(1))
+      values[u / upd_per_inst][o[u]].narrow(0, 0, D).copy_(rows[u]);
+}
+
 }  // namespace
 
 void register_extra_defs(torch::Library& m) {
@@ -226,6 +254,7 @@ void register_extra_defs(torch::Library& m) {
   m.def(
       "restore_updates(Tensor(a!) values, Tensor(b!) enabled, Tensor(c!) n_active, Tensor inst, Tensor oracle, "
       "Tensor(d!) upd_status, Tensor saved, Tensor saved_en, Tensor status, Tensor active) -> ()");
+  m.def("commit_updates(Tensor rows, Tensor oracle, Tensor upd_status, Tensor(a!) values, int upd_per_inst) -> ()");
   register_governance_defs(m);
   register_generator_defs(m);
   register_io_defs(m);
@@ -236,6 +265,7 @@ void register_extra_defs(torch::Library& m) {
 void register_extra_cpu(torch::Library& m) {
   m.impl("apply_updates", &apply_updates_cpu);
   m.impl("restore_updates", &restore_updates_cpu);
+  m.impl("commit_updates", &commit_updates_cpu);
   register_governance_cpu(m);
   register_generator_cpu(m);
   register_bookkeeping_cpu(m);
@@ -245,6 +275,7 @@ void register_extra_cpu(torch::Library& m) {
 void register_extra_hip(torch::Library& m) {
   m.impl("apply_updates", &apply_updates_hip);
   m.impl("restore_updates", &restore_updates_hip);
+  m.impl("commit_updates", &commit_updates_hip);
   register_governance_hip(m);
   register_generator_hip(m);
   register_bookkeeping_hip(m);

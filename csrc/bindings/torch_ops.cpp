@@ -63,10 +63,16 @@ void fast_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& a
                     int64_t n_failing, bool constrained, double max_spread, at::Tensor c1, at::Tensor cons,
                     at::Tensor skew, at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable,
                     at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim, bool legacy,
-                    const c10::optional<at::Tensor>& work, const c10::optional<at::Tensor>& stats) {
+                    const c10::optional<at::Tensor>& work, const c10::optional<at::Tensor>& stats,
+                    const c10::optional<at::Tensor>& upd_rows, const c10::optional<at::Tensor>& upd_oracle,
+                    const c10::optional<at::Tensor>& upd_status, int64_t upd_per_inst) {
   (void)wave_hint;
   (void)work;
   (void)stats;   // (GPU pruned-network counter; the CPU twin runs full sorts)
+  TORCH_CHECK(!upd_rows.has_value() || !upd_rows->defined(), "fused transactional streaming is a GPU path");
+  (void)upd_oracle;
+  (void)upd_status;
+  (void)upd_per_inst;
   fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
   const int64_t B = values.size(0), N = values.size(1), ld = values.size(2), is = values.stride(0);
   TORCH_CHECK(values.scalar_type() == at::kBFloat16 || values.scalar_type() == at::kFloat,
@@ -111,7 +117,9 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
                     int64_t n_failing, bool constrained, double max_spread, at::Tensor c1, at::Tensor cons,
                     at::Tensor skew, at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable,
                     at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim, bool legacy,
-                    const c10::optional<at::Tensor>& work, const c10::optional<at::Tensor>& stats) {
+                    const c10::optional<at::Tensor>& work, const c10::optional<at::Tensor>& stats,
+                    const c10::optional<at::Tensor>& upd_rows, const c10::optional<at::Tensor>& upd_oracle,
+                    const c10::optional<at::Tensor>& upd_status, int64_t upd_per_inst) {
   fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
   TORCH_CHECK(values.scalar_type() == at::kBFloat16 || values.scalar_type() == at::kFloat,
               "GPU fast path stores values in bf16 or fp32");
@@ -187,6 +195,23 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
     TORCH_CHECK(stats->scalar_type() == at::kInt && stats->numel() >= 1 && stats->device() == values.device(),
                 "stats: int32 [>= 1] on the values' device ([0] += pruned-network fallbacks)");
     p.net_fallbacks = (unsigned int*)stats->data_ptr();
+  }
+  if (upd_rows.has_value() && upd_rows->defined()) {
+    TORCH_CHECK(f32 && mode == 0 && constrained, "fused streaming: fp32 storage, whole constrained rounds");
+    TORCH_CHECK(upd_per_inst > 0 && upd_oracle.has_value() && upd_status.has_value(), "fused streaming: "
+                "upd_oracle, upd_status and upd_per_inst > 0 go with upd_rows");
+    const int64_t n = B * upd_per_inst;
+    TORCH_CHECK(upd_rows->scalar_type() == at::kFloat && upd_rows->is_contiguous() && upd_rows->dim() == 2 &&
+                    upd_rows->size(0) == n && upd_rows->size(1) == D && upd_rows->device() == values.device(),
+                "upd_rows: contiguous fp32 [B * U, D] on the values' device");
+    TORCH_CHECK(upd_oracle->scalar_type() == at::kLong && upd_oracle->is_contiguous() && upd_oracle->numel() == n,
+                "upd_oracle: contiguous int64 [B * U]");
+    TORCH_CHECK(upd_status->scalar_type() == at::kInt && upd_status->is_contiguous() && upd_status->numel() == n,
+                "upd_status: contiguous int32 [B * U]");
+    p.upd_rows = upd_rows->data_ptr<float>();
+    p.upd_oracle = upd_oracle->data_ptr<int64_t>();
+    p.upd_status = upd_status->data_ptr<int32_t>();
+    p.upd_per_inst = (int)upd_per_inst;
   }
   const int rc = f32 ? svoc_fast_round_f32(&p, stream) : svoc_fast_round_bf16(&p, stream);
   TORCH_CHECK(rc == 0, f32 ? "svoc_fast_round_f32" : "svoc_fast_round_bf16", " launch failed: ", rc);
@@ -307,7 +332,8 @@ TORCH_LIBRARY(svoc, m) {
       "fast_round(Tensor values, Tensor? active, int D, int n_failing, bool constrained, float max_spread, "
       "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "
       "Tensor(g!) reliable, Tensor(h!) status, int wave_hint=0, int mode=0, int rel_dim=0, bool legacy=False, "
-      "Tensor? work=None, Tensor(i!)? stats=None) -> ()");
+      "Tensor? work=None, Tensor(i!)? stats=None, Tensor? upd_rows=None, Tensor? upd_oracle=None, "
+      "Tensor(j!)? upd_status=None, int upd_per_inst=0) -> ()");
   m.def(
       "exact_round(Tensor values, Tensor? active, int n_failing, bool constrained, int max_spread, "
       "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "

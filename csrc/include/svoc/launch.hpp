@@ -39,6 +39,16 @@ struct FastParams {
   // optional counter: slab networks of the pruned window path (N = 256) that failed their exact check and
   // reran the full network (consensus_fast_winf.hip); null = not counted
   unsigned int* net_fallbacks;
+  // Fused transactional streaming (fp32 window kernel, mode 0; null upd_rows = off): this launch's update
+  // batch, `upd_per_inst` rows per instance in instance order ([B * U, D] fp32, pitch D, row b * U + k for
+  // instance b; upd_oracle [B * U] their oracles, distinct per instance).  The round reads an updated oracle's
+  // row from the batch instead of the state (the state is not written), validates it, and writes every
+  // update's transaction status to upd_status: OK (commit: svoc_commit_updates copies the row), the round's
+  // revert code, or INTERVAL_INPUT for a row outside [0, 1] (the round is recomputed without it).
+  const float* upd_rows;
+  const int64_t* upd_oracle;
+  int32_t* upd_status;
+  int upd_per_inst;
 };
 
 // Workspace per instance of the LDS-free fast kernels, in u32 words (Dp = fast_work_pairs(D)).
@@ -162,6 +172,11 @@ struct RestoreParams {
 
 extern "C" int svoc_apply_updates(const svoc::UpdateParams* p, hipStream_t stream);
 extern "C" int svoc_restore_updates(const svoc::RestoreParams* p, hipStream_t stream);
+// Commit of a fused transactional step (FastParams.upd_rows): update u's row -> values[u / U, oracle[u]] where
+// upd_status[u] is OK (set by the round kernel).  rows [Btot * U, D] (elem_bytes each), values [Btot, N, ld].
+extern "C" int svoc_commit_updates(const void* rows, const int64_t* oracle, const int32_t* upd_status, void* values,
+                                   int64_t inst_stride, int N, int D, int ld, int U, int64_t n_upd, int elem_bytes,
+                                   hipStream_t stream);
 // row b of src -> dst (words 4-byte words per row) where status[b] == OK and (active null or set)
 extern "C" int svoc_commit_rows(const void* src, void* dst, const int32_t* status, const uint8_t* active, int64_t B,
                                 int64_t words, hipStream_t stream);

@@ -28,10 +28,15 @@ template <int NSEG>
 struct SlabDma {
   static constexpr int P = 64 / NSEG, CPR = P / 4, RPI = 64 / CPR;
   int vlane;   // this lane's part of every piece's voffset
+  int row0;    // global row this lane loads in piece 0 (piece k: row0 + k * RPI / NSEG)
+  int colb;    // this lane's byte offset within the row piece
   SVOC_DEV SlabDma(int lane, int rowb) {
     const int j = lane / CPR;   // LDS row of the piece this lane fills
-    vlane = ((j % NSEG) * 64 + j / NSEG) * rowb + (lane % CPR) * 16;
+    row0 = (j % NSEG) * 64 + j / NSEG;
+    colb = (lane % CPR) * 16;
+    vlane = row0 * rowb + colb;
   }
+  SVOC_DEV int row_of(int k) const { return row0 + k * (RPI / NSEG); }
   // issue this wave's 16 pieces of the slab whose first word (of this wave: an fp32 column, a bf16 column
   // pair) is col0.  Inline asm: the
   // __builtin_amdgcn_raw_ptr_buffer_load_lds form crashes ROCm 7.2's instruction selection in this
@@ -51,6 +56,42 @@ struct SlabDma {
           : "=&s"(keep)
           : "v"(vo), "s"(rs.w), "s"(lds), "s"(k * (RPI / NSEG) * rowb)
           : "memory");
+    }
+  }
+  // The same slab, with per-piece row sources (fused transactional streaming): piece k is issued twice
+  // under complementary exec masks -- the lanes whose row comes from the update batch (bit k of
+  // `from_batch`) read byte offset off_b(k) of rb, the others off_s(k) of the state rs.  The masks are
+  // switched inside the asm (exec restored before it ends), so the compiler sees no divergent control
+  // flow around the loads (which cost the kernel ~27 spilled VGPRs when written as if / else).
+  template <class OffS, class OffB>
+  SVOC_DEV void issue_mapped(const BufDesc& rs, const BufDesc& rb, uint32_t* region, OffS off_s, OffB off_b,
+                             uint32_t from_batch) const {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(region + k * 256);
+      const int vs = off_s(k), vb = off_b(k);
+      const uint32_t fb = (from_batch >> k) & 1u;
+      int keep;
+      uint64_t sx;
+      // (the exec masks come from a compare inside the asm: ballots outside it were scheduled early and
+      // held as 16 SGPR pairs -- hundreds of spilled SGPRs; s_nop 4: VALU-written VCC read by SALU)
+      asm volatile(
+          "s_mov_b32 %0, m0\n\t"
+          "s_mov_b32 m0, %7\n\t"
+          "s_mov_b64 %1, exec\n\t"
+          "v_cmp_ne_u32 vcc, 0, %4\n\t"
+          "s_nop 4\n\t"
+          "s_andn2_b64 exec, %1, vcc\n\t"
+          "s_nop 0\n\t"
+          "buffer_load_dwordx4 %2, %5, 0 offen lds\n\t"
+          "s_and_b64 exec, %1, vcc\n\t"
+          "s_nop 0\n\t"
+          "buffer_load_dwordx4 %3, %6, 0 offen lds\n\t"
+          "s_mov_b64 exec, %1\n\t"
+          "s_mov_b32 m0, %0"
+          : "=&s"(keep), "=&s"(sx)
+          : "v"(vs), "v"(vb), "v"(fb), "s"(rs.w), "s"(rb.w), "s"(lds)
+          : "vcc", "memory");
     }
   }
 };

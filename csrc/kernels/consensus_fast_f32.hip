@@ -521,6 +521,7 @@ extern "C" int svoc_fast_round_f32(const FastParams* p, hipStream_t stream) {
     const int rc = svoc_fast_round_f32_win(p, stream);
     if (rc != -2) return rc;
   }
+  if (p->upd_rows) return -3;   // fused transactional streaming exists in the window kernel only
   int rc;
   if (p->N <= 64) rc = launch_f32<1>(*p, stream);
   else if (p->N <= 128) rc = launch_f32<2>(*p, stream);

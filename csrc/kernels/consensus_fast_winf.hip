@@ -157,7 +157,7 @@ SVOC_DEV bool try_pruned(uint32_t (&r)[64], int seg, int lane, uint32_t (&w)[WN]
 // network, window, c1 and qr pass run on the registers while it lands.  2 waves per SIMD (<= 256
 // VGPRs: 64 keys + 64 raw rows + the window), LDS = WAVES x 16 KiB.
 
-template <int NSEG, int WAVES, int H, bool CONS, int MODE>
+template <int NSEG, int WAVES, int H, bool CONS, int MODE, bool FUSED = false>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2))) void consensus_fast_winf_kernel(FastParams p) {
   constexpr int P = 64 / NSEG;          // columns per wave (phase A)
   constexpr int NPAD = 64 * NSEG;
@@ -173,9 +173,20 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
   __shared__ float misc_f[2];
   __shared__ int misc_i[3];     // status, zero-variance flag, cleanup list length
   __shared__ uint32_t redo[128];   // constrained, D <= 4096: the cleanup columns as a bit mask
+  // fused transactional streaming (FastParams.upd_rows): row -> its update's slot in this instance's batch
+  // (-1: the state row), and the slots whose row failed the interval check
+  __shared__ int smap[FUSED ? NPAD : 1];
+  __shared__ uint32_t badu[8];
 
   const int b = blockIdx.x;
-  if (p.active && !p.active[b]) return;
+  static_assert(!FUSED || (MODE == 0 && CONS), "fused streaming: whole constrained rounds");
+  constexpr bool fused = FUSED;
+  const int U = fused ? p.upd_per_inst : 0;
+  if (p.active && !p.active[b]) {
+    // (the fused path runs only when every instance is active; an inactive one would not commit)
+    for (int t = threadIdx.x; t < U; t += WAVES * 64) p.upd_status[(int64_t)b * U + t] = ST_NOT_ACTIVE;
+    return;
+  }
   // (wave made explicitly uniform: it feeds the DMA's M0 and SGPR row offsets)
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (tid < 32) urow[tid] = 0;  // f < 32: unused slots still name a valid row
@@ -195,6 +206,35 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
   const int MOM = 2 * H * Dc * 4;
   const int LST = MOM + 4 * Dc * 4;
   const int STG = Dc * kWinfStageCols * 4;
+  // the batch rows of this instance's updates ([U, D], pitch D): rows being updated this round are read
+  // from here, the state keeps the committed rows until svoc_commit_updates copies the accepted ones
+  const float* urows = fused ? p.upd_rows + (int64_t)b * U * D : inst;
+  const uint32_t ubytes = fused ? (uint32_t)(U * D * 4) : 0u;
+  const __amdgpu_buffer_rsrc_t rb = instance_rsrc(urows, ubytes);
+  const BufDesc rbd = buf_desc(urows, ubytes);
+  if constexpr (FUSED) {
+    for (int t = tid; t < NPAD; t += NT) smap[t] = -1;
+  }
+  if (tid < 8) badu[tid] = 0u;
+  __syncthreads();
+  if (fused)
+    for (int t = tid; t < U; t += NT) {
+      const int64_t o = p.upd_oracle[(int64_t)b * U + t];
+      if (o >= 0 && o < N) smap[o] = t;
+    }
+  __syncthreads();
+  // one value of row `row` (wave-uniform) at byte offset `cb` of the row: batch or state
+  auto row_load = [&](int row, int cb) __attribute__((always_inline)) -> uint32_t {
+    int u = -1;
+    if constexpr (FUSED) u = __builtin_amdgcn_readfirstlane(smap[row]);
+    return u >= 0 ? bload(rb, cb, u * D * 4) : bload(rs, cb, row * rowb);
+  };
+  auto bad_slot = [&](int u) __attribute__((always_inline)) { return (badu[u >> 5] >> (u & 31)) & 1u; };
+  // every update's transaction status once the round's outcome is known (contract.cairo:588-603)
+  auto upd_out = [&](int st) __attribute__((always_inline)) {
+    if (fused)
+      for (int t = tid; t < U; t += NT) p.upd_status[(int64_t)b * U + t] = bad_slot(t) ? ST_INTERVAL_INPUT : st;
+  };
   const int lo1 = (NPAD - N + 1) >> 1;
   const int nv = N - seg * 64;
   const int nl = N + lo1 - seg * 64;
@@ -219,7 +259,44 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
   uint32_t* const region = slab + (PASS1 ? wave * 64 * 64 : 0);
   // this lane's words: global row seg * 64 + i at LDS row NSEG * i + seg, i.e. word 64 i + seg P + cw
   const uint32_t* const mine = region + (PASS1 ? seg * P + cw : 0);
-  if (pass1_slabs > 0) dma.issue(rsd, region, rowb, wave * P);
+  // fused: per-piece row sources of this lane's DMA, packed 4 per register (byte k % 4 of pmap[k / 4] =
+  // batch slot + 1 of the piece's row, 0 = the state row); offsets formed at issue
+  uint32_t pmap[FUSED ? 4 : 1] = {};
+  auto map_pieces = [&]() __attribute__((always_inline)) {
+    if constexpr (FUSED) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int row = dma.row_of(k);
+        const int u = row < N ? smap[row] : -1;
+        if (k % 4 == 0) pmap[k / 4] = 0u;
+        pmap[k / 4] |= (uint32_t)(u + 1) << (8 * (k % 4));
+      }
+    }
+  };
+  auto issue_slab = [&](int s) __attribute__((always_inline)) {
+    if constexpr (FUSED) {
+      const int cb = (s * W + wave * P) * 4 + dma.colb;
+      // (opaque per slab: the masks and offsets derived from the map are loop-invariant, and hoisted out of
+      // the slab loop they take 32+ SGPRs for the whole phase -- spills)
+      uint32_t pm[4] = {pmap[0], pmap[1], pmap[2], pmap[3]};
+      asm volatile("" : "+v"(pm[0]), "+v"(pm[1]), "+v"(pm[2]), "+v"(pm[3]));
+      int rowb_o = rowb, d4 = D * 4;
+      asm volatile("" : "+s"(rowb_o), "+s"(d4));
+      uint32_t* reg_o = region;
+      asm volatile("" : "+s"(reg_o));
+      uint32_t pfrom = 0u;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) pfrom |= (((pm[k / 4] >> (8 * (k % 4))) & 0xffu) ? 1u : 0u) << k;
+      dma.issue_mapped(
+          rsd, rbd, reg_o, [&](int k) { return dma.row_of(k) * rowb_o + cb; },
+          [&](int k) { return ((int)((pm[k / 4] >> (8 * (k % 4))) & 0xffu) - 1) * d4 + cb; }, pfrom);
+    } else {
+      dma.issue(rsd, region, rowb, s * W + wave * P);
+    }
+  };
+  for (int attempt = 0; attempt < 2; ++attempt) {   // (a second pass only when a fused update was invalid)
+  if (fused) map_pieces();
+  if (pass1_slabs > 0) issue_slab(0);
   // One slab of phase A.  FULL: every column of the slab is < D and N = NPAD, so no masks at all; the
   // masked form serves the tail slab and padded N.  (One body per loop: reading the raw rows in two
   // branches of one loop makes the compiler demote them to scratch.)
@@ -239,7 +316,27 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       xs.hi[i] = mine[(i + 32) * 64];
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0): the region is read, the next slab may land
-    if (s + 1 < pass1_slabs) dma.issue(rsd, region, rowb, (s + 1) * W + wave * P);
+    if (s + 1 < pass1_slabs) issue_slab(s + 1);
+    if (fused) {
+      // interval check of the batch rows (contract.cairo:591-593, math.cairo:298-310): the maximum raw
+      // word of the lane's rows (state rows were checked when stored) against 1.0f; past it (or -0.0
+      // somewhere) the batch rows are checked one by one and a failing slot is marked
+      uint32_t mx = 0u;
+#pragma unroll
+      for (int i = 0; i < 64; i += 2) mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(xs.at(i), xs.at(i + 1)));
+      if (__ballot(mx > 0x3f800000u) != 0) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          const int row = seg * 64 + i;
+          const uint32_t raw = xs.at(i);
+          if (vc && row < N && !(raw <= 0x3f800000u || raw == 0x80000000u)) {
+            int u = -1;
+            if constexpr (FUSED) u = smap[row];
+            if (u >= 0) atomicOr(&badu[u >> 5], 1u << (u & 31));
+          }
+        }
+      }
+    }
     {
       uint32_t r[64];
       auto build_keys = [&](uint32_t kpx) __attribute__((always_inline)) {
@@ -331,6 +428,24 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
 #pragma nounroll
     for (int s = nfull; s < pass1_slabs; ++s) slab_body(std::false_type{}, s);
   }
+  if (!fused) break;
+  __syncthreads();
+  uint32_t anybad = 0u;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) anybad |= badu[w];
+  if (anybad == 0u || attempt == 1) break;
+  // an update row failed the interval check: its transaction reverts alone (INTERVAL_INPUT) and the round
+  // is recomputed on the state row instead (the other updates of the batch stand)
+  if constexpr (FUSED) {
+    for (int t = tid; t < NPAD; t += NT)
+      if (smap[t] >= 0 && bad_slot(smap[t])) smap[t] = -1;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < (ACC64 ? 32 : 1); ++i) acc[i] = f32x2{0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < KEEP; ++i) keep[i] = 0.f;
+  }   // attempts
 
   if (net_fallbacks && lane == 0 && p.net_fallbacks) atomicAdd(p.net_fallbacks, (unsigned)net_fallbacks);
   // ------------------------------------------------------------ qr reduction
@@ -435,6 +550,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
   __syncthreads();
   if (misc_i[0] != ST_OK) {
     if (tid == 0) p.status[b] = misc_i[0];
+    upd_out(misc_i[0]);
     return;
   }
 
@@ -460,10 +576,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
         cand = cand && fkey_val<true>(lo) == fkey_val<true>(hi);
       }
       if (__ballot(cand)) {   // rare: compare the reliable rows with the first one
-        const float r0 = u2f(bload(rs, pc * 4, fr * rowb));
+        const float r0 = u2f(row_load(fr, pc * 4));
         for (int i = fr + 1; i < N; ++i) {
           if (!((relmask[i >> 6] >> (i & 63)) & 1)) continue;   // uniform
-          cand = cand && u2f(bload(rs, pc * 4, i * rowb)) == r0;
+          cand = cand && u2f(row_load(i, pc * 4)) == r0;
         }
         zv = zv || cand;
       }
@@ -472,6 +588,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     __syncthreads();
     if (misc_i[1]) {
       if (tid == 0) p.status[b] = ST_ZERO_VARIANCE;
+      upd_out(ST_ZERO_VARIANCE);
       return;
     }
   }
@@ -515,7 +632,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       const int row = t - s0;
       const bool real = (realm >> t) & 1;
       q.uw[t] = 0u;
-      if (CONS || real) q.uw[t] = bload(rs, vo, __builtin_amdgcn_readfirstlane(urow[real ? row : 0]) * rowb);
+      if (CONS || real) q.uw[t] = row_load(__builtin_amdgcn_readfirstlane(urow[real ? row : 0]), vo);
     }
     if constexpr (CONS) {
 #pragma unroll
@@ -657,7 +774,13 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       for (int g = 0; g < NSEG; ++g) {
         const int i = g * 64 + lane;
         const bool use = i < N && ((relmask[g] >> lane) & 1);
-        y[g] = use ? xc[(int64_t)i * p.ld] - cc : 0.f;
+        float xv = 0.f;
+        if (use) {
+          int u = -1;
+          if constexpr (FUSED) u = smap[i];
+          xv = u >= 0 ? urows[(int64_t)u * D + col] : xc[(int64_t)i * p.ld];
+        }
+        y[g] = use ? xv - cc : 0.f;
         t1 += y[g];
       }
       t1 += xor_lane<1>(t1); t1 += xor_lane<2>(t1); t1 += xor_lane<4>(t1);
@@ -760,10 +883,18 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     p.rel[2 * (int64_t)b + 1] = misc_f[1];
     p.status[b] = ST_OK;
   }
+  upd_out(ST_OK);
 }
 
 template <int NSEG, int WAVES, int H, bool CONS>
 static void launch_winf_w(const FastParams& p, hipStream_t stream) {
+  if constexpr (CONS) {
+    if (p.upd_rows) {   // fused transactional streaming (mode 0)
+      hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 0, true>), dim3(p.B), dim3(WAVES * 64), 0,
+                         stream, p);
+      return;
+    }
+  }
   if (p.mode == 1) hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 1>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   else if (p.mode == 2) hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 2>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   else hipLaunchKernelGGL((consensus_fast_winf_kernel<NSEG, WAVES, H, CONS, 0>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
@@ -796,6 +927,9 @@ extern "C" int svoc_fast_round_f32_win(const FastParams* p, hipStream_t stream) 
   if (!p->work || p->N < 2 || p->N > 256 || p->D > p->ld) return -2;
   if ((int64_t)p->N * p->ld * 4 >= (1ll << 31)) return -2;
   if (p->mode == 2 && p->work_fresh) return -2;   // pass 1 ran elsewhere: no windows to read
+  if (p->upd_rows && (p->mode != 0 || !p->constrained || p->upd_per_inst <= 0 || p->upd_per_inst > 256 ||
+                      (int64_t)p->upd_per_inst * p->D * 4 >= (1ll << 31)))
+    return -3;
   if (p->n_failing < 0 || p->n_failing > 32 || p->n_failing > p->N - 2) return -2;
   const int H = fast_win_h(p->N, p->n_failing);
   if (H == 0) return -2;

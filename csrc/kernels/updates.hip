@@ -356,6 +356,57 @@ static int launch_restore(const RestoreParams& p, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+
+// Commit of a fused transactional step: the round kernel read the updated rows from the batch and wrote
+// every update's transaction status; the accepted rows (status OK) are copied into the state here, one
+// update per L lanes, the row's 16-B chunks loaded together (non-temporal: read once) and stored.
+template <int L, int RB>
+__global__ __launch_bounds__(256) void upd_commit_kernel(const unsigned char* __restrict__ rows,
+                                                         const int64_t* __restrict__ oracle,
+                                                         const int32_t* __restrict__ upd_status,
+                                                         unsigned char* __restrict__ values, int64_t inst_stride,
+                                                         int N, int D, int ld, int U, int64_t n_upd, int elem_bytes) {
+  const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
+  const int sub = threadIdx.x & (L - 1);
+  if (u >= n_upd || upd_status[u] != ST_OK) return;
+  const int64_t o = oracle[u];
+  if (o < 0 || o >= N) return;
+  const int64_t b = u / U;
+  const int64_t row_bytes = (int64_t)D * elem_bytes;
+  const unsigned char* src = rows + u * row_bytes;
+  unsigned char* dst = values + (b * inst_stride + o * ld) * elem_bytes;
+  const int64_t nch = row_bytes / 16;
+  if ((row_bytes & 15) == 0 && (((uintptr_t)src | (uintptr_t)dst) & 15) == 0 && nch <= (int64_t)RB * L) {
+    u32x4 v[RB];
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const int64_t i = sub + (int64_t)k * L;
+      v[k] = i < nch ? __builtin_nontemporal_load((const u32x4*)src + i) : u32x4{0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const int64_t i = sub + (int64_t)k * L;
+      if (i < nch) ((u32x4*)dst)[i] = v[k];
+    }
+  } else {
+    for (int64_t i = sub; i < row_bytes; i += L) dst[i] = src[i];
+  }
+}
+
+template <int L>
+static int launch_commit(const void* rows, const int64_t* oracle, const int32_t* st, void* values, int64_t inst_stride,
+                         int N, int D, int ld, int U, int64_t n_upd, int eb, hipStream_t stream) {
+  const int64_t blocks = (n_upd * L + 255) / 256;
+  const int64_t nch = (int64_t)D * eb / 16;
+  if (nch > 8 * L)
+    hipLaunchKernelGGL((upd_commit_kernel<L, 16>), dim3((unsigned)blocks), dim3(256), 0, stream,
+                       (const unsigned char*)rows, oracle, st, (unsigned char*)values, inst_stride, N, D, ld, U, n_upd, eb);
+  else
+    hipLaunchKernelGGL((upd_commit_kernel<L, 8>), dim3((unsigned)blocks), dim3(256), 0, stream,
+                       (const unsigned char*)rows, oracle, st, (unsigned char*)values, inst_stride, N, D, ld, U, n_upd, eb);
+  return (int)hipGetLastError();
+}
+
 }  // namespace svoc
 
 using namespace svoc;
@@ -376,4 +427,15 @@ extern "C" int svoc_apply_updates(const UpdateParams* p, hipStream_t stream) {
 extern "C" int svoc_restore_updates(const RestoreParams* p, hipStream_t stream) {
   if (p->U <= 0) return 0;
   return launch_restore(*p, stream);
+}
+
+extern "C" int svoc_commit_updates(const void* rows, const int64_t* oracle, const int32_t* upd_status, void* values,
+                                   int64_t inst_stride, int N, int D, int ld, int U, int64_t n_upd, int elem_bytes,
+                                   hipStream_t stream) {
+  if (n_upd <= 0) return 0;
+  if (U <= 0 || n_upd * 64 / 256 >= 0x7fffffffll) return -1;
+  const int64_t chunks = ((int64_t)D * elem_bytes + 15) / 16;
+  if (chunks <= 4) return launch_commit<4>(rows, oracle, upd_status, values, inst_stride, N, D, ld, U, n_upd, elem_bytes, stream);
+  if (chunks <= 16) return launch_commit<16>(rows, oracle, upd_status, values, inst_stride, N, D, ld, U, n_upd, elem_bytes, stream);
+  return launch_commit<64>(rows, oracle, upd_status, values, inst_stride, N, D, ld, U, n_upd, elem_bytes, stream);
 }

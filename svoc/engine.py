@@ -176,6 +176,7 @@ class ConsensusEngine:
     def _restore(self, entries, status=None) -> None:
         """Roll back the saved updates of the instances whose round ran and reverted (latest batch first)."""
         status = self.status if status is None else status
+        self._all_active = False   # (a reverted first commit lowers n_active: the fused path re-checks)
         for inst, oracle, st, saved, saved_en in reversed(entries):
             self._ops.restore_updates(self.values, self.enabled, self.n_active, inst, oracle, st, saved, saved_en,
                                       status, self._active)
@@ -228,6 +229,50 @@ class ConsensusEngine:
         self._ops.round_epilogue(self._active[sl], self.status[sl], self.rel[sl], self.consensus_active[sl],
                                  self.touched[sl], self.metrics_fx)
 
+    def _fused_ok(self, inst, oracle, vals, U: int) -> bool:
+        """Whether a pipelined step can take the fused transactional path: fp32 storage on the GPU, whole
+        constrained rounds through the window kernel (N <= 256, f <= 32), at most 256 updates per instance
+        (instance-grouped batch, as step_pipelined requires), fp32 rows of exactly D columns, and every
+        instance already active (the fused round covers no activation; checked once, then tracked)."""
+        if not (self.mode == "fast" and self.device.type == "cuda" and self.vdtype == torch.float32
+                and self.cfg.constrained and 2 <= self.N <= 256 and 0 <= self.cfg.n_failing_oracles <= 32
+                and self.cfg.n_failing_oracles <= self.N - 2 and svops.fast_win_h(self.N, self.cfg.n_failing_oracles)
+                and 0 < U <= 256 and vals.dtype == torch.float32 and vals.dim() == 2 and vals.shape[1] == self.D
+                and oracle.dtype == torch.int64 and not self.cfg.legacy):
+            return False
+        if not getattr(self, "_all_active", False):
+            if torch.cuda.is_current_stream_capturing():
+                return False
+            self._all_active = bool((self.n_active == self.N).all())
+        return self._all_active
+
+    def _status_buffer(self, U: int) -> torch.Tensor:
+        buf = self._save_bufs.get(("st",))
+        if buf is None or buf.shape[0] < U:
+            buf = torch.empty(U, dtype=torch.int32, device=self.device)
+            self._save_bufs[("st",)] = buf
+        return buf[:U]
+
+    def _run_round_range_fused(self, b0: int, b1: int, oracle: torch.Tensor, rows: torch.Tensor, st: torch.Tensor,
+                               U: int) -> None:
+        """Fused transactional round over instances [b0, b1): every instance is active and each has U
+        updates (rows b * U ..); the window kernel reads the updated rows from `rows`, writes each update's
+        transaction status to `st`, and the commit kernel stores the accepted rows (a reverted round's rows
+        never reach the state)."""
+        sl = slice(b0, b1)
+        self._ops.round_prologue(self.n_active[sl], self.touched[sl], self.N, False, self._active[sl])
+        w = self.work()
+        words = w.numel() // self.B
+        w = w[b0 * words:b1 * words]
+        self._ops.fast_round(self.values[sl], self._active[sl], self.D, self.cfg.n_failing_oracles,
+                             self.cfg.constrained, float(self.cfg.unconstrained_max_spread), self.c1[sl],
+                             self.consensus[sl], self.skew[sl], self.kurt[sl], self.rel[sl], self.qr[sl],
+                             self.reliable[sl], self.status[sl], self.wave_hint, 0, 0, self.cfg.legacy, w,
+                             self._net_fb, rows, oracle.contiguous(), st, U)
+        self._ops.commit_updates(rows, oracle, st, self.values[sl], U)
+        self._ops.round_epilogue(self._active[sl], self.status[sl], self.rel[sl], self.consensus_active[sl],
+                                 self.touched[sl], self.metrics_fx)
+
     def step_pipelined(self, inst: torch.Tensor, oracle: torch.Tensor, vals: torch.Tensor,
                        updates_per_instance: int, chunks: int = 2, overlap: bool = False) -> None:
         """apply_updates(unique=True) + run_round, pipelined over ``chunks`` instance ranges on HIP streams.
@@ -261,12 +306,23 @@ class ConsensusEngine:
         su, sc = self._pipe_streams[0], self._pipe_streams[1:]
         step = (self.B + chunks - 1) // chunks
         ranges = [(k * step, min(self.B, (k + 1) * step)) for k in range(chunks) if k * step < self.B]
+        # fused transactional streaming (fp32 window kernel): the round reads the updated rows from the batch
+        # and a commit kernel copies the accepted ones -- no saved copy, no restore (_fused_ok)
+        fused = self.transactional and self._fused_ok(inst, oracle, vals, U)
         # per-step buffers live in the engine (the side streams use them after this returns): saved rows,
         # saved enabled flags and the update statuses, one slice per range
-        sv_all, sen_all, st_all = self._save_buffer(("pipe",), inst.numel()) if self.transactional else (None,) * 3
+        if fused:
+            sv_all = sen_all = None
+            st_all = self._status_buffer(inst.numel())
+            vals = vals.contiguous()
+        else:
+            sv_all, sen_all, st_all = (self._save_buffer(("pipe",), inst.numel()) if self.transactional
+                                       else (None,) * 3)
 
         def upd(k, b0, b1):
             sl = slice(b0 * U, b1 * U)
+            if fused:
+                return   # (the round reads the batch; the commit after it stores the accepted rows)
             if self.transactional:
                 self.apply_updates(inst[sl], oracle[sl], vals[sl], unique=True, _joined=True,
                                    save=(sv_all[sl], sen_all[sl], st_all[sl]))
@@ -275,6 +331,9 @@ class ConsensusEngine:
 
         def rnd(k, b0, b1):
             sl = slice(b0 * U, b1 * U)
+            if fused:
+                self._run_round_range_fused(b0, b1, oracle[sl], vals[sl], st_all[sl], U)
+                return
             rest = (inst[sl], oracle[sl], st_all[sl], sv_all[sl], sen_all[sl]) if self.transactional else None
             self._run_round_range(b0, b1, restore=rest)
         if overlap:
@@ -484,6 +543,7 @@ class ConsensusEngine:
         self.enabled.fill_(1)
         self.n_active.fill_(self.N)
         self.touched.fill_(1)
+        self._all_active = True
 
     # ------------------------------------------------------------------ getters (contract ABI names)
     def get_consensus_value(self, i: Optional[int] = None) -> torch.Tensor:

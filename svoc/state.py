@@ -90,6 +90,7 @@ def load(path: str, device="cpu"):
     e.enabled.copy_(t["enabled"].to(dev))
     e.reliable.copy_(t["reliable"].to(dev))
     e.n_active.copy_(t["n_active_oracles"].to(dev))
+    e._all_active = False   # (the fused streaming path re-checks activation)
     e.consensus_active.copy_(t["consensus_active"].to(dev).bool())
     g.votes.copy_(t["vote_matrix_columns"].to(dev))
     g.prop_tag.copy_(t["proposition_tag"].to(dev))

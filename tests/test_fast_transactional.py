@@ -134,3 +134,41 @@ def test_pipelined_step_restores_reverted_instances(overlap):
     assert pipe.status[3].item() == int(Status.ZERO_VARIANCE) and int((pipe.status == 0).sum()) == B - 1
     for k in ("values", "enabled", "n_active", "consensus", "rel", "c1"):
         assert torch.equal(getattr(pipe, k), getattr(ref, k)), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,D,f,U", [(256, 1024, 32, 64), (64, 700, 8, 16), (200, 300, 20, 50)])
+def test_fused_streaming_matches_generic_path(N, D, f, U):
+    """The fused transactional step (window kernel reading the updated rows from the batch + commit kernel)
+    equals the generic transactional path (update kernel with saved rows + round + restore) bit for bit:
+    state, outputs, update statuses -- with a reverting instance (zero variance) and an instance whose
+    batch holds an invalid row (interval error: that update alone reverts, the round runs without it)."""
+    B = 6
+    cfg = ConsensusConfig(n_oracles=N, dimension=D, n_failing_oracles=f, constrained=True)
+    fz = ConsensusEngine(cfg, batch=B, device="cuda", mode="fast", storage="fp32")
+    gen = ConsensusEngine(cfg, batch=B, device="cuda", mode="fast", storage="fp32")
+    for e in (fz, gen):
+        e.randomize(seed=N + D)
+        e.run_round()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    inst = torch.arange(B, device="cuda").repeat_interleave(U)
+    orc = torch.stack([torch.randperm(N, device="cuda", generator=g)[:U] for _ in range(B)]).reshape(-1)
+    vals = torch.rand(B * U, D, device="cuda", generator=g)
+    # instance 1: an update row with 1.5 in one column (rejected alone); instance 4: all its updated rows at
+    # one value and the rest of the column too -> zero variance in column 3 if U == N, else a plain round
+    vals[1 * U + 2, D // 2] = 1.5
+    fz.values[4, :, 3] = 0.625
+    gen.values[4, :, 3] = 0.625
+    vals[4 * U:5 * U, 3] = 0.625
+    fz.step_pipelined(inst, orc, vals, U, chunks=2, overlap=False)
+    st_f = fz._status_buffer(B * U).clone()
+    gen._all_active = False      # force the generic path (update kernel + saved rows + restore)
+    gen._fused_ok = lambda *a: False
+    gen.step_pipelined(inst, orc, vals, U, chunks=2, overlap=False)
+    st_g = gen._save_bufs[("pipe",)][2][:B * U].clone()
+    torch.cuda.synchronize()
+    assert torch.equal(st_f, st_g), (st_f.view(B, U), st_g.view(B, U))
+    assert st_f[1 * U + 2].item() == int(Status.INTERVAL_INPUT)
+    assert fz.status[4].item() == int(Status.ZERO_VARIANCE)
+    for k in ("status", "values", "enabled", "n_active", "consensus", "rel", "c1", "reliable", "skew", "kurt", "qr"):
+        assert torch.equal(getattr(fz, k), getattr(gen, k)), k
