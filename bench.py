@@ -156,7 +156,10 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
                                        dtype=torch.int64 if mode == "exact" else eng.vdtype,
                                        # the state's failing oracles stay the failing ones (D-shard:
                                        # every rank's slice of the same rows, so the stream's own set)
-                                       failing=None if dshard else eng.failing_mask)
+                                       failing=None if (dshard or c.get("independent_failing")) else eng.failing_mask)
+        # (independent_failing: the stream draws its own failing oracles, so U(0,1) rows land among the
+        # engine's reliable ones -- reliable outliers every round: the exact kernels' hard case)
+        extra["independent_failing"] = bool(c.get("independent_failing"))
     if args.config == "c5":
         from svoc.codec import address_to_limbs
         from svoc.governance import Governance

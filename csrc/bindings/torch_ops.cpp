@@ -305,7 +305,7 @@ void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& 
   // instances it flags; SVOC_EXACT_I128=1 forces the i128 kernel everywhere (tests, A/B)
   at::Tensor stage, fallback;
   const char* force = std::getenv("SVOC_EXACT_I128");
-  if (constrained && !legacy && p.N >= 4 && !(force && force[0] == '1')) {
+  if (constrained && p.N >= 4 && !(force && force[0] == '1')) {
     stage = at::empty({(int64_t)p.B, 4, (int64_t)p.D}, values.options().dtype(at::kInt));
     fallback = at::empty({(int64_t)p.B}, values.options().dtype(at::kByte));
     p.stage = stage.data_ptr<int32_t>();

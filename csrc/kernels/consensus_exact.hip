@@ -372,9 +372,9 @@ static int exact_round_i128(const ExactParams* p, hipStream_t stream) {
 }
 
 // Exact round: the column-parallel kernel (consensus_wsad.hip) takes every instance it can prove
-// bit-exact in fp64 / int32 arithmetic (constrained, values in [0, 1e6], a successful round); the
-// others -- any revert, out-of-domain values, unconstrained or legacy rounds -- are flagged and run
-// through the i128 kernel right after it on the same stream.
+// bit-exact in fp64 / int64 arithmetic (constrained or obsolete-contract rounds, values in [0, 1e6], a
+// successful round); the others -- any revert, out-of-domain values, unconstrained rounds -- are
+// flagged and run through the i128 kernel right after it on the same stream.
 extern "C" int svoc_exact_round(const ExactParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
   if (p->N < 1 || p->N > 1024 || p->D < 1) return -1;

@@ -4,10 +4,11 @@
 // Semantics: contract/src/contract.cairo:442-503 (constrained) in the exact integer arithmetic of
 // signed_decimal.cairo:52-116 and math.cairo:113-398 (smooth median, quadratic risk, reliability,
 // rank mask, mean, variance, sqrt, skewness, kurtosis; Appendix A.2 of SURVEY.md).  Accepted:
-// constrained, non-legacy rounds over values in [0, 1e6] (the interval the contract enforces on
-// every update, contract.cairo:591-593) that succeed.  Everything else -- every revert, whose status
-// code must come out in the reference's stage order, out-of-domain values, unconstrained or legacy
-// rounds -- is flagged in p.fallback and recomputed right after by the i128 kernel.
+// constrained rounds (the obsolete N-D contract's too: no moments, reliability without /D) over values
+// in [0, 1e6] (the interval the contract enforces on every update, contract.cairo:591-593) that
+// succeed, reliable outliers included (their z-power products are summed in int64).  Everything else --
+// every revert, whose status code must come out in the reference's stage order, out-of-domain values,
+// unconstrained rounds -- is flagged in p.fallback and recomputed right after by the i128 kernel.
 //
 // Why it is fast: the i128 kernel gives each instance one wave and loops over the columns with a
 // group reduction per column per statistic (5 GB/s at 64 x 1024).  Here a lane owns a COLUMN (NSEG
@@ -259,10 +260,12 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       s_all = add(s_all, qv, st);
       if ((relmask[t >> 6] >> (t & 63)) & 1) s_rel = add(s_rel, qv, st);
     }
-    const int64_t rd = p.rel_dim > 0 ? p.rel_dim : D;   // D-sharded: the global dimension
+    // D-sharded: the global dimension; the obsolete contracts divide by nothing (contract_nd.cairo:340-442)
+    const int64_t rd = p.legacy ? 1 : (p.rel_dim > 0 ? p.rel_dim : D);
     const i128 rel1 = constrained_reliability(idiv(s_all, (i128)N, st), rd, st);
     if (!in_unit_interval(rel1)) st = ST_RELIABILITY_INTERVAL;
-    if (f < 0 || R < 4) st = ST_TOO_FEW_RELIABLE;
+    // (the kurtosis needs 4 reliable rows; the obsolete contracts have no moments, the smooth median 2)
+    if (f < 0 || R < (p.legacy ? 2 : 4)) st = ST_TOO_FEW_RELIABLE;
     i128 rel2 = 0;
     if (st == ST_OK) {
       rel2 = constrained_reliability(idiv(s_rel, (i128)R, st), rd, st);
@@ -330,6 +333,14 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       cons = (lo + hi) >> 1;
     }
     __builtin_amdgcn_sched_barrier(0);
+    if (p.legacy) {   // (uniform) obsolete contracts: consensus only, no moments stored
+      if (seg == 0 && vc) {
+        stg[D + col] = (int32_t)cons;
+        stg[2 * D + col] = 0;
+        stg[3 * D + col] = 0;
+      }
+      continue;
+    }
     // the column is re-read per statistic (L2-hot) instead of held in 64 more VGPRs: the fp64 work
     // below needs the registers, and occupancy hides the re-read latency
     // mean (math.cairo:240-254): idiv(sum, R) of non-negative values
@@ -370,25 +381,41 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     const double isd = 1.0 / sd;
     // z-score powers (math.cairo:320-363), reliable rows only (a masked row has z = 0: all powers 0)
     double s3 = 0.0, s4 = 0.0;
+    uint64_t olm = 0;   // rows whose z^2 passes 2^25 (|z| >= 5.79): their powers are summed exactly below
     // z-score powers of one row (a masked row has z = 0: all powers 0)
-    auto zpow = [&](uint32_t x, uint32_t mk) {
+    auto zpow = [&](uint32_t x, uint32_t mk, int i) {
       const double dx = mk ? (double)x - mu : 0.0;
       const double z = wdiv_d(dx, sd, isd);
       const double z2 = wmul_d(z, z);
-      bad = bad || z2 >= 33554432.0;   // 2^25: keeps every product below wmul_d's 2^50 bound
-      s3 += wmul_d(z2, z);
-      s4 += wmul_d(z2, z2);
+      const bool inb = z2 < 33554432.0;   // 2^25: keeps every product below wmul_d's 2^50 bound
+      olm |= (uint64_t)(inb ? 0u : 1u) << i;
+      s3 += inb ? wmul_d(z2, z) : 0.0;
+      s4 += inb ? wmul_d(z2, z2) : 0.0;
     };
     if constexpr (BATCH) {
       load_lo(rs, after(vo, sd), rowb, xr);
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bound the fp64 temporaries in flight
-        zpow(xr[i], bit_mask(mm, i));
+        zpow(xr[i], bit_mask(mm, i), i);
       }
     } else {
 #pragma unroll 8
-      for (int i = 0; i < 64; ++i) zpow(wload<V32>(rs, vo, i * rowb, hw_), bit_mask(mm, i));
+      for (int i = 0; i < 64; ++i) zpow(wload<V32>(rs, vo, i * rowb, hw_), bit_mask(mm, i), i);
+    }
+    // outlier rows (rare; a reliable row far from the mean): the same z and z^2 (exact in fp64), then
+    // wsad_mul(z^2, z) and wsad_mul(z^2, z^2) in int64 -- |z| <= sqrt(R - 1) in real units keeps both
+    // products below 2^63 (signed_decimal.cairo:110-112: truncation toward zero, as int64 division)
+    while (olm) {
+      const int i = __builtin_ctzll(olm);
+      olm &= olm - 1;
+      uint32_t hwo;
+      const uint32_t x = wload<V32>(rs, vo, i * rowb, hwo);
+      const double z = wdiv_d((double)x - mu, sd, isd);
+      const int64_t zi = (int64_t)z, z2i = (int64_t)wmul_d(z, z);
+      if (z2i > (1ll << 40)) bad = true;   // (impossible for |z| <= sqrt(R - 1); kept as a guard)
+      s3 += (double)((z2i * zi + 500000ll) / 1000000ll);
+      s4 += (double)((z2i * z2i + 500000ll) / 1000000ll);
     }
     s3 = group_sum<NSEG, P>(s3);
     s4 = group_sum<NSEG, P>(s4);
@@ -451,7 +478,7 @@ extern "C" int svoc_exact_round_wsad(const ExactParams* p, hipStream_t stream) {
   // lane = column: with few columns most lanes idle, and for N <= 32 the i128 kernel packs 2-8
   // instances per wave instead (profiles/r2_exact_crossover.json: 7 x 6 140 M vs 10 M rounds/s,
   // 16 x 16 27 M vs 10 M; but 64 x 16 already 8.3 M vs 6.0 M for this kernel)
-  if (!p->constrained || p->legacy || p->N < 4 || p->N > 256) return -2;
+  if (!p->constrained || p->N < 4 || p->N > 256) return -2;
   if (p->N <= 32 && p->D < p->wsad_min_d) return -2;
   if (!p->stage || !p->fallback) return -2;
   if ((int64_t)p->N * p->D * (p->val32 ? 4 : 8) >= (1ll << 31)) return -2;   // 32-bit buffer offsets

@@ -215,3 +215,67 @@ def _split_rounds(vg, whole, N, D, f, B, expect_revert):
     for k in ("c1", "consensus", "skew", "kurt"):
         got = torch.cat([outs[0][k].cpu(), outs[1][k].cpu()], dim=1)
         assert torch.equal(got[ok], whole[k][ok]), k
+
+
+@pytest.mark.parametrize("N,D,f", [(64, 512, 8), (256, 300, 32), (100, 130, 10)])
+@pytest.mark.parametrize("dtype", [torch.int64, torch.int32])
+def test_wsad_kernel_reliable_outliers(N, D, f, dtype):
+    """A RELIABLE row far from the column mean (|z| up to ~12 real units) in a few columns: the z-power
+    products pass the fp64 path's 2^50 bound, and the column-parallel kernel sums those rows' powers in
+    int64 instead of handing the instance to the i128 kernel (round 3: every such instance fell back).
+    The kernel alone must take every round and equal the i128 kernel bit for bit."""
+    B = 8
+    v = _wsad(B, N, D, f, seed=N + D + 17, a=80.0)          # tight honest cluster (sd ~0.039)
+    g = torch.Generator().manual_seed(N)
+    for b in range(B):
+        # one row pushed +-0.45 in 3 columns: its qr grows by ~0.6 only, so it stays reliable, and alone in
+        # its column it sits at |z| ~ 6-9 real units
+        rows = torch.randperm(N, generator=g)[:1]
+        cols = torch.randperm(D, generator=g)[:3]
+        for r in rows.tolist():
+            for c in cols.tolist():
+                v[b, r, c] = 950_000 if v[b, r, c] < 500_000 else 50_000
+    vg = v.to(DEV, dtype)
+    fast = _run(vg, f, {"SVOC_EXACT_WSAD_ONLY": "1", "SVOC_EXACT_WSAD_MIN_D": "1"})
+    ref = _run(v.to(DEV), f, {"SVOC_EXACT_I128": "1"})
+    assert (ref["status"] == 0).all(), ref["status"]
+    assert (fast["status"] == 0).all(), fast["status"]
+    for k in OUTS:
+        assert torch.equal(fast[k], ref[k]), k
+
+
+@pytest.mark.parametrize("N,D,f", [(64, 256, 8), (200, 300, 20), (16, 64, 13)])
+def test_wsad_kernel_legacy_rounds(N, D, f):
+    """Obsolete N-D contract rounds (reliability without /D, no moments: contract_nd.cairo:340-442) run in
+    the column-parallel kernel too (round 3 sent every legacy round to the i128 kernel) -- bit-identical,
+    including R = 3 reliable rows, which only the current contract's kurtosis rejects."""
+    B = 6
+    # every row near 0.5 (+-0.02): the RMS deviation over ALL dims stays << 0.5, as the /D-less
+    # reliability needs (the generator's U(0,1) failing rows would push it past the interval)
+    g = torch.Generator().manual_seed(N * 3 + D)
+    v = 500_000 + torch.randint(-20_000, 20_001, (B, N, D), generator=g, dtype=torch.int64)
+    vg = v.to(DEV)
+    def run(env):
+        o = alloc_exact_out(B, N, D, DEV)
+        old = {k: os.environ.get(k) for k in ("SVOC_EXACT_I128", "SVOC_EXACT_WSAD_ONLY", "SVOC_EXACT_WSAD_MIN_D")}
+        try:
+            for k in old:
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            svops.ops().exact_round(vg, None, f, True, 0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"],
+                                    o["qr"], o["reliable"], o["status"], True)
+            torch.cuda.synchronize()
+        finally:
+            for k, val in old.items():
+                if val is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = val
+        return {k: t.cpu() for k, t in o.items()}
+    fast = run({"SVOC_EXACT_WSAD_ONLY": "1", "SVOC_EXACT_WSAD_MIN_D": "1"})
+    ref = run({"SVOC_EXACT_I128": "1"})
+    assert (ref["status"] == 0).all(), ref["status"]
+    assert (fast["status"] == 0).all(), fast["status"]
+    for k in OUTS:
+        assert torch.equal(fast[k], ref[k]), k
+    assert not fast["skew"].any() and not fast["kurt"].any()

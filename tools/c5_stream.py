@@ -103,17 +103,29 @@ class Runner:
                 self.step(i)
 
     def run(self, i0: int, i1: int) -> None:
-        """Steps [i0, i1): eager up to a period boundary, graph replays, eager tail."""
+        """Steps [i0, i1): eager up to a period boundary, graph replays, eager tail (a progress line every
+        30 s: long eager replays must not look hung)."""
         i = i0
+        last = time.perf_counter()
+
+        def tick():
+            nonlocal last
+            if time.perf_counter() - last > 30:
+                print(f"[c5] step {i}/{i1}", flush=True)
+                last = time.perf_counter()
         while i < i1 and i % self.period:
             self.step(i)
             i += 1
         while self.graph is not None and i + self.period <= i1:
             self.graph.replay()
             i += self.period
+            if i % (1024 * self.period) == 0:
+                tick()
         while i < i1:
             self.step(i)
             i += 1
+            if i % 1024 == 0:
+                tick()
 
 
 def state_digest(svc: ConsensusService) -> dict:
