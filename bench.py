@@ -408,7 +408,7 @@ def main():
     log_eng, log_step = eng, r["step"]
     if alt:
         # the same step at the alternative storage dtype (a fresh engine; the first one is freed first)
-        del r, eng
+        r = eng = None
         log_eng = log_step = None
         if dev.type == "cuda":
             torch.cuda.empty_cache()
@@ -419,9 +419,28 @@ def main():
             "hbm_gbps_min_traffic": min_gbps(ra, ra["eng"].values.element_size()),
             "rank_ms_spread": [min(ra["rank_ms"]), max(ra["rank_ms"])]}
         log_eng, log_step = ra["eng"], ra["step"]
+    if args.config == "c3" and fast and args.storage is None and dev.type == "cuda" and not dshard:
+        # the transaction-faithful form of the same stream: the EXACT engine (wsad, bit-identical to the
+        # contract), every one of the 64 updates per instance its own transaction (store + full round +
+        # revert on failure: contract.cairo:588-603).  Fixed 2 timed steps (1 warm-up): ~0.45 s each.
+        import copy
+        r = eng = None
+        log_eng = log_step = None
+        torch.cuda.empty_cache()
+        ax = copy.copy(args)
+        ax.steps, ax.warmup = 2, 1
+        cx = {**c, "mode": "exact", "transactional": True}
+        cx.pop("pipeline", None)
+        rx = measure(ax, cx, None, dev, rank, world, dshard)
+        out["config"]["exact_stream"] = {
+            "engine": "exact (wsad)", "storage": rx["storage"], "transactions_per_instance_per_step": rx["U"],
+            "value": rx["B"] * scale * ax.steps * rx["rounds_per_instance"] / rx["elapsed"],
+            "unit": "consensus rounds/s (one per update transaction)", "steps": ax.steps, "warmup": ax.warmup,
+            "ms_per_step": 1e3 * rx["elapsed"] / ax.steps, "ok_fraction": rx["ok"]}
+        log_eng, log_step = rx["eng"], rx["step"]
     if c.get("alt_precision") == "fp32" and dev.type == "cuda":
         # c4 at the reference's precision: the same step with fp32 encoder weights / activations
-        del r, eng
+        r = eng = None
         log_eng = log_step = None
         torch.cuda.empty_cache()
         rp = measure(args, c, storage, dev, rank, world, dshard, enc_dtype=torch.float32)

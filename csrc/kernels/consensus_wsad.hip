@@ -127,6 +127,8 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   __shared__ uint64_t relmask[4], lowmask[4];
   __shared__ int64_t rels[2];
   __shared__ int flag;
+  __shared__ int early_st;   // a revert decided before the moments (its final status)
+  __shared__ int div0;       // a moment stage divides by zero (the round reverts with DIV_BY_ZERO)
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -134,7 +136,11 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     if (tid == 0) p.fallback[b] = 0;
     return;
   }
-  if (tid == 0) flag = 0;
+  if (tid == 0) {
+    flag = 0;
+    early_st = ST_OK;
+    div0 = 0;
+  }
   const int seg = lane / P, cw = lane % P;
   const int N = p.N, D = p.D;
   const int rowb = D * ESZ;
@@ -262,18 +268,26 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     }
     // D-sharded: the global dimension; the obsolete contracts divide by nothing (contract_nd.cairo:340-442)
     const int64_t rd = p.legacy ? 1 : (p.rel_dim > 0 ? p.rel_dim : D);
+    // The reference's stages in order (contract.cairo:442-503; reference_cpu.cpp exact_round_one): rel1 and
+    // its interval check, the rank cut, pass 2 (R >= 2 reliable rows, else the i128 kernel names the
+    // smooth median's error), rel2 and its interval check, then the moments, whose only failure in this
+    // domain is a division by zero (a reliable column of variance 0 or 1, or R <= 3).  A failure before
+    // the moments is final here (the round reverts with that code, outputs untouched, no fallback).
     const i128 rel1 = constrained_reliability(idiv(s_all, (i128)N, st), rd, st);
-    if (!in_unit_interval(rel1)) st = ST_RELIABILITY_INTERVAL;
-    // (the kurtosis needs 4 reliable rows; the obsolete contracts have no moments, the smooth median 2)
-    if (f < 0 || R < (p.legacy ? 2 : 4)) st = ST_TOO_FEW_RELIABLE;
+    if (st == ST_OK && !in_unit_interval(rel1)) st = ST_RELIABILITY_INTERVAL;
+    if (st == ST_OK && f > N) st = ST_USIZE_UNDERFLOW;
+    const bool fb = st == ST_OK && (f < 0 || R < 2);
     i128 rel2 = 0;
-    if (st == ST_OK) {
+    if (st == ST_OK && !fb) {
       rel2 = constrained_reliability(idiv(s_rel, (i128)R, st), rd, st);
-      if (!in_unit_interval(rel2)) st = ST_RELIABILITY_INTERVAL;
+      if (st == ST_OK && !in_unit_interval(rel2)) st = ST_RELIABILITY_INTERVAL;
     }
+    // (the kurtosis divides by (n-2)(n-3), the skewness by (n-1)(n-2); the obsolete contracts stop before)
+    if (st == ST_OK && !fb && !p.legacy && R < 4) st = ST_DIV_BY_ZERO;
     rels[0] = (int64_t)rel1;
     rels[1] = (int64_t)rel2;
-    if (st != ST_OK) flag = 1;
+    early_st = st;
+    if (fb) flag = 1;
     // pass-2 sentinel split: the first (NPAD - R + 1) / 2 non-reliable rows (row order) become -inf
     int need = (NPAD - R + 1) >> 1;
     for (int w = 0; w < 4; ++w) {
@@ -293,13 +307,21 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     if (tid == 0) p.fallback[b] = 1;
     return;
   }
+  if (early_st != ST_OK) {   // reverted before the moments: final, outputs untouched
+    if (tid == 0) {
+      p.status[b] = early_st;
+      p.fallback[b] = 0;
+    }
+    return;
+  }
 
   // ------------------------------------------------------------ pass 2 (contract.cairo:476-500)
   const uint64_t mymask = relmask[seg];
   const uint64_t mylow = lowmask[seg];
   const double Rd = (double)R, invR = 1.0 / Rd;
   const double k3 = (double)((R - 1) * (R - 2)), ik3 = 1.0 / k3;
-  bool bad = false;
+  bool bad = false;   // a result this kernel cannot represent: the i128 kernel recomputes the round
+  bool dz = false;    // the contract divides by zero in the moments: the round reverts
 #pragma nounroll
   for (int s = 0; s < nslab; ++s) {
     const int col = s * W + wave * P + cw;
@@ -377,7 +399,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     // var 0 (sqrt 0 -> wsad_div by zero) and var 1 (sqrt(1) divides by zero) revert the round
     double sd = 1.0;
     const bool ok_sd = var >= 2.0 && wsqrt_d(var, sd);
-    if (vc && !ok_sd) bad = true;
+    if (vc && !ok_sd) dz = true;   // sqrt(0) -> wsad_div by 0, sqrt(1) divides by 0: DIV_BY_ZERO
     const double isd = 1.0 / sd;
     // z-score powers (math.cairo:320-363), reliable rows only (a masked row has z = 0: all powers 0)
     double s3 = 0.0, s4 = 0.0;
@@ -432,9 +454,17 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     }
   }
   if (bad || (MODE == 2 && badv)) flag = 1;
+  if (dz) div0 = 1;
   __syncthreads();
   if (flag) {
     if (tid == 0) p.fallback[b] = 1;
+    return;
+  }
+  if (div0) {   // (every moment failure is DIV_BY_ZERO, whichever column comes first: final)
+    if (tid == 0) {
+      p.status[b] = ST_DIV_BY_ZERO;
+      p.fallback[b] = 0;
+    }
     return;
   }
 

@@ -350,8 +350,12 @@ static int launch_updates(const UpdateParams& p, hipStream_t stream) {
 }
 
 static int launch_restore(const RestoreParams& p, hipStream_t stream) {
-  int64_t blocks = ((int64_t)p.U + 255) / 256;
-  if (blocks > 64) blocks = 64;
+  // at most 64 workgroups for the pipelined c3 ranges (32 k updates), at most 8 updates per thread past that
+  // (a flat 64-workgroup grid left the c5 stream's 1M updates per step at 64 dependent iterations per
+  // thread: +0.14 ms per step)
+  const int64_t need = ((int64_t)p.U + 255) / 256;
+  int64_t blocks = (need + 7) / 8;
+  if (blocks < 64) blocks = need < 64 ? need : 64;
   hipLaunchKernelGGL(upd_restore_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p);
   return (int)hipGetLastError();
 }

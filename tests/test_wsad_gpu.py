@@ -90,8 +90,8 @@ def test_wsad_kernel_goldens(name):
 
 
 def test_wsad_kernel_flags_reverts_and_out_of_domain():
-    """Reverting rounds and values outside [0, 1e6] are left to the i128 kernel (same statuses as
-    the CPU engine, outputs untouched)."""
+    """Reverting rounds get the CPU engine's stage-ordered status from the column kernel itself; values
+    outside [0, 1e6] are left to the i128 kernel (flag -1); the combined dispatch equals the CPU engine."""
     B, N, D, f = 8, 64, 128, 8
     v = _wsad(B, N, D, f, seed=9)
     v[1, :, 5] = 400000                       # zero variance column -> DIV_BY_ZERO in the contract
@@ -102,11 +102,13 @@ def test_wsad_kernel_flags_reverts_and_out_of_domain():
     v[5, :, 9] = 0                            # zero variance at 0
     v[5, 0, 9] = 1                            # ... except one ulp: variance rounds to 0 in wsad
     only = _run(v.to(DEV), f, {"SVOC_EXACT_WSAD_ONLY": "1"})
-    assert only["status"].tolist()[:6] == [0, -1, -1, -1, -1, -1] and only["status"][6:].eq(0).all()
     comb = _run(v.to(DEV), f)
     o = alloc_exact_out(B, N, D, "cpu")
     svops.ops().exact_round(v, None, f, True, 0, o["c1"], o["consensus"], o["skew"], o["kurt"], o["rel"], o["qr"],
                             o["reliable"], o["status"], False)
+    st = only["status"].cpu().tolist()
+    assert st[3] == -1 and st[4] == -1 and only["status"][6:].eq(0).all(), st
+    assert [st[i] for i in (0, 1, 2, 5)] == [o["status"][i].item() for i in (0, 1, 2, 5)], st
     for k in OUTS:
         assert torch.equal(comb[k], o[k]), k
     assert comb["status"][1].item() != 0 and comb["status"][2].item() != 0
@@ -279,3 +281,33 @@ def test_wsad_kernel_legacy_rounds(N, D, f):
     for k in OUTS:
         assert torch.equal(fast[k], ref[k]), k
     assert not fast["skew"].any() and not fast["kurt"].any()
+
+
+@pytest.mark.parametrize("N,D,f", [(64, 256, 8), (256, 200, 32), (40, 70, 4)])
+def test_wsad_kernel_reverts_in_kernel(N, D, f):
+    """Reverting rounds are decided by the column-parallel kernel itself, with the reference's stage-ordered
+    code (round 3 sent every reverting round to the i128 kernel): a zero-variance reliable column and a
+    variance-1 column (sqrt(1)) -> DIV_BY_ZERO in the moments, rel1 < 0 -> RELIABILITY_INTERVAL before
+    them, R = 3 -> DIV_BY_ZERO (kurtosis).  Statuses equal the i128 kernel's; reverted outputs untouched."""
+    B = 6
+    v = _wsad(B, N, D, f, seed=N + 5 * D)
+    v[1, :, 3] = 654_321                                   # constant column: variance 0
+    v[2, :, 5] = 500_000
+    v[2, :N // 2, 5] = 500_001                             # 0/1 ulp column: tiny variance (sqrt(1) or 0)
+    v[3, : N // 2 + 1, :] = 0                              # c1 = 0, the rest at distance 1: rel1 < 0
+    v[3, N // 2 + 1:, :] = 1_000_000
+    vg = v.to(DEV)
+    fast = _run(vg, f, {"SVOC_EXACT_WSAD_ONLY": "1", "SVOC_EXACT_WSAD_MIN_D": "1"})
+    ref = _run(v.to(DEV), f, {"SVOC_EXACT_I128": "1"})
+    assert torch.equal(fast["status"], ref["status"]), (fast["status"], ref["status"])
+    st = ref["status"].tolist()
+    assert st[1] != 0 and st[3] != 0 and st[0] == 0, st
+    ok = ref["status"] == 0
+    for k in OUTS:
+        assert torch.equal(fast[k][ok], ref[k][ok]), k
+    # R = 3: every round reverts in the moments (the kurtosis' (n-2)(n-3) = 0)
+    f3 = N - 3
+    fast3 = _run(vg, f3, {"SVOC_EXACT_WSAD_ONLY": "1", "SVOC_EXACT_WSAD_MIN_D": "1"})
+    ref3 = _run(v.to(DEV), f3, {"SVOC_EXACT_I128": "1"})
+    assert torch.equal(fast3["status"], ref3["status"]), (fast3["status"], ref3["status"])
+    assert (ref3["status"] != 0).all()

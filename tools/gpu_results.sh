@@ -19,6 +19,7 @@ PY
 }
 if [ -z "${PART2:-}" ]; then
 run c3 400 --config c3 --steps 20 --warmup 3 &&
+run c3_notxn 300 --config c3 --storage fp32 --transactional 0 --steps 20 --warmup 3 &&
 run c3_bf16 300 --config c3 --storage bf16 --steps 20 --warmup 3 &&
 run c2 300 --config c2 --steps 20 --warmup 3 &&
 run c2_fp32 300 --config c2 --storage fp32 --steps 20 --warmup 3 &&
@@ -44,5 +45,6 @@ for spec in "c3:--storage fp32" "c2:--storage bf16" "c4:"; do   # one storage pe
       > $R/gpurun_out/prof_$cfg.log 2>&1) || exit 1
 done
 # last: 64 exact transactions per instance per step at the YAML batch (1024 instances)
-run c3_exact_stream 150 --config-file configs/c3_exact_stream.yaml --steps 2 --warmup 1 || exit 1
+run c3_exact_stream 150 --config-file configs/c3_exact_stream.yaml --steps 2 --warmup 1 &&
+run c3_exact_stream_indep 150 --config-file configs/c3_exact_stream_indep.yaml --steps 2 --warmup 1 || exit 1
 echo "=== done"

@@ -23,6 +23,8 @@ ROWS = [
     ("c2", "c2: 64 × 1024, 10k batched instances, bf16", "≈93/s numpy fp64"),
     ("c3", "c3: 256 × 4096 streaming, failing-oracle masking, fp32 storage (headline: reference resolution)",
      "≈6/s numpy fp64"),
+    ("c3_notxn", "c3, coalesced without transactions (a reverted batch's rows stay; the round-3 headline form)",
+     "≈6/s numpy fp64"),
     ("c3_bf16", "c3 shape, fast mode over bf16 storage", "≈6/s numpy fp64"),
     ("c4", "c4: BERT-base sentiment oracles → consensus", "—"),
     ("c5", "c5: governance + reliability stream, 1M instances (7 × 6)", "≈127,900/s numpy fp64 (7×6)"),
@@ -35,6 +37,8 @@ ROWS = [
     ("c5_exact_stream", "c5 shape, exact transactional update stream (store + round + revert per update)",
      "939/s exact Python emulator"),
     ("c3_exact_stream", "c3 shape, exact transactional update stream, 1024 instances × 64 transactions/step",
+     "0.61/s exact Python emulator (64 × 1024)"),
+    ("c3_exact_stream_indep", "c3 exact transactional stream, independent failing set (reliable outliers)",
      "0.61/s exact Python emulator (64 × 1024)"),
     ("wide512", "512 oracles × 2048 dims, 1024 instances (N > 256)", "—"),
     ("wide512_fp32", "512 × 2048, fast mode over fp32 storage", "—"),
