@@ -108,7 +108,9 @@ __global__ __launch_bounds__(256) void consensus_fast_small_kernel(FastParams p)
     cA = 0.5f * (bf16_lo(lo) + bf16_lo(hi));
     cB = 0.5f * (bf16_hi(lo) + bf16_hi(hi));
   }
-  if (live) {
+  // c1: with c1_out (mode 0) written at the commit below, where the round succeeded (no staging row and
+  // no commit_rows launch after this kernel); without it, into the row the caller passed
+  if (live && !p.c1_out) {
     if (vA) p.c1[b * D + colA] = cA;
     if (vB) p.c1[b * D + colA + 1] = cB;
   }
@@ -166,7 +168,7 @@ __global__ __launch_bounds__(256) void consensus_fast_small_kernel(FastParams p)
     if (!(rel2 >= 0.f && rel2 <= 1.f)) st = ST_RELIABILITY_INTERVAL;
     else if (R < 4 && !p.legacy) st = ST_TOO_FEW_RELIABLE;
   }
-  if (st != ST_OK) {  // revert: only the pass-1 diagnostic c1 and the status are written
+  if (st != ST_OK) {  // revert: only the status is written (and the pass-1 c1 when the caller took it unstaged)
     if (live && g == 0) p.status[b] = st;
     return;           // uniform over the group
   }
@@ -250,6 +252,7 @@ __global__ __launch_bounds__(256) void consensus_fast_small_kernel(FastParams p)
     p.consensus[o] = cons_o[h];
     p.skew[o] = sk_o[h];
     p.kurt[o] = ku_o[h];
+    if (p.c1_out) p.c1_out[o] = h ? cB : cA;
   }
 #pragma unroll
   for (int i = 0; i < NR; ++i)  // constant register indices only (a runtime index spills to scratch)

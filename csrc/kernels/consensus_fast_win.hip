@@ -806,12 +806,13 @@ extern "C" int svoc_fast_round_bf16_small(const FastParams* p, hipStream_t strea
 //   default: this one-network window kernel where it applies (workspace given, f <= 32, N <= 256);
 //   otherwise, and for wave_hint -7 (tests: the cross-check), the two-network register-streaming kernel
 //     (consensus_fast_reg.hip).
-//   c1 (mode 0 with c1_out): the window kernel commits it itself; after the others, commit_rows does.
+//   c1 (mode 0 with c1_out): the window and small kernels commit it themselves; after the others,
+//   commit_rows does.
 extern "C" int svoc_fast_round_bf16(const FastParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
   int rc;
   if (p->wave_hint == 0 && p->mode == 0 && p->N <= 16 && p->D <= 128) {
-    rc = svoc_fast_round_bf16_small(p, stream);
+    return svoc_fast_round_bf16_small(p, stream);   // (commits c1 into c1_out itself)
   } else {
     if (p->wave_hint != -7) {
       rc = svoc_fast_round_bf16_win(p, stream);

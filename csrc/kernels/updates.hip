@@ -233,9 +233,15 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
     // indices (their addresses do not depend on them), validated and stored from registers -- one
     // memory round trip before the stores instead of three (profiles/r2_pmc_c5.md)
     const int nw = (int)(row_bytes >> 2);
-    uint32_t w[4];
+    uint32_t w[4], old[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) w[k] = (in && k < nw) ? ((const uint32_t*)src)[k] : 0u;
+    // the slot's old words and enabled flag, loaded together (one round trip after the indices; the
+    // stores below could alias them, so loaded any later they would wait for those stores)
+    const bool slot = in && !bad;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) old[k] = (slot && p.saved && k < nw) ? ((const uint32_t*)dst)[k] : 0u;
+    const uint8_t was = slot ? p.enabled[b * p.N + o] : (uint8_t)1;
     bool ok = true, fin = true;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -254,11 +260,18 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
       uint32_t* sv = (uint32_t*)((unsigned char*)p.saved + u * row_bytes);
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if (k < nw) sv[k] = ((const uint32_t*)dst)[k];
+        if (k < nw) __builtin_nontemporal_store(old[k], sv + k);   // read back only on a revert
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k)
       if (k < nw) ((uint32_t*)dst)[k] = w[k];
+    if (p.saved_en) p.saved_en[u] = was;
+    if (!was) {
+      p.enabled[b * p.N + o] = 1;
+      atomicAdd(&p.n_active[b], 1);
+    }
+    p.touched[b] = 1;
+    return;
   } else {
     bool ok = true, fin = true;
     if (in) {
@@ -350,11 +363,11 @@ static int launch_updates(const UpdateParams& p, hipStream_t stream) {
 }
 
 static int launch_restore(const RestoreParams& p, hipStream_t stream) {
-  // at most 64 workgroups for the pipelined c3 ranges (32 k updates), at most 8 updates per thread past that
-  // (a flat 64-workgroup grid left the c5 stream's 1M updates per step at 64 dependent iterations per
-  // thread: +0.14 ms per step)
+  // at least 64 workgroups (the pipelined c3 ranges: 32 k updates, 2 per thread), 2 updates per thread
+  // past that (a flat 64-workgroup grid left the c5 stream's 1M updates per step at 64 dependent
+  // iterations per thread: +0.14 ms per step)
   const int64_t need = ((int64_t)p.U + 255) / 256;
-  int64_t blocks = (need + 7) / 8;
+  int64_t blocks = (need + 1) / 2;
   if (blocks < 64) blocks = need < 64 ? need : 64;
   hipLaunchKernelGGL(upd_restore_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p);
   return (int)hipGetLastError();
