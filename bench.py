@@ -114,7 +114,10 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
         from svoc.parallel.dshard import flush_sharded, run_round_sharded, shard_bounds
         lo, hi = shard_bounds(c["D"], rank, world)
         D_local = hi - lo
-    cfg = ConsensusConfig(n_oracles=c["N"], dimension=D_local, n_failing_oracles=c["f"], constrained=True)
+    # (constrained: false -- the reference's R^M mode, contract.cairo:370-434; max_spread in real units)
+    cfg = ConsensusConfig(n_oracles=c["N"], dimension=D_local, n_failing_oracles=c["f"],
+                          constrained=bool(c.get("constrained", True)),
+                          unconstrained_max_spread=float(c.get("max_spread", 1.0)))
     mode = args.mode or c.get("mode", "fast")
     eng = ConsensusEngine(cfg, batch=B, device=dev, mode=mode, storage=storage)
     eng.wave_hint = args.wave_hint

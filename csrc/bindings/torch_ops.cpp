@@ -301,11 +301,11 @@ void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& 
     work = at::empty({(int64_t)p.B, 6, (int64_t)p.D}, values.options().dtype(at::kLong));
     p.work = work.data_ptr<int64_t>();
   }
-  // column-parallel kernel (consensus_wsad.hip) for constrained rounds, the i128 kernel for the
-  // instances it flags; SVOC_EXACT_I128=1 forces the i128 kernel everywhere (tests, A/B)
+  // column-parallel kernel (consensus_wsad.hip), the i128 kernel for the instances it flags;
+  // SVOC_EXACT_I128=1 forces the i128 kernel everywhere (tests, A/B)
   at::Tensor stage, fallback;
   const char* force = std::getenv("SVOC_EXACT_I128");
-  if (constrained && p.N >= 4 && !(force && force[0] == '1')) {
+  if (p.N >= 4 && !(force && force[0] == '1')) {
     stage = at::empty({(int64_t)p.B, 4, (int64_t)p.D}, values.options().dtype(at::kInt));
     fallback = at::empty({(int64_t)p.B}, values.options().dtype(at::kByte));
     p.stage = stage.data_ptr<int32_t>();

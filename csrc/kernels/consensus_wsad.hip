@@ -6,9 +6,11 @@
 // rank mask, mean, variance, sqrt, skewness, kurtosis; Appendix A.2 of SURVEY.md).  Accepted:
 // constrained rounds (the obsolete N-D contract's too: no moments, reliability without /D) over values
 // in [0, 1e6] (the interval the contract enforces on every update, contract.cairo:591-593) that
-// succeed, reliable outliers included (their z-power products are summed in int64).  Everything else --
-// every revert, whose status code must come out in the reference's stage order, out-of-domain values,
-// unconstrained rounds -- is flagged in p.fallback and recomputed right after by the i128 kernel.
+// succeed, reliable outliers included (their z-power products are summed in int64), and the reverting
+// ones: the kernel reports the reference's stage-ordered status (reliability interval after each pass,
+// usize underflow / index OOB for R < 2, too few reliable, division by zero of a zero-variance column)
+// and writes nothing else.  Out-of-domain values and unconstrained rounds are flagged in p.fallback
+// and recomputed right after by the i128 kernel.
 //
 // Why it is fast: the i128 kernel gives each instance one wave and loops over the columns with a
 // group reduction per column per statistic (5 GB/s at 64 x 1024).  Here a lane owns a COLUMN (NSEG
@@ -98,6 +100,27 @@ SVOC_DEV void qtree_all(const uint32_t (&q)[64], int lane, uint64_t* acc, std::i
   ((acc[Is] += qtree<__builtin_ctz(P), Is, P>(q, lane)), ...);
 }
 
+// The same butterfly with 64-bit partial sums (unconstrained: a deviation's qdev may reach 2^31)
+template <int L, int I, int P>
+SVOC_DEV uint64_t qtree64(const uint32_t (&q)[64], int lane) {
+  if constexpr (L == 0) {
+    return q[I];
+  } else {
+    constexpr int msk = P >> L;
+    const uint64_t lo_v = qtree64<L - 1, I, P>(q, lane);
+    const uint64_t hi_v = qtree64<L - 1, I + (64 >> L), P>(q, lane);
+    const bool up = (lane & msk) != 0;
+    const uint64_t send = up ? lo_v : hi_v;
+    const uint64_t keep = up ? hi_v : lo_v;
+    const uint32_t rlo = xor_lane_u32<msk>((uint32_t)send), rhi = xor_lane_u32<msk>((uint32_t)(send >> 32));
+    return keep + (((uint64_t)rhi << 32) | rlo);
+  }
+}
+template <int P, int... Is>
+SVOC_DEV void qtree64_all(const uint32_t (&q)[64], int lane, uint64_t* acc, std::integer_sequence<int, Is...>) {
+  ((acc[Is] += qtree64<__builtin_ctz(P), Is, P>(q, lane)), ...);
+}
+
 // sum over the NSEG lanes of a column group (lanes lane ^ t*P)
 template <int NSEG, int P, class T>
 SVOC_DEV T group_sum(T v) {
@@ -109,7 +132,12 @@ SVOC_DEV T group_sum(T v) {
 // MODE (launch.hpp ExactParams::mode): 0 whole round; 1 D-sharded first half (c1 + qr partials out);
 // 2 D-sharded second half (c1 and the all-reduced qr in).  Instances it cannot take in mode 1 / 2 go
 // to the i128 kernel's same mode through p.fallback, as in mode 0.
-template <int NSEG, int WAVES, bool V32, int MODE>
+// CONS = false: unconstrained rounds (contract.cairo:370-434): signed values, pass-2 consensus = the reliable
+// mean (no second network), reliabilities W - wsad_div(min(ms, sqrt(mean qr)), ms).  Domain (else the
+// i128 kernel): int32 values within 2^25 (33.55 in real units) of their column's smooth median and of
+// its reliable mean -- the bound under which the fp64 forms of qdev / wsad_div are exact (wsad_fast.hpp);
+// the qr butterfly then sums 64-bit partials.
+template <int NSEG, int WAVES, bool V32, int MODE, bool CONS>
 __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams p) {
   constexpr int P = 64 / NSEG;      // columns per wave
   constexpr int NPAD = 64 * NSEG;   // padded oracle rows
@@ -137,7 +165,8 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     return;
   }
   if (tid == 0) {
-    flag = 0;
+    // (unconstrained, D-sharded second half over int64 values: no pass 1 here to validate the high words)
+    flag = (!CONS && MODE == 2 && !V32) ? 1 : 0;
     early_st = ST_OK;
     div0 = 0;
   }
@@ -159,6 +188,9 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   uint64_t acc[KEEP];
 #pragma unroll
   for (int k = 0; k < KEEP; ++k) acc[k] = 0;
+  // a stored low word as a number: [0, 1e6] (constrained) or an int32 (unconstrained)
+  auto xv = [](uint32_t x) __attribute__((always_inline)) { return CONS ? (double)x : (double)(int32_t)x; };
+  constexpr uint32_t kSign = CONS ? 0u : 0x80000000u;   // order-preserving key of an int32
 
   // ------------------------------------------------------------ pass 1 (contract.cairo:455-463)
 #pragma nounroll
@@ -174,33 +206,42 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
         uint32_t hw;
         const uint32_t x = wload<V32>(rs, vo, i * rowb, hw);
         const bool real = i < nv;
-        badv |= (vc && real && (x > kWsadMax || hw != 0)) ? 1u : 0u;   // outside [0, 1e6]
-        r[i] = (real ? x : (i < nl ? 0u : ~0u)) ^ pol;
+        if constexpr (CONS) badv |= (vc && real && (x > kWsadMax || hw != 0)) ? 1u : 0u;   // outside [0, 1e6]
+        else if constexpr (!V32) badv |= (vc && real && hw != (uint32_t)((int32_t)x >> 31)) ? 1u : 0u;   // not an int32
+        r[i] = (real ? x ^ kSign : (i < nl ? 0u : ~0u)) ^ pol;
       }
       uint32_t lo, hi;
       median_group<NSEG>(r, lo, hi);   // smooth median: ranks N/2 - 1, N/2 (math.cairo:113-126)
-      c1 = (lo + hi) >> 1;             // idiv_pos64(a + b, 2) of non-negative values
+      if constexpr (CONS) {
+        c1 = (lo + hi) >> 1;           // idiv_pos64(a + b, 2) of non-negative values
+      } else {                         // I128Div(a + b, 2): truncation toward zero
+        const int64_t sum = (int64_t)(int32_t)(lo ^ kSign) + (int64_t)(int32_t)(hi ^ kSign);
+        c1 = (uint32_t)(int32_t)(sum / 2);
+      }
     }
     if (seg == 0 && vc) stg[col] = (int32_t)c1;
     __builtin_amdgcn_sched_barrier(0);
     // quadratic risk (math.cairo:225-238): this column's qdev of every row, summed over the columns
     uint32_t q[64];
-    const double cd = (double)c1;
+    const double cd = xv(c1);
     if constexpr (BATCH1) {
       load_lo(rs, after(vo, c1), rowb, q);
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bound the fp64 temporaries in flight
-        q[i] = (vc && i < nv) ? (uint32_t)qdev_d((double)q[i], cd) : 0u;
+        if (!CONS) badv |= (vc && i < nv && !(fabs(xv(q[i]) - cd) < 33554432.0)) ? 1u : 0u;   // 2^25
+        q[i] = (vc && i < nv) ? (uint32_t)qdev_d(xv(q[i]), cd) : 0u;
       }
     } else {
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
-        q[i] = (vc && i < nv) ? (uint32_t)qdev_d((double)x, cd) : 0u;
+        if (!CONS) badv |= (vc && i < nv && !(fabs(xv(x) - cd) < 33554432.0)) ? 1u : 0u;
+        q[i] = (vc && i < nv) ? (uint32_t)qdev_d(xv(x), cd) : 0u;
       }
     }
-    qtree_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
+    if constexpr (CONS) qtree_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
+    else qtree64_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
   }
   {
     int base = 0;
@@ -273,13 +314,18 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     // smooth median's error), rel2 and its interval check, then the moments, whose only failure in this
     // domain is a division by zero (a reliable column of variance 0 or 1, or R <= 3).  A failure before
     // the moments is final here (the round reverts with that code, outputs untouched, no fallback).
-    const i128 rel1 = constrained_reliability(idiv(s_all, (i128)N, st), rd, st);
+    // Unconstrained (contract.cairo:379-433): the pass-2 essence is the reliable mean, whose division by
+    // R = 0 is the first failure of an empty reliable set; R = 1 .. 3 fail later, in the moments.
+    const i128 rel1 = CONS ? constrained_reliability(idiv(s_all, (i128)N, st), rd, st)
+                           : unconstrained_reliability(wsqrt(idiv(s_all, (i128)N, st), st), (i128)p.max_spread, st);
     if (st == ST_OK && !in_unit_interval(rel1)) st = ST_RELIABILITY_INTERVAL;
     if (st == ST_OK && f > N) st = ST_USIZE_UNDERFLOW;
-    const bool fb = st == ST_OK && (f < 0 || R < 2);
+    const bool fb = st == ST_OK && (f < 0 || (CONS ? R < 2 : p.legacy != 0));
+    if (!CONS && st == ST_OK && !fb && R == 0) st = ST_DIV_BY_ZERO;
     i128 rel2 = 0;
     if (st == ST_OK && !fb) {
-      rel2 = constrained_reliability(idiv(s_rel, (i128)R, st), rd, st);
+      rel2 = CONS ? constrained_reliability(idiv(s_rel, (i128)R, st), rd, st)
+                  : unconstrained_reliability(wsqrt(idiv(s_rel, (i128)R, st), st), (i128)p.max_spread, st);
       if (st == ST_OK && !in_unit_interval(rel2)) st = ST_RELIABILITY_INTERVAL;
     }
     // (the kurtosis divides by (n-2)(n-3), the skewness by (n-1)(n-2); the obsolete contracts stop before)
@@ -329,8 +375,8 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     const int vo = seg_off + (vc ? col : 0) * ESZ;
     uint64_t mm = mymask, ml = mylow;
     asm volatile("" : "+v"(mm), "+v"(ml));   // keep the 64 row masks out of the slab loop's live set
-    uint32_t cons;
-    {
+    uint32_t cons = 0;
+    if constexpr (CONS) {
       uint32_t r[64];
       if constexpr (BATCH && (MODE != 2 || V32)) {   // values validated in pass 1 (or 32-bit): one batch
         load_lo(rs, vo, rowb, r);
@@ -355,7 +401,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       cons = (lo + hi) >> 1;
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (p.legacy) {   // (uniform) obsolete contracts: consensus only, no moments stored
+    if (CONS && p.legacy) {   // (uniform) obsolete contracts: consensus only, no moments stored
       if (seg == 0 && vc) {
         stg[D + col] = (int32_t)cons;
         stg[2 * D + col] = 0;
@@ -367,35 +413,64 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     // below needs the registers, and occupancy hides the re-read latency
     // mean (math.cairo:240-254): idiv(sum, R) of non-negative values
     uint32_t xr[64];
-    uint32_t sx = 0;
-    if constexpr (BATCH1) {
-      load_lo(rs, after(vo, cons), rowb, xr);
+    double mu;
+    if constexpr (CONS) {
+      uint32_t sx = 0;
+      if constexpr (BATCH1) {
+        load_lo(rs, after(vo, cons), rowb, xr);
 #pragma unroll
-      for (int i = 0; i < 64; ++i) sx += xr[i] & bit_mask(mm, i);
-    } else {
+        for (int i = 0; i < 64; ++i) sx += xr[i] & bit_mask(mm, i);
+      } else {
 #pragma unroll 16
-      for (int i = 0; i < 64; ++i) sx += wload<V32>(rs, vo, i * rowb, hw_) & bit_mask(mm, i);
+        for (int i = 0; i < 64; ++i) sx += wload<V32>(rs, vo, i * rowb, hw_) & bit_mask(mm, i);
+      }
+      sx = group_sum<NSEG, P>(sx);
+      mu = floor_div_d((double)sx, Rd, invR);
+    } else {   // signed sum (|sum| < 2^39: exact), I128Div toward zero; the mean is the consensus
+      load_lo(rs, after(vo, mm), rowb, xr);
+      double sxd = 0.0;
+#pragma unroll
+      for (int i = 0; i < 64; ++i) sxd += bit_mask(mm, i) ? xv(xr[i]) : 0.0;
+      sxd = group_sum<NSEG, P>(sxd);
+      mu = trunc_div_d(sxd, Rd, invR);
+      cons = (uint32_t)(int32_t)mu;
     }
-    sx = group_sum<NSEG, P>(sx);
-    const double mu = floor_div_d((double)sx, Rd, invR);
     // population variance (math.cairo:208-222): mean of qdev(x, mu) over the reliable rows
-    uint32_t sv = 0;
-    if constexpr (BATCH) {
-      load_lo(rs, after(vo, mu), rowb, xr);
+    double var;
+    if constexpr (CONS) {
+      uint32_t sv = 0;
+      if constexpr (BATCH) {
+        load_lo(rs, after(vo, mu), rowb, xr);
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
+          sv += bit_mask(mm, i) & (uint32_t)qdev_d((double)xr[i], mu);
+        }
+      } else {
+#pragma unroll 16
+        for (int i = 0; i < 64; ++i) {
+          const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
+          sv += bit_mask(mm, i) & (uint32_t)qdev_d((double)x, mu);
+        }
+      }
+      sv = group_sum<NSEG, P>(sv);
+      var = floor_div_d((double)sv, Rd, invR);
+    } else {   // fp64 sums (exact: every term < 2^31 under the |x - mu| < 2^25 bound checked here)
+      double svd = 0.0;
+      if constexpr (BATCH) load_lo(rs, after(vo, mu), rowb, xr);
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
-        sv += bit_mask(mm, i) & (uint32_t)qdev_d((double)xr[i], mu);
+        const double xi = xv(BATCH ? xr[i] : wload<V32>(rs, vo, i * rowb, hw_));
+        const bool mk = bit_mask(mm, i) != 0u;
+        if (vc && mk && !(fabs(xi - mu) < 33554432.0)) bad = true;
+        svd += mk ? qdev_d(xi, mu) : 0.0;
       }
-    } else {
-#pragma unroll 16
-      for (int i = 0; i < 64; ++i) {
-        const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
-        sv += bit_mask(mm, i) & (uint32_t)qdev_d((double)x, mu);
-      }
+      svd = group_sum<NSEG, P>(svd);
+      var = floor_div_d(svd, Rd, invR);
+      if (vc && !(var < 2147483648.0)) bad = true;   // wsqrt_d's bound
+      if (bad) var = 0.0;
     }
-    sv = group_sum<NSEG, P>(sv);
-    const double var = floor_div_d((double)sv, Rd, invR);
     // var 0 (sqrt 0 -> wsad_div by zero) and var 1 (sqrt(1) divides by zero) revert the round
     double sd = 1.0;
     const bool ok_sd = var >= 2.0 && wsqrt_d(var, sd);
@@ -406,7 +481,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     uint64_t olm = 0;   // rows whose z^2 passes 2^25 (|z| >= 5.79): their powers are summed exactly below
     // z-score powers of one row (a masked row has z = 0: all powers 0)
     auto zpow = [&](uint32_t x, uint32_t mk, int i) {
-      const double dx = mk ? (double)x - mu : 0.0;
+      const double dx = mk ? xv(x) - mu : 0.0;
       const double z = wdiv_d(dx, sd, isd);
       const double z2 = wmul_d(z, z);
       const bool inb = z2 < 33554432.0;   // 2^25: keeps every product below wmul_d's 2^50 bound
@@ -433,7 +508,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       olm &= olm - 1;
       uint32_t hwo;
       const uint32_t x = wload<V32>(rs, vo, i * rowb, hwo);
-      const double z = wdiv_d((double)x - mu, sd, isd);
+      const double z = wdiv_d(xv(x) - mu, sd, isd);
       const int64_t zi = (int64_t)z, z2i = (int64_t)wmul_d(z, z);
       if (z2i > (1ll << 40)) bad = true;   // (impossible for |z| <= sqrt(R - 1); kept as a guard)
       s3 += (double)((z2i * zi + 500000ll) / 1000000ll);
@@ -488,14 +563,20 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   }
 }
 
-template <int NSEG>
-static int launch_wsad(const ExactParams& p, hipStream_t stream) {
+template <int NSEG, bool CONS>
+static int launch_wsad_c(const ExactParams& p, hipStream_t stream) {
   constexpr int WAVES = 4;
-  auto k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 0> : consensus_wsad_kernel<NSEG, WAVES, false, 0>;
-  if (p.mode == 1) k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 1> : consensus_wsad_kernel<NSEG, WAVES, false, 1>;
-  if (p.mode == 2) k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 2> : consensus_wsad_kernel<NSEG, WAVES, false, 2>;
+  auto k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 0, CONS> : consensus_wsad_kernel<NSEG, WAVES, false, 0, CONS>;
+  if (p.mode == 1)
+    k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 1, CONS> : consensus_wsad_kernel<NSEG, WAVES, false, 1, CONS>;
+  if (p.mode == 2)
+    k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 2, CONS> : consensus_wsad_kernel<NSEG, WAVES, false, 2, CONS>;
   hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   return (int)hipGetLastError();
+}
+template <int NSEG>
+static int launch_wsad(const ExactParams& p, hipStream_t stream) {
+  return p.constrained ? launch_wsad_c<NSEG, true>(p, stream) : launch_wsad_c<NSEG, false>(p, stream);
 }
 
 }  // namespace svoc
@@ -508,7 +589,7 @@ extern "C" int svoc_exact_round_wsad(const ExactParams* p, hipStream_t stream) {
   // lane = column: with few columns most lanes idle, and for N <= 32 the i128 kernel packs 2-8
   // instances per wave instead (profiles/r2_exact_crossover.json: 7 x 6 140 M vs 10 M rounds/s,
   // 16 x 16 27 M vs 10 M; but 64 x 16 already 8.3 M vs 6.0 M for this kernel)
-  if (!p->constrained || p->N < 4 || p->N > 256) return -2;
+  if (p->N < 4 || p->N > 256) return -2;
   if (p->N <= 32 && p->D < p->wsad_min_d) return -2;
   if (!p->stage || !p->fallback) return -2;
   if ((int64_t)p->N * p->D * (p->val32 ? 4 : 8) >= (1ll << 31)) return -2;   // 32-bit buffer offsets

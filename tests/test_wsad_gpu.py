@@ -24,7 +24,7 @@ def _wsad(B, N, D, f, seed, a=20.0):
     return (x[:, :, :D] * 1e6).to(torch.int64).contiguous()
 
 
-def _run(values, f, env=None, active=None):
+def _run(values, f, env=None, active=None, constrained=True, ms=0):
     B, N, D = values.shape
     o = alloc_exact_out(B, N, D, values.device)
     old = {k: os.environ.get(k) for k in ("SVOC_EXACT_I128", "SVOC_EXACT_WSAD_ONLY", "SVOC_EXACT_WSAD_MIN_D")}
@@ -32,7 +32,7 @@ def _run(values, f, env=None, active=None):
         for k in old:
             os.environ.pop(k, None)
         os.environ.update(env or {})
-        svops.ops().exact_round(values, active, f, True, 0, o["c1"], o["consensus"], o["skew"], o["kurt"],
+        svops.ops().exact_round(values, active, f, constrained, ms, o["c1"], o["consensus"], o["skew"], o["kurt"],
                                 o["rel"], o["qr"], o["reliable"], o["status"], False)
         torch.cuda.synchronize()
     finally:
@@ -311,3 +311,96 @@ def test_wsad_kernel_reverts_in_kernel(N, D, f):
     ref3 = _run(v.to(DEV), f3, {"SVOC_EXACT_I128": "1"})
     assert torch.equal(fast3["status"], ref3["status"]), (fast3["status"], ref3["status"])
     assert (ref3["status"] != 0).all()
+
+
+# ---------------------------------------------------------------------------------------------------
+# Unconstrained rounds (contract.cairo:370-434) in the column kernel: signed int32-range values within
+# 2^25 (33.55 real units) of the column median / reliable mean; the essence is the reliable mean.
+
+MS = 10 * 1_000_000   # unconstrained_max_spread of the reference's tests (test_contract.cairo:253-261)
+
+
+def _signed(B, N, D, f, seed, honest_sd=1e6, fail_span=20e6, centre=3e6):
+    g = torch.Generator().manual_seed(seed)
+    x = centre + honest_sd * torch.randn(B, N, D, generator=g, dtype=torch.float64)
+    bad = torch.stack([torch.randperm(N, generator=g)[:f] for _ in range(B)])
+    fv = centre + fail_span * (2 * torch.rand(B, f, D, generator=g, dtype=torch.float64) - 1)
+    x.scatter_(1, bad[:, :, None].expand(B, f, D), fv)
+    return x.round().to(torch.int64).contiguous()
+
+
+def _cpu(v, f, constrained, ms):
+    B, N, D = v.shape
+    o = alloc_exact_out(B, N, D, "cpu")
+    svops.ops().exact_round(v.cpu().to(torch.int64), None, f, constrained, ms, o["c1"], o["consensus"], o["skew"],
+                            o["kurt"], o["rel"], o["qr"], o["reliable"], o["status"], False)
+    return o
+
+
+def test_wsad_kernel_unconstrained_golden():
+    values, constrained, ms, gold = GOLDEN["unconstrained_2d"]
+    assert not constrained
+    v = torch.tensor([values] * 3, dtype=torch.int64, device=DEV)
+    o = _run(v, N_FAILING, {"SVOC_EXACT_WSAD_ONLY": "1", "SVOC_EXACT_WSAD_MIN_D": "1"}, constrained=False, ms=ms)
+    assert o["status"].tolist() == [0, 0, 0]
+    assert o["c1"][0].tolist() == gold["c1"]
+    assert o["consensus"][2].tolist() == gold["consensus"]
+    assert o["rel"][1].tolist() == [gold["rel1"], gold["rel2"]]
+    assert o["skew"][0].tolist() == gold["skewness"]
+    assert o["kurt"][0].tolist() == gold["kurtosis"]
+    assert o["qr"][0].tolist() == gold["qr"]
+
+
+@pytest.mark.parametrize("N,D,f", [(7, 6, 2), (64, 1024, 8), (64, 100, 20), (100, 260, 10), (200, 136, 20),
+                                   (256, 300, 32)])
+@pytest.mark.parametrize("dtype", [torch.int64, torch.int32])
+def test_wsad_kernel_unconstrained_bit_exact(N, D, f, dtype):
+    """Every round of signed data with far failing oracles: the column kernel alone takes them all and
+    equals the i128 kernel and the CPU engine bit for bit."""
+    B = 12
+    v = _signed(B, N, D, f, seed=N * 7 + D)
+    fast = _run(v.to(DEV, dtype), f, {"SVOC_EXACT_WSAD_ONLY": "1", "SVOC_EXACT_WSAD_MIN_D": "1"}, constrained=False,
+                ms=MS)
+    ref = _run(v.to(DEV), f, {"SVOC_EXACT_I128": "1"}, constrained=False, ms=MS)
+    cpu = _cpu(v, f, False, MS)
+    assert (fast["status"] != -1).all(), fast["status"]        # nothing handed to the i128 kernel
+    for k in OUTS:
+        assert torch.equal(fast[k], ref[k]), k
+        assert torch.equal(fast[k], cpu[k]), k
+
+
+def test_wsad_kernel_unconstrained_domain_and_reverts():
+    """Out-of-domain instances (a deviation past 2^25, a value past int32) are handed to the i128 kernel;
+    reverts come out with the CPU engine's stage-ordered status; the dispatcher equals the CPU engine."""
+    B, N, D, f = 10, 64, 96, 8
+    v = _signed(B, N, D, f, seed=3)
+    v[1, 5, 7] = v[1, 5, 7] + 40_000_000            # |x - c1| > 2^25: out of the column kernel's domain
+    v[2, 9, 1] = 3_000_000_000                      # not an int32 (int64 storage)
+    v[3, :, 4] = -2_500_000                         # a zero-variance column -> DIV_BY_ZERO
+    v[4] = v[4] * 0 + 1_000_000                     # every value equal: DIV_BY_ZERO (variance 0)
+    v[5, :, :] = -v[5, :, :]                        # negative everything: a plain round
+    vg = v.to(DEV)
+    only = _run(vg, f, {"SVOC_EXACT_WSAD_ONLY": "1"}, constrained=False, ms=MS)
+    cpu = _cpu(v, f, False, MS)
+    st = only["status"].tolist()
+    assert st[1] == -1 and st[2] == -1, st
+    for i in (0, 3, 4, 5, 6, 7, 8, 9):
+        assert st[i] == cpu["status"][i].item(), (i, st, cpu["status"].tolist())
+    assert cpu["status"][3].item() != 0 and cpu["status"][4].item() != 0 and cpu["status"][5].item() == 0
+    comb = _run(vg, f, None, constrained=False, ms=MS)
+    for k in OUTS:
+        assert torch.equal(comb[k], cpu[k]), k
+
+
+@pytest.mark.parametrize("f,ms", [(62, MS), (64, MS), (65, MS), (8, 0), (8, 1)])
+def test_wsad_kernel_unconstrained_stage_order(f, ms):
+    """R = 2 (moments divide by zero), R = 0 (the mean divides by zero), f > N (usize underflow),
+    max_spread 0 (wsad_div by zero) and 1 (saturated reliability): the CPU engine's status, no fallback."""
+    B, N, D = 4, 64, 70
+    v = _signed(B, N, D, min(f, N), seed=f + ms)
+    only = _run(v.to(DEV), f, {"SVOC_EXACT_WSAD_ONLY": "1"}, constrained=False, ms=ms)
+    cpu = _cpu(v, f, False, ms)
+    assert only["status"].tolist() == cpu["status"].tolist()
+    comb = _run(v.to(DEV), f, None, constrained=False, ms=ms)
+    for k in OUTS:
+        assert torch.equal(comb[k], cpu[k]), k
