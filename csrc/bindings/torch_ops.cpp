@@ -65,11 +65,17 @@ void fast_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& a
                     at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim, bool legacy,
                     const c10::optional<at::Tensor>& work, const c10::optional<at::Tensor>& stats,
                     const c10::optional<at::Tensor>& upd_rows, const c10::optional<at::Tensor>& upd_oracle,
-                    const c10::optional<at::Tensor>& upd_status, int64_t upd_per_inst) {
+                    const c10::optional<at::Tensor>& upd_status, int64_t upd_per_inst,
+                    const c10::optional<at::Tensor>& rst_saved, const c10::optional<at::Tensor>& rst_saved_en,
+                    const c10::optional<at::Tensor>& rst_enabled, const c10::optional<at::Tensor>& rst_n_active) {
   (void)wave_hint;
   (void)work;
   (void)stats;   // (GPU pruned-network counter; the CPU twin runs full sorts)
   TORCH_CHECK(!upd_rows.has_value() || !upd_rows->defined(), "fused transactional streaming is a GPU path");
+  TORCH_CHECK(!rst_saved.has_value() || !rst_saved->defined(), "in-kernel rollback is a GPU path");
+  (void)rst_saved_en;
+  (void)rst_enabled;
+  (void)rst_n_active;
   (void)upd_oracle;
   (void)upd_status;
   (void)upd_per_inst;
@@ -119,7 +125,9 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
                     at::Tensor status, int64_t wave_hint, int64_t mode, int64_t rel_dim, bool legacy,
                     const c10::optional<at::Tensor>& work, const c10::optional<at::Tensor>& stats,
                     const c10::optional<at::Tensor>& upd_rows, const c10::optional<at::Tensor>& upd_oracle,
-                    const c10::optional<at::Tensor>& upd_status, int64_t upd_per_inst) {
+                    const c10::optional<at::Tensor>& upd_status, int64_t upd_per_inst,
+                    const c10::optional<at::Tensor>& rst_saved, const c10::optional<at::Tensor>& rst_saved_en,
+                    const c10::optional<at::Tensor>& rst_enabled, const c10::optional<at::Tensor>& rst_n_active) {
   fast_round_checks(values, D, c1, cons, skew, kurt, rel, qr, reliable, status);
   TORCH_CHECK(values.scalar_type() == at::kBFloat16 || values.scalar_type() == at::kFloat,
               "GPU fast path stores values in bf16 or fp32");
@@ -212,6 +220,40 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
     p.upd_oracle = upd_oracle->data_ptr<int64_t>();
     p.upd_status = upd_status->data_ptr<int32_t>();
     p.upd_per_inst = (int)upd_per_inst;
+  }
+  if (rst_saved.has_value() && rst_saved->defined()) {
+    // in-kernel rollback of the generic transactional path (launch.hpp FastParams.rst_saved): the update
+    // kernel's saved rows / flags and statuses for B * U instance-grouped updates; -3 from the dispatcher when
+    // the kernel that runs cannot do it (the caller then launches svoc_restore_updates)
+    TORCH_CHECK(!(upd_rows.has_value() && upd_rows->defined()), "rst_saved: not with the fused path's upd_rows");
+    TORCH_CHECK(mode == 0 && upd_per_inst > 0 && upd_oracle.has_value() && upd_status.has_value() &&
+                    rst_saved_en.has_value() && rst_enabled.has_value() && rst_n_active.has_value(),
+                "rst_saved: mode 0, with upd_oracle, upd_status, upd_per_inst, rst_saved_en, rst_enabled, rst_n_active");
+    const int64_t n = B * upd_per_inst;
+    TORCH_CHECK(rst_saved->scalar_type() == values.scalar_type() && rst_saved->is_contiguous() &&
+                    rst_saved->dim() == 2 && rst_saved->size(0) == n && rst_saved->size(1) == D,
+                "rst_saved: contiguous [B * U, D] in the values' dtype");
+    TORCH_CHECK(rst_saved_en->scalar_type() == at::kByte && rst_saved_en->is_contiguous() && rst_saved_en->numel() == n,
+                "rst_saved_en: contiguous uint8 [B * U]");
+    TORCH_CHECK(upd_oracle->scalar_type() == at::kLong && upd_oracle->is_contiguous() && upd_oracle->numel() == n,
+                "upd_oracle: contiguous int64 [B * U]");
+    TORCH_CHECK(upd_status->scalar_type() == at::kInt && upd_status->is_contiguous() && upd_status->numel() == n,
+                "upd_status: contiguous int32 [B * U]");
+    TORCH_CHECK(rst_enabled->scalar_type() == at::kByte && rst_enabled->is_contiguous() && rst_enabled->numel() == B * N,
+                "rst_enabled: contiguous uint8 [B, N]");
+    TORCH_CHECK(rst_n_active->scalar_type() == at::kInt && rst_n_active->is_contiguous() && rst_n_active->numel() == B,
+                "rst_n_active: contiguous int32 [B]");
+    p.rst_saved = rst_saved->data_ptr();
+    p.rst_saved_en = rst_saved_en->data_ptr<uint8_t>();
+    p.rst_oracle = upd_oracle->data_ptr<int64_t>();
+    p.rst_status = upd_status->data_ptr<int32_t>();
+    p.rst_enabled = rst_enabled->data_ptr<uint8_t>();
+    p.rst_n_active = rst_n_active->data_ptr<int32_t>();
+    p.rst_U = (int)upd_per_inst;
+    const int rc = f32 ? svoc_fast_round_f32(&p, stream) : svoc_fast_round_bf16(&p, stream);
+    TORCH_CHECK(rc == 0 || rc == -3, f32 ? "svoc_fast_round_f32" : "svoc_fast_round_bf16", " launch failed: ", rc);
+    TORCH_CHECK(rc == 0, "in-kernel rollback does not apply to this round (use restore_updates)");
+    return;
   }
   const int rc = f32 ? svoc_fast_round_f32(&p, stream) : svoc_fast_round_bf16(&p, stream);
   TORCH_CHECK(rc == 0, f32 ? "svoc_fast_round_f32" : "svoc_fast_round_bf16", " launch failed: ", rc);
@@ -333,7 +375,8 @@ TORCH_LIBRARY(svoc, m) {
       "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "
       "Tensor(g!) reliable, Tensor(h!) status, int wave_hint=0, int mode=0, int rel_dim=0, bool legacy=False, "
       "Tensor? work=None, Tensor(i!)? stats=None, Tensor? upd_rows=None, Tensor? upd_oracle=None, "
-      "Tensor(j!)? upd_status=None, int upd_per_inst=0) -> ()");
+      "Tensor(j!)? upd_status=None, int upd_per_inst=0, Tensor? rst_saved=None, Tensor? rst_saved_en=None, "
+      "Tensor(k!)? rst_enabled=None, Tensor(l!)? rst_n_active=None) -> ()");
   m.def(
       "exact_round(Tensor values, Tensor? active, int n_failing, bool constrained, int max_spread, "
       "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "

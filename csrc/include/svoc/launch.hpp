@@ -49,6 +49,19 @@ struct FastParams {
   const int64_t* upd_oracle;
   int32_t* upd_status;
   int upd_per_inst;
+  // In-kernel rollback of the generic transactional path (bf16 window kernel, mode 0; null rst_saved = off):
+  // updates b * rst_U .. b * rst_U + rst_U - 1 of this launch belong to instance b, and the update kernel
+  // saved what they overwrote (rst_saved [B * U, D] in the values' dtype, rst_saved_en the old `enabled`
+  // flags, kNotSaved where it wrote nothing).  A reverting workgroup copies the rows back, undoes first
+  // commits (`enabled`, n_active) and gives every applied update the round's status -- what
+  // svoc_restore_updates does, without its launch after the round.  (The state rows are written only then.)
+  const void* rst_saved;
+  const uint8_t* rst_saved_en;
+  const int64_t* rst_oracle;
+  int32_t* rst_status;
+  uint8_t* rst_enabled;
+  int32_t* rst_n_active;
+  int rst_U;
 };
 
 // Workspace per instance of the LDS-free fast kernels, in u32 words (Dp = fast_work_pairs(D)).

@@ -522,6 +522,7 @@ extern "C" int svoc_fast_round_f32(const FastParams* p, hipStream_t stream) {
     if (rc != -2) return rc;
   }
   if (p->upd_rows) return -3;   // fused transactional streaming exists in the window kernel only
+  if (p->rst_saved) return -3;  // in-kernel rollback: the bf16 window kernel only
   int rc;
   if (p->N <= 64) rc = launch_f32<1>(*p, stream);
   else if (p->N <= 128) rc = launch_f32<2>(*p, stream);

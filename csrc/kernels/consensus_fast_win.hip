@@ -250,7 +250,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   __shared__ int misc_i[3];     // status, zero-variance flag, cleanup list length
 
   const int b = blockIdx.x;
-  if (p.active && !p.active[b]) return;
+  if (p.active && !p.active[b]) return;   // (no round, no rollback: the instance keeps its updates)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid < 32) urow[tid] = 0;  // f < 32: unused slots still name a valid row
   if (tid == 0) misc_i[2] = 0;
@@ -274,6 +274,34 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   const uint32_t pol = group_polarity<NSEG>(seg);
   const uint32_t kp = 0x80008000u ^ pol;   // constrained key = raw ^ kp
   uint32_t* const stw = stage + (STAGE ? wave * 32 * 64 : 0);
+  // a reverting round's exit (uniform over the workgroup): the status, and with FastParams.rst_saved the
+  // rollback of this instance's saved update batch (launch.hpp)
+  auto revert = [&](int st) __attribute__((always_inline)) {
+    if (tid == 0) p.status[b] = st;
+    if (MODE != 0 || !p.rst_saved) return;
+    const int U = p.rst_U;
+    const int64_t u0 = (int64_t)b * U;
+    uint16_t* const vals = (uint16_t*)p.values + (int64_t)b * p.inst_stride;
+    for (int j = 0; j < U; ++j) {   // (uniform: every thread reads the same update)
+      const int64_t u = u0 + j;
+      if (p.rst_status[u] != ST_OK) continue;
+      const int64_t o = p.rst_oracle[u];
+      const uint8_t was = p.rst_saved_en[u];
+      if (o < 0 || o >= N || was == kNotSaved) continue;
+      const uint16_t* src = (const uint16_t*)p.rst_saved + u * D;
+      uint16_t* dst = vals + o * p.ld;
+      for (int c = tid; c < D; c += NT) dst[c] = src[c];
+      if (was == 0 && tid == 0) {
+        p.rst_enabled[(int64_t)b * N + o] = 0;
+        p.rst_n_active[b] -= 1;
+      }
+    }
+    __syncthreads();   // (every thread has read the statuses above)
+    for (int j = tid; j < U; j += NT) {
+      const int64_t u = u0 + j, o = p.rst_oracle[u];
+      if (p.rst_status[u] == ST_OK && o >= 0 && o < N) p.rst_status[u] = st;
+    }
+  };
 
   float acc[KEEP];
 #pragma unroll
@@ -482,7 +510,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   }
   __syncthreads();
   if (misc_i[0] != ST_OK) {
-    if (tid == 0) p.status[b] = misc_i[0];
+    revert(misc_i[0]);
     return;
   }
   const int npairs = (D + 1) >> 1;
@@ -527,7 +555,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
     if (zv) misc_i[1] = 1;
     __syncthreads();
     if (misc_i[1]) {
-      if (tid == 0) p.status[b] = ST_ZERO_VARIANCE;
+      revert(ST_ZERO_VARIANCE);
       return;
     }
   }
@@ -725,7 +753,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   // unconstrained: copied from the staging area, only when the round succeeded)
   if (!CONS) {
     if (misc_i[1]) {
-      if (tid == 0) p.status[b] = ST_ZERO_VARIANCE;
+      revert(ST_ZERO_VARIANCE);
       return;
     }
     commit_staged<NT>(ws, STG, D2, D, tid, p.consensus + ob, p.skew + ob, p.kurt + ob);
@@ -812,12 +840,14 @@ extern "C" int svoc_fast_round_bf16(const FastParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
   int rc;
   if (p->wave_hint == 0 && p->mode == 0 && p->N <= 16 && p->D <= 128) {
+    if (p->rst_saved) return -3;   // in-kernel rollback: the window kernel only
     return svoc_fast_round_bf16_small(p, stream);   // (commits c1 into c1_out itself)
   } else {
     if (p->wave_hint != -7) {
       rc = svoc_fast_round_bf16_win(p, stream);
       if (rc != -2) return rc;
     }
+    if (p->rst_saved) return -3;
     rc = svoc_fast_round_bf16_reg(p, stream);
   }
   if (rc == 0 && p->mode == 0 && p->c1_out)

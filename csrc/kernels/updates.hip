@@ -155,7 +155,10 @@ __global__ __launch_bounds__(256) void upd_apply_kernel(UpdateParams p) {
 // unique (instance, oracle) pairs (e.g. a synthetic stream, one bootstrap batch per window): no
 // last-writer resolution needed, so validation and the row copy run in one pass over the updates
 // (one read of the update rows instead of two)
-template <int L, int RB>
+// SAVE (transactional streaming, p.saved set): the rows being overwritten are loaded with the new ones and
+// saved; a separate instantiation, so the plain form keeps its register footprint (the save path's
+// conditional loads took the L = 64, RB = 8 kernel from 57 to 276 VGPRs when they shared one body)
+template <int L, int RB, bool SAVE>
 __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
   const int64_t u = ((int64_t)blockIdx.x * 256 + threadIdx.x) / L;
   const int sub = threadIdx.x & (L - 1);
@@ -178,18 +181,24 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
   const int64_t nch = row_bytes / 16;
   if (p.dtype <= 1 && vec && nch <= (int64_t)RB * L) {  // uniform over the launch
     uint4 v[RB];
-    u32x4 old[RB];   // transactional: the row being overwritten, loaded in the same batch (one round trip)
+    u32x4 old[SAVE ? RB : 1];   // transactional: the row being overwritten, loaded in the same batch
     bool ok = true, fin = true;
     const bool live = in;
-    const bool sv_on = p.saved != nullptr;   // uniform
 #pragma unroll
     for (int k = 0; k < RB; ++k) {
       const int64_t i = sub + (int64_t)k * L;
       u32x4 t = {0u, 0u, 0u, 0u};
       if (live && i < nch) t = __builtin_nontemporal_load((const u32x4*)src + i);
       v[k] = uint4{t.x, t.y, t.z, t.w};
-      old[k] = u32x4{0u, 0u, 0u, 0u};
-      if (sv_on && live && !bad && i < nch) old[k] = ((const u32x4*)dst)[i];
+    }
+    if constexpr (SAVE) {
+      // (bad indices: the row address is not dereferenced -- a clamped in-bounds slot is read instead)
+      const unsigned char* ds = bad ? (const unsigned char*)p.values : dst;
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        const int64_t i = sub + (int64_t)k * L;
+        old[k] = (live && i < nch) ? ((const u32x4*)ds)[i] : u32x4{0u, 0u, 0u, 0u};
+      }
     }
 #pragma unroll
     for (int k = 0; k < RB; ++k) {
@@ -214,7 +223,7 @@ __global__ __launch_bounds__(256) void upd_fused_unique_kernel(UpdateParams p) {
       if (st != ST_OK && p.saved_en) p.saved_en[u] = kNotSaved;
     }
     if (st != ST_OK) return;
-    if (sv_on) {   // (uniform) the old row, saved beside the update
+    if constexpr (SAVE) {   // the old row, saved beside the update
       u32x4* sv = (u32x4*)((unsigned char*)p.saved + u * row_bytes);
 #pragma unroll
       for (int k = 0; k < RB; ++k) {
@@ -350,10 +359,14 @@ static int launch_updates(const UpdateParams& p, hipStream_t stream) {
   if (p.unique) {
     // registers for the whole row: 8 16-B chunks per lane, 16 for rows past 8 * L chunks (fp32 c3)
     const int64_t nch = (int64_t)p.D * p.elem_bytes / 16;
-    if (L == 64 && nch > 8 * L)
-      hipLaunchKernelGGL((upd_fused_unique_kernel<L, 16>), dim3((unsigned)blocks), dim3(256), 0, stream, p);
-    else
-      hipLaunchKernelGGL((upd_fused_unique_kernel<L, 8>), dim3((unsigned)blocks), dim3(256), 0, stream, p);
+    const bool big = L == 64 && nch > 8 * L;
+    if (p.saved) {
+      if (big) hipLaunchKernelGGL((upd_fused_unique_kernel<L, 16, true>), dim3((unsigned)blocks), dim3(256), 0, stream, p);
+      else hipLaunchKernelGGL((upd_fused_unique_kernel<L, 8, true>), dim3((unsigned)blocks), dim3(256), 0, stream, p);
+    } else {
+      if (big) hipLaunchKernelGGL((upd_fused_unique_kernel<L, 16, false>), dim3((unsigned)blocks), dim3(256), 0, stream, p);
+      else hipLaunchKernelGGL((upd_fused_unique_kernel<L, 8, false>), dim3((unsigned)blocks), dim3(256), 0, stream, p);
+    }
     return (int)hipGetLastError();
   }
   hipLaunchKernelGGL(upd_validate_kernel<L>, dim3((unsigned)blocks), dim3(256), 0, stream, p);

@@ -32,6 +32,7 @@ Steady-state steps issue no host synchronisation, so they can be captured in a H
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional, Sequence
 
 import numpy as np
@@ -210,24 +211,44 @@ class ConsensusEngine:
                                  self.metrics_fx)
         self.rounds += 1
 
-    def _run_round_range(self, b0: int, b1: int, only_touched: bool = True, restore=None) -> None:
+    def _run_round_range(self, b0: int, b1: int, only_touched: bool = True, restore=None, U: int = 0) -> None:
         """run_round over instances [b0, b1) only (views of the state; fast mode); ``restore``: the
-        range's saved update batch (inst, oracle, st, saved, saved_en), rolled back where it reverted."""
+        range's saved update batch (inst, oracle, st, saved, saved_en), rolled back where it reverted --
+        by the round kernel itself when ``U`` (updates per instance, instance-grouped) is given and the
+        kernel supports it (:meth:`_kernel_rollback_ok`), else by the restore kernel after it."""
         sl = slice(b0, b1)
         self._ops.round_prologue(self.n_active[sl], self.touched[sl], self.N, bool(only_touched), self._active[sl])
         w = self.work()
         if w is not None:
             words = w.numel() // self.B
             w = w[b0 * words:b1 * words]
-        self._ops.fast_round(self.values[sl], self._active[sl], self.D, self.cfg.n_failing_oracles,
-                             self.cfg.constrained, float(self.cfg.unconstrained_max_spread), self.c1[sl],
-                             self.consensus[sl], self.skew[sl], self.kurt[sl], self.rel[sl], self.qr[sl],
-                             self.reliable[sl], self.status[sl], self.wave_hint, 0, 0, self.cfg.legacy, w,
-                             self._net_fb)
-        if restore is not None:
-            self._restore([restore])
+        args = (self.values[sl], self._active[sl], self.D, self.cfg.n_failing_oracles,
+                self.cfg.constrained, float(self.cfg.unconstrained_max_spread), self.c1[sl],
+                self.consensus[sl], self.skew[sl], self.kurt[sl], self.rel[sl], self.qr[sl],
+                self.reliable[sl], self.status[sl], self.wave_hint, 0, 0, self.cfg.legacy, w, self._net_fb)
+        if restore is not None and U > 0:
+            _, oracle, st, saved, saved_en = restore
+            self._all_active = False   # (a reverted first commit lowers n_active)
+            self._ops.fast_round(*args, None, oracle.contiguous(), st, U, saved, saved_en, self.enabled[sl],
+                                 self.n_active[sl])
+        else:
+            self._ops.fast_round(*args)
+            if restore is not None:
+                self._restore([restore])
         self._ops.round_epilogue(self._active[sl], self.status[sl], self.rel[sl], self.consensus_active[sl],
                                  self.touched[sl], self.metrics_fx)
+
+    def _kernel_rollback_ok(self, U: int) -> bool:
+        """Whether the round kernel itself rolls back a reverted instance's saved batch (FastParams.rst_saved):
+        the bf16 window kernel -- whole constrained rounds, 16 < N <= 256 (or D > 128: not the small-instance
+        kernel), f <= 32 with a window, U updates per instance."""
+        f = self.cfg.n_failing_oracles
+        if os.environ.get("SVOC_KERNEL_ROLLBACK", "1") == "0":   # (A/B: the restore kernel instead)
+            return False
+        return (self.mode == "fast" and self.device.type == "cuda" and self.vdtype == torch.bfloat16
+                and self.cfg.constrained and not self.cfg.legacy and self.wave_hint == 0
+                and 2 <= self.N <= 256 and (self.N > 16 or self.D > 128) and 0 <= f <= 32 and f <= self.N - 2
+                and bool(svops.fast_win_h(self.N, f)) and self.work() is not None and 0 < U)
 
     def _fused_ok(self, inst, oracle, vals, U: int) -> bool:
         """Whether a pipelined step can take the fused transactional path: fp32 storage on the GPU, whole
@@ -309,6 +330,7 @@ class ConsensusEngine:
         # fused transactional streaming (fp32 window kernel): the round reads the updated rows from the batch
         # and a commit kernel copies the accepted ones -- no saved copy, no restore (_fused_ok)
         fused = self.transactional and self._fused_ok(inst, oracle, vals, U)
+        kroll = self.transactional and not fused and self._kernel_rollback_ok(U)
         # per-step buffers live in the engine (the side streams use them after this returns): saved rows,
         # saved enabled flags and the update statuses, one slice per range
         if fused:
@@ -335,7 +357,7 @@ class ConsensusEngine:
                 self._run_round_range_fused(b0, b1, oracle[sl], vals[sl], st_all[sl], U)
                 return
             rest = (inst[sl], oracle[sl], st_all[sl], sv_all[sl], sen_all[sl]) if self.transactional else None
-            self._run_round_range(b0, b1, restore=rest)
+            self._run_round_range(b0, b1, restore=rest, U=U if (rest is not None and kroll) else 0)
         if overlap:
             # range k lives on stream sc[k] alone (update, then round; the next step's update of range k
             # queues behind this round on the same stream: no cross-stream waits).  The streams start

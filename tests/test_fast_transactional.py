@@ -112,12 +112,16 @@ def test_non_transactional_keeps_rows():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("overlap", [False, True])
-def test_pipelined_step_restores_reverted_instances(overlap):
-    """step_pipelined (per-range update + round + restore on side streams) == step() on a batch where
+@pytest.mark.parametrize("storage", ["fp32", "bf16"])
+def test_pipelined_step_restores_reverted_instances(overlap, storage):
+    """step_pipelined (per-range update + round + rollback on side streams: the fused fp32 path, the bf16
+    window kernel's in-kernel rollback) == step() (update kernel, round, restore kernel) on a batch where
     some instances revert (eager and overlapped across steps)."""
     N, D, B = 64, 512, 8
     U = N                            # every oracle of every instance publishes
-    ref, pipe = _engine("cuda", N=N, D=D, B=B), _engine("cuda", N=N, D=D, B=B)
+    ref, pipe = _engine("cuda", storage, N=N, D=D, B=B), _engine("cuda", storage, N=N, D=D, B=B)
+    if storage == "bf16":
+        assert pipe._kernel_rollback_ok(U)
     for e in (ref, pipe):
         e.randomize(seed=3)
         e.run_round()
@@ -172,3 +176,38 @@ def test_fused_streaming_matches_generic_path(N, D, f, U):
     assert fz.status[4].item() == int(Status.ZERO_VARIANCE)
     for k in ("status", "values", "enabled", "n_active", "consensus", "rel", "c1", "reliable", "skew", "kurt", "qr"):
         assert torch.equal(getattr(fz, k), getattr(gen, k)), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,D,f,U", [(256, 1024, 32, 64), (64, 700, 8, 16), (200, 300, 20, 50)])
+def test_bf16_kernel_rollback_matches_restore_kernel(N, D, f, U):
+    """bf16 pipelined step: the window kernel's in-kernel rollback (FastParams.rst_saved) equals the restore
+    kernel after the round bit for bit -- state, enabled / n_active, outputs, update statuses -- with
+    reverting instances (zero variance) among succeeding ones."""
+    B = 6
+    cfg = ConsensusConfig(n_oracles=N, dimension=D, n_failing_oracles=f, constrained=True)
+    kr = ConsensusEngine(cfg, batch=B, device="cuda", mode="fast", storage="bf16")
+    rk = ConsensusEngine(cfg, batch=B, device="cuda", mode="fast", storage="bf16")
+    for e in (kr, rk):
+        e.randomize(seed=N + D)
+        e.run_round()
+    rk._kernel_rollback_ok = lambda U: False
+    g = torch.Generator(device="cuda").manual_seed(5)
+    inst = torch.arange(B, device="cuda").repeat_interleave(U)
+    orc = torch.stack([torch.randperm(N, device="cuda", generator=g)[:U] for _ in range(B)]).reshape(-1)
+    vals = torch.rand(B * U, D, device="cuda", generator=g)
+    for e in (kr, rk):                 # instances 1 and 4: one column constant -> zero variance (revert)
+        e.values[1, :, 3] = 0.625
+        e.values[4, :, 7] = 0.25
+    vals[1 * U:2 * U, 3] = 0.625
+    vals[4 * U:5 * U, 7] = 0.25
+    for e in (kr, rk):
+        e.step_pipelined(inst, orc, vals, U, chunks=2, overlap=False)
+    torch.cuda.synchronize()
+    st_k = kr._save_bufs[("pipe",)][2][:B * U]
+    st_r = rk._save_bufs[("pipe",)][2][:B * U]
+    assert torch.equal(st_k, st_r)
+    assert kr.status[1].item() == int(Status.ZERO_VARIANCE) and kr.status[4].item() == int(Status.ZERO_VARIANCE)
+    assert (st_k.view(B, U)[1] == int(Status.ZERO_VARIANCE)).all()
+    for k in ("status", "values", "enabled", "n_active", "consensus", "rel", "c1", "reliable", "skew", "kurt", "qr"):
+        assert torch.equal(getattr(kr, k), getattr(rk, k)), k
