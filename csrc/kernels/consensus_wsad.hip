@@ -478,41 +478,58 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     const double isd = 1.0 / sd;
     // z-score powers (math.cairo:320-363), reliable rows only (a masked row has z = 0: all powers 0)
     double s3 = 0.0, s4 = 0.0;
-    uint64_t olm = 0;   // rows whose z^2 passes 2^25 (|z| >= 5.79): their powers are summed exactly below
+    bool outl = false;   // a row with z^2 >= 2^25 (|z| >= 5.79): this column's sums are redone below
     // z-score powers of one row (a masked row has z = 0: all powers 0)
-    auto zpow = [&](uint32_t x, uint32_t mk, int i) {
+    auto zpow = [&](uint32_t x, uint32_t mk) {
       const double dx = mk ? xv(x) - mu : 0.0;
       const double z = wdiv_d(dx, sd, isd);
       const double z2 = wmul_d(z, z);
-      const bool inb = z2 < 33554432.0;   // 2^25: keeps every product below wmul_d's 2^50 bound
-      olm |= (uint64_t)(inb ? 0u : 1u) << i;
-      s3 += inb ? wmul_d(z2, z) : 0.0;
-      s4 += inb ? wmul_d(z2, z2) : 0.0;
+      outl = outl || !(z2 < 33554432.0);   // 2^25: keeps every product below wmul_d's 2^50 bound
+      s3 += wmul_d(z2, z);
+      s4 += wmul_d(z2, z2);
     };
     if constexpr (BATCH) {
       load_lo(rs, after(vo, sd), rowb, xr);
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bound the fp64 temporaries in flight
-        zpow(xr[i], bit_mask(mm, i), i);
+        zpow(xr[i], bit_mask(mm, i));
       }
     } else {
 #pragma unroll 8
-      for (int i = 0; i < 64; ++i) zpow(wload<V32>(rs, vo, i * rowb, hw_), bit_mask(mm, i), i);
+      for (int i = 0; i < 64; ++i) zpow(wload<V32>(rs, vo, i * rowb, hw_), bit_mask(mm, i));
     }
-    // outlier rows (rare; a reliable row far from the mean): the same z and z^2 (exact in fp64), then
-    // wsad_mul(z^2, z) and wsad_mul(z^2, z^2) in int64 -- |z| <= sqrt(R - 1) in real units keeps both
-    // products below 2^63 (signed_decimal.cairo:110-112: truncation toward zero, as int64 division)
-    while (olm) {
-      const int i = __builtin_ctzll(olm);
-      olm &= olm - 1;
-      uint32_t hwo;
-      const uint32_t x = wload<V32>(rs, vo, i * rowb, hwo);
-      const double z = wdiv_d(xv(x) - mu, sd, isd);
-      const int64_t zi = (int64_t)z, z2i = (int64_t)wmul_d(z, z);
-      if (z2i > (1ll << 40)) bad = true;   // (impossible for |z| <= sqrt(R - 1); kept as a guard)
-      s3 += (double)((z2i * zi + 500000ll) / 1000000ll);
-      s4 += (double)((z2i * z2i + 500000ll) / 1000000ll);
+    // a column with outlier rows (rare; a reliable row far from the mean) is summed again, row by row: the
+    // same z and z^2 (exact in fp64), and for the outliers wsad_mul(z^2, z) / wsad_mul(z^2, z^2) in int64
+    // -- |z| <= sqrt(R - 1) in real units keeps both products below 2^63 (signed_decimal.cairo:110-112:
+    // truncation toward zero, as int64 division).  The fast loop above stays as lean as without outliers.
+    if (outl) {
+      s3 = 0.0;
+      s4 = 0.0;
+#pragma nounroll
+      for (int g = 0; g < 64; g += 8) {   // 8 rows per step: their loads in flight together
+        uint32_t xg[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          uint32_t hwo;
+          xg[k] = wload<V32>(rs, vo, (g + k) * rowb, hwo);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const uint32_t mk = bit_mask(mm, g + k);
+          const double z = wdiv_d(mk ? xv(xg[k]) - mu : 0.0, sd, isd);
+          const double z2 = wmul_d(z, z);
+          if (z2 < 33554432.0) {
+            s3 += wmul_d(z2, z);
+            s4 += wmul_d(z2, z2);
+          } else {
+            const int64_t zi = (int64_t)z, z2i = (int64_t)z2;
+            if (z2i > (1ll << 40)) bad = true;   // (impossible for |z| <= sqrt(R - 1); kept as a guard)
+            s3 += (double)((z2i * zi + 500000ll) / 1000000ll);
+            s4 += (double)((z2i * z2i + 500000ll) / 1000000ll);
+          }
+        }
+      }
     }
     s3 = group_sum<NSEG, P>(s3);
     s4 = group_sum<NSEG, P>(s4);
