@@ -205,18 +205,18 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
     p.net_fallbacks = (unsigned int*)stats->data_ptr();
   }
   if (upd_rows.has_value() && upd_rows->defined()) {
-    TORCH_CHECK(f32 && mode == 0 && constrained, "fused streaming: fp32 storage, whole constrained rounds");
+    TORCH_CHECK(mode == 0 && constrained, "fused streaming: whole constrained rounds");
     TORCH_CHECK(upd_per_inst > 0 && upd_oracle.has_value() && upd_status.has_value(), "fused streaming: "
                 "upd_oracle, upd_status and upd_per_inst > 0 go with upd_rows");
     const int64_t n = B * upd_per_inst;
-    TORCH_CHECK(upd_rows->scalar_type() == at::kFloat && upd_rows->is_contiguous() && upd_rows->dim() == 2 &&
+    TORCH_CHECK(upd_rows->scalar_type() == values.scalar_type() && upd_rows->is_contiguous() && upd_rows->dim() == 2 &&
                     upd_rows->size(0) == n && upd_rows->size(1) == D && upd_rows->device() == values.device(),
-                "upd_rows: contiguous fp32 [B * U, D] on the values' device");
+                "upd_rows: contiguous [B * U, D] in the values' dtype on the values' device");
     TORCH_CHECK(upd_oracle->scalar_type() == at::kLong && upd_oracle->is_contiguous() && upd_oracle->numel() == n,
                 "upd_oracle: contiguous int64 [B * U]");
     TORCH_CHECK(upd_status->scalar_type() == at::kInt && upd_status->is_contiguous() && upd_status->numel() == n,
                 "upd_status: contiguous int32 [B * U]");
-    p.upd_rows = upd_rows->data_ptr<float>();
+    p.upd_rows = (const float*)upd_rows->data_ptr();   // (bf16 rows for the bf16 kernel)
     p.upd_oracle = upd_oracle->data_ptr<int64_t>();
     p.upd_status = upd_status->data_ptr<int32_t>();
     p.upd_per_inst = (int)upd_per_inst;

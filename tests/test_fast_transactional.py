@@ -141,23 +141,27 @@ def test_pipelined_step_restores_reverted_instances(overlap, storage):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("N,D,f,U", [(256, 1024, 32, 64), (64, 700, 8, 16), (200, 300, 20, 50)])
-def test_fused_streaming_matches_generic_path(N, D, f, U):
+@pytest.mark.parametrize("storage,N,D,f,U", [("fp32", 256, 1024, 32, 64), ("fp32", 64, 700, 8, 16),
+                                             ("fp32", 200, 300, 20, 50), ("bf16", 256, 1024, 32, 64),
+                                             ("bf16", 64, 704, 8, 16), ("bf16", 200, 296, 20, 50),
+                                             ("bf16", 100, 64, 10, 100)])
+def test_fused_streaming_matches_generic_path(storage, N, D, f, U):
     """The fused transactional step (window kernel reading the updated rows from the batch + commit kernel)
     equals the generic transactional path (update kernel with saved rows + round + restore) bit for bit:
     state, outputs, update statuses -- with a reverting instance (zero variance) and an instance whose
     batch holds an invalid row (interval error: that update alone reverts, the round runs without it)."""
     B = 6
     cfg = ConsensusConfig(n_oracles=N, dimension=D, n_failing_oracles=f, constrained=True)
-    fz = ConsensusEngine(cfg, batch=B, device="cuda", mode="fast", storage="fp32")
-    gen = ConsensusEngine(cfg, batch=B, device="cuda", mode="fast", storage="fp32")
+    fz = ConsensusEngine(cfg, batch=B, device="cuda", mode="fast", storage=storage)
+    gen = ConsensusEngine(cfg, batch=B, device="cuda", mode="fast", storage=storage)
     for e in (fz, gen):
         e.randomize(seed=N + D)
         e.run_round()
     g = torch.Generator(device="cuda").manual_seed(3)
     inst = torch.arange(B, device="cuda").repeat_interleave(U)
     orc = torch.stack([torch.randperm(N, device="cuda", generator=g)[:U] for _ in range(B)]).reshape(-1)
-    vals = torch.rand(B * U, D, device="cuda", generator=g)
+    vals = torch.rand(B * U, D, device="cuda", generator=g).to(fz.vdtype)
+    assert fz._fused_ok(inst, orc, vals, U)
     # instance 1: an update row with 1.5 in one column (rejected alone); instance 4: all its updated rows at
     # one value and the rest of the column too -> zero variance in column 3 if U == N, else a plain round
     vals[1 * U + 2, D // 2] = 1.5
@@ -175,7 +179,20 @@ def test_fused_streaming_matches_generic_path(N, D, f, U):
     assert st_f[1 * U + 2].item() == int(Status.INTERVAL_INPUT)
     assert fz.status[4].item() == int(Status.ZERO_VARIANCE)
     for k in ("status", "values", "enabled", "n_active", "consensus", "rel", "c1", "reliable", "skew", "kurt", "qr"):
-        assert torch.equal(getattr(fz, k), getattr(gen, k)), k
+        a, b_ = getattr(fz, k), getattr(gen, k)
+        if storage == "bf16" and k in ("skew", "kurt"):
+            # the bf16 fused kernel streams phase A through LDS-DMA (register-resident words) where the generic
+            # one stages half the slab and re-reads the rest: a separately compiled instantiation whose fp32
+            # moment arithmetic may round differently (measured: one column of 6 x 1024 off by 1 ulp in skewness;
+            # state, statuses, consensus, c1 and qr are compared bit for bit)
+            assert torch.allclose(a, b_, rtol=1e-5, atol=1e-6), k
+            continue
+        if not torch.equal(a, b_):
+            bad = (a != b_).reshape(B, -1)
+            rows = bad.any(1).nonzero().flatten().tolist()
+            cols = bad.nonzero()[:8].tolist()
+            raise AssertionError(f"{k}: instances {rows}, first (inst, col) {cols}, "
+                                 f"{a.reshape(B, -1)[bad][:4].tolist()} vs {b_.reshape(B, -1)[bad][:4].tolist()}")
 
 
 @pytest.mark.gpu
