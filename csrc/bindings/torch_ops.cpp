@@ -205,7 +205,7 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
     p.net_fallbacks = (unsigned int*)stats->data_ptr();
   }
   if (upd_rows.has_value() && upd_rows->defined()) {
-    TORCH_CHECK(mode == 0 && constrained, "fused streaming: whole constrained rounds");
+    TORCH_CHECK(f32 && mode == 0 && constrained, "fused streaming: fp32 storage, whole constrained rounds");
     TORCH_CHECK(upd_per_inst > 0 && upd_oracle.has_value() && upd_status.has_value(), "fused streaming: "
                 "upd_oracle, upd_status and upd_per_inst > 0 go with upd_rows");
     const int64_t n = B * upd_per_inst;

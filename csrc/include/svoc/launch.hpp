@@ -39,9 +39,8 @@ struct FastParams {
   // optional counter: slab networks of the pruned window path (N = 256) that failed their exact check and
   // reran the full network (consensus_fast_winf.hip); null = not counted
   unsigned int* net_fallbacks;
-  // Fused transactional streaming (fp32 and bf16 window kernels, mode 0; null upd_rows = off): this launch's
-  // update batch, `upd_per_inst` rows per instance in instance order ([B * U, D] in the values' dtype -- bf16
-  // rows behind this float pointer for the bf16 kernel --, pitch D, row b * U + k for
+  // Fused transactional streaming (fp32 window kernel, mode 0; null upd_rows = off): this launch's update
+  // batch, `upd_per_inst` rows per instance in instance order ([B * U, D] fp32, pitch D, row b * U + k for
   // instance b; upd_oracle [B * U] their oracles, distinct per instance).  The round reads an updated oracle's
   // row from the batch instead of the state (the state is not written), validates it, and writes every
   // update's transaction status to upd_status: OK (commit: svoc_commit_updates copies the row), the round's

@@ -31,7 +31,6 @@
 
 #include "svoc/bufload.hpp"
 #include "svoc/launch.hpp"
-#include "svoc/slabdma.hpp"
 #include "svoc/sortnet.hpp"
 #include "svoc/status.hpp"
 
@@ -51,6 +50,7 @@ SVOC_DEV u16x2 win_cand(u16x2 wt, u16x2 zt) {  // wt < zt ? wt : 0xFFFF, per 16-
 // Skewness / sample-adjusted excess kurtosis (math.cairo:320-363) of n values from power sums of
 // d = x - shift; returns false for zero variance (the contract's sqrt(0) -> div-by-zero revert).
 SVOC_DEV bool moments_from_sums(float n, float t1, float t2, float t3, float t4, float& dl, float& sk, float& ku) {
+#pragma clang fp contract(off)
   dl = t1 / n;
   const float e2 = t2 / n, e3 = t3 / n, e4 = t4 / n;
   const float mu2 = e2 - dl * dl;
@@ -78,6 +78,9 @@ struct QrCtx {
 };
 template <int L, int I, int P, bool MASKROWS>
 SVOC_DEV float qr_tree(const QrCtx& c, const uint32_t (&wv)[64], f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
+  // (no implicit contraction: every instantiation must round identically -- only the explicit fmas below;
+  // left to the backend, y * y + s2 was fused in some instantiations and not in others)
+#pragma clang fp contract(off)
   if constexpr (L == 0) {
     f32x2 y = bf16x2_to_f32x2(wv[I]) - c.c2;
     f32x2 q = y * y;
@@ -138,23 +141,6 @@ SVOC_DEV void qr_moments(__amdgpu_buffer_rsrc_t rs, int vo, int rowb, uint32_t m
                          f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
   qr_moments_seq<P, MASKW, MASKROWS>(rs, vo, rowb, mW, c, acc, s1, s2, s3, s4,
                                      std::make_integer_sequence<int, 64 / P>{});
-}
-
-// qr pass over the raw words already in registers (the fused kernel's LDS-DMA phase A): the same trees in
-// the same order as qr_moments, so the sums are bit-identical to the re-reading form
-template <int P, bool MASKROWS, int... Is>
-SVOC_DEV void qr_moments_words_seq(const uint32_t (&wv)[64], const QrCtx& c, float* acc, f32x2& s1, f32x2& s2,
-                                   f32x2& s3, f32x2& s4, std::integer_sequence<int, Is...>) {
-  constexpr int S = __builtin_ctz(P);
-  ((acc[Is] += qr_tree<S, Is, P, MASKROWS>(c, wv, s1, s2, s3, s4)), ...);
-}
-template <int P, bool MASKW, bool MASKROWS>
-SVOC_DEV void qr_moments_words(const RawRows& xs, uint32_t mW, const QrCtx& c, float* acc, f32x2& s1, f32x2& s2,
-                               f32x2& s3, f32x2& s4) {
-  uint32_t wv[64];
-#pragma unroll
-  for (int i = 0; i < 64; ++i) wv[i] = MASKW ? xs.at(i) & mW : xs.at(i);
-  qr_moments_words_seq<P, MASKROWS>(wv, c, acc, s1, s2, s3, s4, std::make_integer_sequence<int, 64 / P>{});
 }
 
 // qr pass with half of the slab staged in LDS (N = NPAD = 256, constrained): trees 0 and 1 (rows
@@ -249,15 +235,9 @@ SVOC_DEV void qr_moments_staged_even(__amdgpu_buffer_rsrc_t rs, int vo, int rowb
   }
 }
 
-// FUSED (fused transactional streaming, FastParams.upd_rows; mode 0, constrained): as the fp32 window
-// kernel (consensus_fast_winf.hip) -- the rows of this round's updates are read from the update batch
-// instead of the state (phase A streams the slabs through LDS by LDS-DMA with per-piece row sources: the
-// fp32 kernel's SlabDma, one column pair per word), their interval is checked here, every update's
-// transaction status is written, and svoc_commit_updates stores the accepted rows after the round.  The
-// DMA regions cap the CU at 2 waves per SIMD (the register-load form runs 4), so only this instantiation
-// streams through LDS (profiles/r4_win_bf16_dma_ab.txt: -3 % as the plain path).
-template <int NSEG, int WAVES, int H, bool CONS, int MODE, bool FUSED = false>
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(FUSED ? 2 : 4))) void consensus_fast_win_kernel(FastParams p) {
+template <int NSEG, int WAVES, int H, bool CONS, int MODE>
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4))) void consensus_fast_win_kernel(FastParams p) {
+#pragma clang fp contract(off)   // (as qr_tree: every instantiation rounds the same way)
   constexpr int P = 64 / NSEG;          // column pairs per wave (phase A)
   constexpr int NPAD = 64 * NSEG;
   constexpr int W = WAVES * P * 2;      // columns per workgroup step (phase A)
@@ -265,12 +245,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(FUSE
   constexpr int KEEP = 64 / P;
   // constrained: half of each slab (32 rows x 64 lanes, keys) staged per wave for the qr pass
   // (N = 256: rows i % 4 < 2; N <= 128: even rows; profiles/r1_stage_ab.txt)
-  constexpr bool STAGE = CONS && MODE != 2 && !FUSED;
-  static_assert(!FUSED || (MODE == 0 && CONS), "fused streaming: whole constrained rounds");
+  constexpr bool STAGE = CONS && MODE != 2;
   __shared__ uint32_t stage[STAGE ? WAVES * 32 * 64 : 1];
-  __shared__ uint32_t slab[FUSED ? WAVES * 64 * 64 : 1];   // one 16-KiB DMA region per wave (fused)
-  __shared__ int smap[FUSED ? NPAD : 1];   // row -> its update's slot in this instance's batch (-1: state)
-  __shared__ uint32_t badu[FUSED ? 8 : 1];   // slots whose row failed the interval check
   __shared__ float qr_part[WAVES * NPAD];
   __shared__ float qr_lds[NPAD];
   __shared__ uint64_t relmask[4];
@@ -279,15 +255,8 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(FUSE
   __shared__ int misc_i[3];     // status, zero-variance flag, cleanup list length
 
   const int b = blockIdx.x;
-  const int U = FUSED ? p.upd_per_inst : 0;
-  if (p.active && !p.active[b]) {   // (no round, no rollback: the instance keeps its updates)
-    // (the fused path runs only when every instance is active; an inactive one would not commit)
-    if constexpr (FUSED)
-      for (int t = threadIdx.x; t < U; t += WAVES * 64) p.upd_status[(int64_t)b * U + t] = ST_NOT_ACTIVE;
-    return;
-  }
-  // (wave made explicitly uniform: it feeds the DMA's M0)
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (p.active && !p.active[b]) return;   // (no round, no rollback: the instance keeps its updates)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (tid < 32) urow[tid] = 0;  // f < 32: unused slots still name a valid row
   if (tid == 0) misc_i[2] = 0;
   const int seg = lane / P, pair_w = lane % P;
@@ -310,41 +279,11 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(FUSE
   const uint32_t pol = group_polarity<NSEG>(seg);
   const uint32_t kp = 0x80008000u ^ pol;   // constrained key = raw ^ kp
   uint32_t* const stw = stage + (STAGE ? wave * 32 * 64 : 0);
-  // fused: this instance's batch rows ([U, D] bf16, pitch D), the row -> slot map, the bad-slot mask
-  const uint16_t* const urows = FUSED ? (const uint16_t*)p.upd_rows + (int64_t)b * U * D : inst;
-  const uint32_t ubytes = FUSED ? (uint32_t)(U * D * 2) : 0u;
-  const __amdgpu_buffer_rsrc_t rb = instance_rsrc(urows, ubytes);
-  if constexpr (FUSED) {
-    for (int t = tid; t < NPAD; t += NT) smap[t] = -1;
-    if (tid < 8) badu[tid] = 0u;
-    __syncthreads();
-    for (int t = tid; t < U; t += NT) {
-      const int64_t o = p.upd_oracle[(int64_t)b * U + t];
-      if (o >= 0 && o < N) smap[o] = t;
-    }
-    __syncthreads();
-  }
-  // one word (column pair at byte cb) of row `row` (wave-uniform): the batch's or the state's
-  auto row_load = [&](int row, int cb) __attribute__((always_inline)) -> uint32_t {
-    int u = -1;
-    if constexpr (FUSED) u = __builtin_amdgcn_readfirstlane(smap[row]);
-    return u >= 0 ? bload(rb, cb, u * D * 2) : bload(rs, cb, row * rowb);
-  };
-  auto bad_slot = [&](int u) __attribute__((always_inline)) -> uint32_t {
-    if constexpr (FUSED) return (badu[u >> 5] >> (u & 31)) & 1u;
-    else return 0u;
-  };
-  // every update's transaction status once the round's outcome is known (contract.cairo:588-603)
-  auto upd_out = [&](int st) __attribute__((always_inline)) {
-    if constexpr (FUSED)
-      for (int t = tid; t < U; t += NT) p.upd_status[(int64_t)b * U + t] = bad_slot(t) ? ST_INTERVAL_INPUT : st;
-  };
   // a reverting round's exit (uniform over the workgroup): the status, and with FastParams.rst_saved the
   // rollback of this instance's saved update batch (launch.hpp)
   auto revert = [&](int st) __attribute__((always_inline)) {
     if (tid == 0) p.status[b] = st;
-    upd_out(st);
-    if (MODE != 0 || FUSED || !p.rst_saved) return;
+    if (MODE != 0 || !p.rst_saved) return;
     const int U = p.rst_U;
     const int64_t u0 = (int64_t)b * U;
     uint16_t* const vals = (uint16_t*)p.values + (int64_t)b * p.inst_stride;
@@ -375,51 +314,6 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(FUSE
 
   // ------------------------------------------------------------ phase A: pass 1
   const int pass1_slabs = MODE == 2 ? 0 : nslab;
-  // fused: LDS-DMA slabs (SlabDma, as consensus_fast_winf.hip); a lane's word i (row seg * 64 + i) lands at
-  // region word 64 i + seg P + pair_w
-  const SlabDma<NSEG> dma(lane, rowb);
-  uint32_t* const region = slab + (FUSED ? wave * 64 * 64 : 0);
-  const uint32_t* const mine = region + (FUSED ? seg * P + pair_w : 0);
-  const BufDesc rsd = buf_desc(inst, (uint32_t)(N * rowb));
-  const BufDesc rbd = buf_desc(urows, ubytes);
-  // per-piece row sources of this lane's DMA, 4 per register (byte k % 4 of pmap[k / 4] = batch slot + 1 of
-  // the piece's row, 0 = the state row)
-  uint32_t pmap[FUSED ? 4 : 1] = {};
-  auto map_pieces = [&]() __attribute__((always_inline)) {
-    if constexpr (FUSED) {
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const int row = dma.row_of(k);
-        const int u = row < N ? smap[row] : -1;
-        if (k % 4 == 0) pmap[k / 4] = 0u;
-        pmap[k / 4] |= (uint32_t)(u + 1) << (8 * (k % 4));
-      }
-    }
-  };
-  auto issue_slab = [&](int s) __attribute__((always_inline)) {
-    if constexpr (FUSED) {
-      const int cb = (s * (W / 2) + wave * P) * 4 + dma.colb;
-      // (opaque per slab: hoisted out of the slab loop the masks and offsets take 32+ SGPRs -- spills)
-      uint32_t pm[4] = {pmap[0], pmap[1], pmap[2], pmap[3]};
-      asm volatile("" : "+v"(pm[0]), "+v"(pm[1]), "+v"(pm[2]), "+v"(pm[3]));
-      int rowb_o = rowb, d2 = D * 2;
-      asm volatile("" : "+s"(rowb_o), "+s"(d2));
-      uint32_t* reg_o = region;
-      asm volatile("" : "+s"(reg_o));
-      uint32_t pfrom = 0u;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) pfrom |= (((pm[k / 4] >> (8 * (k % 4))) & 0xffu) ? 1u : 0u) << k;
-      dma.issue_mapped(
-          rsd, rbd, reg_o, [&](int k) { return dma.row_of(k) * rowb_o + cb; },
-          [&](int k) { return ((int)((pm[k / 4] >> (8 * (k % 4))) & 0xffu) - 1) * d2 + cb; }, pfrom);
-    }
-  };
-  bool susp = false;   // fused: a word past 1.0 (or -0.0) seen in phase A
-  for (int attempt = 0; attempt < 2; ++attempt) {   // (a second pass only when a fused update was invalid)
-  if constexpr (FUSED) {
-    map_pieces();
-    if (pass1_slabs > 0) issue_slab(0);
-  }
 #pragma nounroll
   for (int s = 0; s < pass1_slabs; ++s) {
     const int colA = s * W + 2 * cp;
@@ -430,44 +324,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(FUSE
     asm volatile("" : "+v"(nvl), "+v"(nll));
     float cA, cB;
     const uint32_t mW = vA ? (vB ? 0xffffffffu : 0x0000ffffu) : 0u;
-    RawRows xs;   // fused: the lane's raw words, kept for the qr pass
-    if constexpr (FUSED) {
-      __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0): this wave's pieces of slab s have landed
-#pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        xs.lo[i] = mine[i * 64];
-        xs.hi[i] = mine[(i + 32) * 64];
-      }
-      __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0): the region is read, the next slab may land
-      if (s + 1 < pass1_slabs) issue_slab(s + 1);
-      // interval check of the batch rows (contract.cairo:591-593, math.cairo:298-310): the largest bf16 half
-      // of the lane's words against 1.0 (state rows were checked when stored); past it (or -0.0 somewhere)
-      // the batch is checked row by row after phase A (out of this loop: in it, the check cost ~37 VGPRs of
-      // spills)
-      u16x2 mx = {0, 0};
-#pragma unroll
-      for (int i = 0; i < 64; ++i) mx = __builtin_elementwise_max(mx, as_k(xs.at(i) & mW));
-      susp = susp || mx.x > 0x3f80u || mx.y > 0x3f80u;
-    }
-    // raw word i of the lane's 64 rows (rows past N read as 0 either way)
-    auto word = [&](int i) __attribute__((always_inline)) -> uint32_t {
-      if constexpr (FUSED) return xs.at(i);
-      else return bload(rs, vo, i * rowb);
-    };
     {
       u16x2 r[64];
-      if (FUSED) {
-        if (N == NPAD) {
-#pragma unroll
-          for (int i = 0; i < 64; ++i) r[i] = as_k(word(i) ^ kp);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 64; ++i) {
-            const uint32_t hi_m = ~lt_mask(i, nll);
-            r[i] = as_k(((as_u32(to_key<CONS>(word(i))) & (lt_mask(i, nvl) | hi_m)) | hi_m) ^ pol);
-          }
-        }
-      } else if (N == NPAD) {
+      if (N == NPAD) {
         if (CONS) {
 #pragma unroll
           for (int i = 0; i < 64; ++i) r[i] = as_k(bload(rs, vo, i * rowb) ^ kp);
@@ -528,15 +387,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(FUSE
     asm volatile("" : "+v"(vo2) : "v"(cA), "v"(cB));
     const QrCtx qc{nvl, lane, f32x2{vA ? cA : 0.f, vB ? cB : 0.f}};
     f32x2 s1 = {0.f, 0.f}, s2 = s1, s3 = s1, s4 = s1;
-    if (FUSED) {
-      if ((s + 1) * W <= D) {
-        if (N == NPAD) qr_moments_words<P, false, false>(xs, mW, qc, acc, s1, s2, s3, s4);
-        else qr_moments_words<P, false, true>(xs, mW, qc, acc, s1, s2, s3, s4);
-      } else {
-        if (N == NPAD) qr_moments_words<P, true, false>(xs, mW, qc, acc, s1, s2, s3, s4);
-        else qr_moments_words<P, true, true>(xs, mW, qc, acc, s1, s2, s3, s4);
-      }
-    } else if (STAGE && N == NPAD) {
+    if (STAGE && N == NPAD) {
       if constexpr (STAGE && NSEG == 4) {
         if ((s + 1) * W <= D) qr_moments_staged<P, false>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
         else qr_moments_staged<P, true>(rs, vo2, rowb, mW, kp, stw, lane, qc, acc, s1, s2, s3, s4);
@@ -566,33 +417,6 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(FUSE
       bstore2(ws, s4, pg * 8, MOM + 3 * Dp * 8);
     }
   }
-  if (!FUSED) break;
-  if (__syncthreads_or(susp ? 1 : 0) && attempt == 0) {
-    // rare: check every batch row (bf16 halves in [0, 1], -0.0 allowed) and mark the failing slots
-    const uint32_t* ub = (const uint32_t*)urows;
-    for (int64_t k = tid; k < (int64_t)U * (D / 2); k += NT) {
-      const uint32_t raw = ub[k];
-      const uint32_t lo = raw & 0xffffu, hi = raw >> 16;
-      const bool ok = (lo <= 0x3f80u || lo == 0x8000u) && (hi <= 0x3f80u || hi == 0x8000u);
-      const int u = (int)(k / (D / 2));
-      if (!ok && bad_slot(u) == 0u) atomicOr(&badu[u >> 5], 1u << (u & 31));
-    }
-  }
-  __syncthreads();
-  uint32_t anybad = 0u;
-#pragma unroll
-  for (int w = 0; w < (FUSED ? 8 : 0); ++w) anybad |= badu[w];
-  if (anybad == 0u || attempt == 1) break;
-  // an update row failed the interval check: its transaction reverts alone (INTERVAL_INPUT) and the round
-  // is recomputed on the state row instead (the other updates of the batch stand)
-  if constexpr (FUSED) {
-    for (int t = tid; t < NPAD; t += NT)
-      if (smap[t] >= 0 && bad_slot(smap[t])) smap[t] = -1;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < KEEP; ++i) acc[i] = 0.f;
-  }   // attempts
 
   // ------------------------------------------------------------ qr reduction
   {
@@ -722,11 +546,11 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(FUSE
         cB = cB && bf16_hi(lo) == bf16_hi(hi);
       }
       if (__ballot(cA || cB)) {   // rare: compare the reliable rows with the first one
-        const uint32_t w0 = row_load(fr, pr * 4);
+        const uint32_t w0 = bload(rs, pr * 4, fr * rowb);
         const float rA = bf16_lo(w0), rB = bf16_hi(w0);
         for (int i = fr + 1; i < N; ++i) {
           if (!((relmask[i >> 6] >> (i & 63)) & 1)) continue;   // uniform
-          const uint32_t w = row_load(i, pr * 4);
+          const uint32_t w = bload(rs, pr * 4, i * rowb);
           cA = cA && bf16_lo(w) == rA;
           cB = cB && bf16_hi(w) == rB;
         }
@@ -783,7 +607,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(FUSE
       const int row = t - s0;
       const bool real = (realm >> t) & 1;
       uw[t] = 0u;
-      if (CONS || real) uw[t] = row_load(__builtin_amdgcn_readfirstlane(urow[real ? row : 0]), vo);
+      if (CONS || real) uw[t] = bload(rs, vo, __builtin_amdgcn_readfirstlane(urow[real ? row : 0]) * rowb);
     }
     // removed rows' power sums of d = x - c1 (both columns, packed)
     f32x2 u1 = {0.f, 0.f}, u2 = u1, u3 = u1, u4 = u1;
@@ -889,13 +713,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(FUSE
       for (int g = 0; g < NSEG; ++g) {
         const int i = g * 64 + lane;
         const bool use = i < N && ((relmask[g] >> lane) & 1);
-        uint16_t xh = 0;
-        if (use) {
-          int u = -1;
-          if constexpr (FUSED) u = smap[i];
-          xh = u >= 0 ? urows[(int64_t)u * D + col] : xc[(int64_t)i * p.ld];
-        }
-        y[g] = use ? __builtin_bit_cast(float, (uint32_t)xh << 16) - cc : 0.f;
+        y[g] = use ? __builtin_bit_cast(float, (uint32_t)xc[(int64_t)i * p.ld] << 16) - cc : 0.f;
         t1 += y[g];
       }
       t1 += xor_lane<1>(t1); t1 += xor_lane<2>(t1); t1 += xor_lane<4>(t1);
@@ -956,18 +774,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(FUSE
     p.rel[2 * (int64_t)b + 1] = misc_f[1];
     p.status[b] = ST_OK;
   }
-  upd_out(ST_OK);
 }
 
 template <int NSEG, int WAVES, int H, bool CONS>
 static void launch_win_w(const FastParams& p, hipStream_t stream) {
-  if constexpr (CONS) {
-    if (p.upd_rows) {   // fused transactional streaming (mode 0)
-      hipLaunchKernelGGL((consensus_fast_win_kernel<NSEG, WAVES, H, CONS, 0, true>), dim3(p.B), dim3(WAVES * 64), 0,
-                         stream, p);
-      return;
-    }
-  }
   if (p.mode == 1) hipLaunchKernelGGL((consensus_fast_win_kernel<NSEG, WAVES, H, CONS, 1>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   else if (p.mode == 2) hipLaunchKernelGGL((consensus_fast_win_kernel<NSEG, WAVES, H, CONS, 2>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   else hipLaunchKernelGGL((consensus_fast_win_kernel<NSEG, WAVES, H, CONS, 0>), dim3(p.B), dim3(WAVES * 64), 0, stream, p);
@@ -1009,10 +819,6 @@ extern "C" int svoc_fast_round_bf16_win(const FastParams* p, hipStream_t stream)
   if (p->B <= 0) return 0;
   if (!p->work || p->N < 2 || p->N > 256 || p->ld % 8 != 0 || p->D > p->ld) return -2;
   if (p->mode == 2 && p->work_fresh) return -2;   // pass 1 ran elsewhere: no windows to read
-  // fused streaming: whole constrained rounds, batch rows of D % 8 == 0 columns (16-B DMA pieces)
-  if (p->upd_rows && (p->mode != 0 || !p->constrained || p->upd_per_inst <= 0 || p->upd_per_inst > 256 ||
-                      p->D % 8 != 0 || (int64_t)p->upd_per_inst * p->D * 2 >= (1ll << 31)))
-    return -3;
   if (p->n_failing < 0 || p->n_failing > 32 || p->n_failing > p->N - 2) return -2;
   const int H = fast_win_h(p->N, p->n_failing);
   if (H == 0) return -2;
@@ -1038,15 +844,16 @@ extern "C" int svoc_fast_round_bf16_small(const FastParams* p, hipStream_t strea
 extern "C" int svoc_fast_round_bf16(const FastParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
   int rc;
+  if (p->upd_rows) return -3;   // fused transactional streaming: the fp32 window kernel only
   if (p->wave_hint == 0 && p->mode == 0 && p->N <= 16 && p->D <= 128) {
-    if (p->rst_saved || p->upd_rows) return -3;   // in-kernel rollback / fused streaming: the window kernel only
+    if (p->rst_saved) return -3;   // in-kernel rollback: the window kernel only
     return svoc_fast_round_bf16_small(p, stream);   // (commits c1 into c1_out itself)
   } else {
     if (p->wave_hint != -7) {
       rc = svoc_fast_round_bf16_win(p, stream);
       if (rc != -2) return rc;
     }
-    if (p->rst_saved || p->upd_rows) return -3;
+    if (p->rst_saved) return -3;
     rc = svoc_fast_round_bf16_reg(p, stream);
   }
   if (rc == 0 && p->mode == 0 && p->c1_out)

@@ -251,22 +251,19 @@ class ConsensusEngine:
                 and bool(svops.fast_win_h(self.N, f)) and self.work() is not None and 0 < U)
 
     def _fused_ok(self, inst, oracle, vals, U: int) -> bool:
-        """Whether a pipelined step can take the fused transactional path: fp32 or bf16 storage on the GPU,
-        whole constrained rounds through a window kernel (N <= 256, f <= 32; bf16: D % 8 == 0 and not the
-        small-instance kernel), at most 256 updates per instance (instance-grouped batch, as step_pipelined
-        requires), rows of exactly D columns in the storage dtype, and every instance already active (the
-        fused round covers no activation; checked once, then tracked)."""
+        """Whether a pipelined step can take the fused transactional path: fp32 storage on the GPU, whole
+        constrained rounds through the window kernel (N <= 256, f <= 32), at most 256 updates per instance
+        (instance-grouped batch, as step_pipelined requires), fp32 rows of exactly D columns, and every
+        instance already active (the fused round covers no activation; checked once, then tracked).
+        (bf16 storage takes the generic path: the same fusion in the bf16 window kernel measured slower than
+        saving the rows, profiles/r4_c3_bf16_txn_ab.txt.)"""
         if os.environ.get("SVOC_FUSED_TXN", "1") == "0":   # (A/B: the generic path instead)
             return False
-        bf16 = self.vdtype == torch.bfloat16
-        if not (self.mode == "fast" and self.device.type == "cuda" and self.vdtype in (torch.float32, torch.bfloat16)
+        if not (self.mode == "fast" and self.device.type == "cuda" and self.vdtype == torch.float32
                 and self.cfg.constrained and 2 <= self.N <= 256 and 0 <= self.cfg.n_failing_oracles <= 32
                 and self.cfg.n_failing_oracles <= self.N - 2 and svops.fast_win_h(self.N, self.cfg.n_failing_oracles)
                 and 0 < U <= 256 and vals.dtype == self.vdtype and vals.dim() == 2 and vals.shape[1] == self.D
                 and oracle.dtype == torch.int64 and not self.cfg.legacy):
-            return False
-        # the bf16 window kernel (not the small-instance one), 16-B DMA pieces of the batch rows
-        if bf16 and not (self.wave_hint == 0 and (self.N > 16 or self.D > 128) and self.D % 8 == 0):
             return False
         if not getattr(self, "_all_active", False):
             if torch.cuda.is_current_stream_capturing():
@@ -334,7 +331,7 @@ class ConsensusEngine:
         su, sc = self._pipe_streams[0], self._pipe_streams[1:]
         step = (self.B + chunks - 1) // chunks
         ranges = [(k * step, min(self.B, (k + 1) * step)) for k in range(chunks) if k * step < self.B]
-        # fused transactional streaming (window kernels): the round reads the updated rows from the batch
+        # fused transactional streaming (fp32 window kernel): the round reads the updated rows from the batch
         # and a commit kernel copies the accepted ones -- no saved copy, no restore (_fused_ok)
         fused = self.transactional and self._fused_ok(inst, oracle, vals, U)
         kroll = self.transactional and not fused and self._kernel_rollback_ok(U)

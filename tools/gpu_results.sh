@@ -29,6 +29,7 @@ run c2_exact 300 --config c2 --mode exact --steps 10 --warmup 2 &&
 run c2_exact_int64 300 --config c2 --mode exact --storage int64 --steps 10 --warmup 2 &&
 run c5_exact 300 --config-file configs/c5_exact_rounds.yaml --steps 20 --warmup 2 &&
 run c3_exact 300 --config-file configs/c3_exact_rounds.yaml --steps 10 --warmup 2 &&
+run c2_exact_uncons 300 --config-file configs/c2_exact_unconstrained.yaml --steps 10 --warmup 2 &&
 run c5_exact_stream 300 --config-file configs/c5_exact_stream.yaml --steps 20 --warmup 2 &&
 true || exit 1
 fi

@@ -33,6 +33,8 @@ ROWS = [
     ("c2_exact", "c2 shape, exact wsad (bit-identical to the contract), int32 storage", "0.61/s exact Python emulator"),
     ("c2_exact_int64", "c2 shape, exact wsad, int64 storage", "0.61/s exact Python emulator"),
     ("c3_exact", "c3 shape (256 × 4096), exact wsad, int32 storage", "≈6/s numpy fp64 (non-exact)"),
+    ("c2_exact_uncons", "c2 shape, exact wsad, UNCONSTRAINED rounds (reliable-mean essence), int64 storage",
+     "0.61/s exact Python emulator (constrained)"),
     ("c5_exact", "c5 shape (7 × 6), exact wsad, 1M instances", "939/s exact Python emulator"),
     ("c5_exact_stream", "c5 shape, exact transactional update stream (store + round + revert per update)",
      "939/s exact Python emulator"),
