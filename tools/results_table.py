@@ -21,11 +21,11 @@ RESULTS = os.path.join(ROOT, "profiles", "results.jsonl")
 ROWS = [
     ("c1", "c1: 4 oracles × 2 dims, one exact round, CPU (plumbing)", "2,518/s Python emulator (7×2)"),
     ("c2", "c2: 64 × 1024, 10k batched instances, bf16", "≈93/s numpy fp64"),
-    ("c3", "c3: 256 × 4096 streaming, failing-oracle masking, fp32 storage (headline: reference resolution)",
-     "≈6/s numpy fp64"),
+    ("c3", "c3: 256 × 4096 streaming, failing-oracle masking, fp32 storage, transactional (headline: reference "
+           "resolution)", "≈6/s numpy fp64"),
     ("c3_notxn", "c3, coalesced without transactions (a reverted batch's rows stay; the round-3 headline form)",
      "≈6/s numpy fp64"),
-    ("c3_bf16", "c3 shape, fast mode over bf16 storage", "≈6/s numpy fp64"),
+    ("c3_bf16", "c3 shape, fast mode over bf16 storage, transactional", "≈6/s numpy fp64"),
     ("c4", "c4: BERT-base sentiment oracles → consensus", "—"),
     ("c5", "c5: governance + reliability stream, 1M instances (7 × 6)", "≈127,900/s numpy fp64 (7×6)"),
     ("c2_fp32", "c2 shape, fast mode over fp32 storage (reference resolution)", "≈93/s numpy fp64"),
