@@ -122,15 +122,19 @@ def _ds_exact_worker(rank, world, port, outdir, x, cfgd):
     dist.destroy_process_group()
 
 
-def test_dsharding_exact_two_ranks_on_one_gpu():
-    """Exact (wsad) D-sharding on the GPU i128 kernel's split modes: bit-identical to one whole round."""
+@pytest.mark.parametrize("constrained", [True, False])
+def test_dsharding_exact_two_ranks_on_one_gpu(constrained):
+    """Exact (wsad) D-sharding on the GPU split modes (column kernel, i128 kernel for what it hands over;
+    unconstrained: signed values): bit-identical to one whole round."""
     from helpers import beta_oracles
     from svoc.config import ConsensusConfig
     from svoc.engine import ConsensusEngine
     B, N, D, f = 6, 64, 200, 8
     x, _ = beta_oracles(B, N, D, f, seed=9, dtype=torch.float64)
     x = (x[:, :, :D] * 1e6).to(torch.int64).contiguous()
-    cfgd = dict(n_oracles=N, dimension=D, n_failing_oracles=f, constrained=True)
+    if not constrained:
+        x = x * 3 - 1_500_000          # signed, wider than [0, 1e6]
+    cfgd = dict(n_oracles=N, dimension=D, n_failing_oracles=f, constrained=constrained, unconstrained_max_spread=1.0)
     ref = ConsensusEngine(ConsensusConfig(**cfgd), B, device="cuda", mode="exact")
     ref.values.copy_(x.to("cuda", ref.values.dtype))
     ref.enabled.fill_(1); ref.n_active.fill_(N); ref.touched.fill_(1)
