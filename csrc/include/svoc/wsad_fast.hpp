@@ -17,21 +17,30 @@
 
 namespace svoc {
 
-// floor(t / d) for integral 0 <= t < 2^51 and integral 1 <= d < 2^31, given inv = 1.0 / d.
+// The reciprocal floor_div_d takes: 1 / d (rounded to nearest) scaled by (1 - 2^-48).  It lies below 1 / d
+// by more than 2^-49 relative -- so t * inv, rounded, stays below t / d and its floor is never too large --
+// and by less than 2^-47.8 -- so it falls short of t / d by less than 1 while t / d < 2^47.
+SVOC_HD double recip_lo(double d) { return (1.0 / d) * (1.0 - 0x1p-48); }
+
+// floor(t / d) for integral 0 <= t < 2^51, integral 1 <= d < 2^31 and quotient below 2^47 (every use in
+// the exact kernel: qdev and wsad_mul quotients < 2^31, wsad_div's < 2^47 for divisors >= 16 or inside
+// wsqrt's Newton steps, means / variances < 2^39), given inv = recip_lo(d).  The estimate is the quotient
+// or one less, so a single one-sided remainder test fixes it (one compare and one add fewer than a
+// two-sided test around a rounded-to-nearest reciprocal).
 SVOC_HD double floor_div_d(double t, double d, double inv) {
-  double q = floor(t * inv);          // |error| of t * inv < 0.5: q is the quotient or one off
-  const double r = fma(-q, d, t);     // exact remainder (a small integer)
-  q = r < 0.0 ? q - 1.0 : (r >= d ? q + 1.0 : q);
-  return q;
+  const double q = floor(t * inv);    // floor(t / d) or one less
+  const double r = fma(-q, d, t);     // exact remainder (an integer in [0, 2d))
+  return r >= d ? q + 1.0 : q;
 }
 
-// I128Div(a, d) = trunc(a / d) toward zero (signed_decimal.cairo:52-63) for |a| < 2^51, 1 <= d < 2^31.
+// I128Div(a, d) = trunc(a / d) toward zero (signed_decimal.cairo:52-63) for |a| < 2^51, 1 <= d < 2^31, a
+// quotient below 2^47; inv = recip_lo(d).
 SVOC_HD double trunc_div_d(double a, double d, double inv) {
   const double q = floor_div_d(fabs(a), d, inv);
   return a < 0.0 ? -q : q;
 }
 
-constexpr double kW = 1e6, kInvW = 1e-6, kHalfW = 5e5;
+constexpr double kW = 1e6, kInvW = (1.0 / 1e6) * (1.0 - 0x1p-48), kHalfW = 5e5;   // kInvW = recip_lo(1e6)
 
 // wsad_mul(a, b) = I128Div(a * b + HALF_WSAD, WSAD) for |a * b| < 2^50 (signed_decimal.cairo:110-112).
 SVOC_HD double wmul_d(double a, double b) { return trunc_div_d(fma(a, b, kHalfW), kW, kInvW); }
@@ -42,8 +51,8 @@ SVOC_HD double qdev_d(double a, double b) {
   return floor_div_d(fma(d, d, kHalfW), kW, kInvW);
 }
 
-// wsad_div(a, b) = I128Div(a * WSAD + I128Div(b, 2), b) for 1 <= b < 2^31, |a| < 2^31
-// (signed_decimal.cairo:114-116); inv = 1.0 / b.
+// wsad_div(a, b) = I128Div(a * WSAD + I128Div(b, 2), b) for 1 <= b < 2^31, |a| < 2^31 and a quotient below
+// 2^47 (signed_decimal.cairo:114-116); inv = recip_lo(b).
 SVOC_HD double wdiv_d(double a, double b, double inv) {
   return trunc_div_d(fma(a, kW, floor(b * 0.5)), b, inv);
 }
@@ -61,7 +70,7 @@ SVOC_HD bool wsqrt_d(double v, double& out) {
   for (int i = 0; i < MAX_SQRT_ITERATIONS; ++i) {
     if (g == g2) break;
     if (g == 0.0) return false;
-    const double n = wdiv_d(v, g, 1.0 / g);
+    const double n = wdiv_d(v, g, recip_lo(g));   // (quotient <= max(2e6, sqrt(v * 1e6)): Newton from above)
     g2 = g;
     g = floor((g + n) * 0.5);
   }

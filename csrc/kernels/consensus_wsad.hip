@@ -364,8 +364,8 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   // ------------------------------------------------------------ pass 2 (contract.cairo:476-500)
   const uint64_t mymask = relmask[seg];
   const uint64_t mylow = lowmask[seg];
-  const double Rd = (double)R, invR = 1.0 / Rd;
-  const double k3 = (double)((R - 1) * (R - 2)), ik3 = 1.0 / k3;
+  const double Rd = (double)R, invR = recip_lo(Rd);
+  const double k3 = (double)((R - 1) * (R - 2)), ik3 = recip_lo(k3);
   bool bad = false;   // a result this kernel cannot represent: the i128 kernel recomputes the round
   bool dz = false;    // the contract divides by zero in the moments: the round reverts
 #pragma nounroll
@@ -475,7 +475,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     double sd = 1.0;
     const bool ok_sd = var >= 2.0 && wsqrt_d(var, sd);
     if (vc && !ok_sd) dz = true;   // sqrt(0) -> wsad_div by 0, sqrt(1) divides by 0: DIV_BY_ZERO
-    const double isd = 1.0 / sd;
+    const double isd = recip_lo(sd);
     // z-score powers (math.cairo:320-363), reliable rows only (a masked row has z = 0: all powers 0)
     double s3 = 0.0, s4 = 0.0;
     bool outl = false;   // a row with z^2 >= 2^25 (|z| >= 5.79): this column's sums are redone below

@@ -6,6 +6,7 @@
 // Checks: the reference fixture's golden outputs (contract/tests/test_contract.cairo:
 // 150-158), threaded batch == sequential single-instance results (exact and fast engines),
 // governance state machine invariants, and a .svoc save/load round trip with CRC verification.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -158,10 +159,11 @@ static void wsad_fast_paths() {
     if ((int64_t)wmul_d((double)z, (double)y) != (int64_t)wmul(z, y, st)) ++bad;
     // wsad_div by a standard deviation
     const int64_t num = uni(-1000000, 1000000), sd = uni(1, 2000000);
-    if ((int64_t)wdiv_d((double)num, (double)sd, 1.0 / (double)sd) != (int64_t)wdiv(num, sd, st)) ++bad;
-    // truncating division (means, variances)
-    const int64_t s = uni(-(1ll << 50), 1ll << 50), d = uni(1, 1 << 30);
-    if ((int64_t)trunc_div_d((double)s, (double)d, 1.0 / (double)d) != (int64_t)idiv(s, d, st)) ++bad;
+    if ((int64_t)wdiv_d((double)num, (double)sd, recip_lo((double)sd)) != (int64_t)wdiv(num, sd, st)) ++bad;
+    // truncating division (means, variances): dividends below 2^51, quotients below 2^47 (the stated bound)
+    const int64_t d = it % 4 == 0 ? uni(1, 16) : uni(16, 1 << 30);
+    const int64_t s = d < 16 ? uni(-(1ll << 46), 1ll << 46) : uni(-(1ll << 50), 1ll << 50);
+    if ((int64_t)trunc_div_d((double)s, (double)d, recip_lo((double)d)) != (int64_t)idiv(s, d, st)) ++bad;
     // sqrt of variances
     if (it % 16 == 0) {
       const int64_t v = it % 32 == 0 ? uni(0, 2000000) : uni(0, (1ll << 31) - 1);
@@ -182,13 +184,13 @@ static void wsad_fast_paths() {
   }
   // boundary quotients: remainders 0 and d - 1 around large dividends
   for (int64_t d : {(int64_t)1, (int64_t)2, (int64_t)3, (int64_t)7, (int64_t)1000000, (int64_t)999983, (int64_t)((1ll << 31) - 1)}) {
-    for (int64_t q : {(int64_t)0, (int64_t)1, (int64_t)12345, (int64_t)((1ll << 51) / d - 2)}) {
+    for (int64_t q : {(int64_t)0, (int64_t)1, (int64_t)12345, std::min((int64_t)((1ll << 51) / d - 2), (int64_t)((1ll << 47) - 1))}) {
       for (int64_t r : {(int64_t)0, d - 1}) {
         const int64_t t = q * d + r;
         if (t >= (1ll << 51)) continue;
         int st = ST_OK;
-        CHECK((int64_t)trunc_div_d((double)t, (double)d, 1.0 / (double)d) == (int64_t)idiv(t, d, st));
-        CHECK((int64_t)trunc_div_d(-(double)t, (double)d, 1.0 / (double)d) == (int64_t)idiv(-t, d, st));
+        CHECK((int64_t)trunc_div_d((double)t, (double)d, recip_lo((double)d)) == (int64_t)idiv(t, d, st));
+        CHECK((int64_t)trunc_div_d(-(double)t, (double)d, recip_lo((double)d)) == (int64_t)idiv(-t, d, st));
       }
     }
   }
