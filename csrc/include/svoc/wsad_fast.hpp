@@ -36,8 +36,11 @@ SVOC_HD double floor_div_d(double t, double d, double inv) {
 // I128Div(a, d) = trunc(a / d) toward zero (signed_decimal.cairo:52-63) for |a| < 2^51, 1 <= d < 2^31, a
 // quotient below 2^47; inv = recip_lo(d).
 SVOC_HD double trunc_div_d(double a, double d, double inv) {
-  const double q = floor_div_d(fabs(a), d, inv);
-  return a < 0.0 ? -q : q;
+  // the same one-sided estimate on the signed dividend: trunc(a * inv) is the quotient or one step short
+  // toward zero, and the remainder (same sign as a) says which -- no absolute value / sign restore
+  const double q = trunc(a * inv);
+  const double r = fma(-q, d, a);     // exact, |r| < 2d
+  return fabs(r) >= d ? q + copysign(1.0, a) : q;
 }
 
 constexpr double kW = 1e6, kInvW = (1.0 / 1e6) * (1.0 - 0x1p-48), kHalfW = 5e5;   // kInvW = recip_lo(1e6)
