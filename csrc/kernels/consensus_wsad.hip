@@ -100,6 +100,13 @@ SVOC_DEV void qtree_all(const uint32_t (&q)[64], int lane, uint64_t* acc, std::i
   ((acc[Is] += qtree<__builtin_ctz(P), Is, P>(q, lane)), ...);
 }
 
+// |x - c| < 2^25 for int32 x, c, in integer arithmetic (the unconstrained domain check; fp64 forms of it
+// held the 64 rows' conversions live and cost ~120 VGPRs): both within 2^30 of 0, so x - c cannot wrap
+SVOC_DEV bool near25(uint32_t x, uint32_t c) {
+  const bool small = (x + (1u << 30)) < (1u << 31) && (c + (1u << 30)) < (1u << 31);
+  return small && (x - c + ((1u << 25) - 1u)) < ((1u << 26) - 1u);
+}
+
 // The same butterfly with 64-bit partial sums (unconstrained: a deviation's qdev may reach 2^31)
 template <int L, int I, int P>
 SVOC_DEV uint64_t qtree64(const uint32_t (&q)[64], int lane) {
@@ -134,9 +141,9 @@ SVOC_DEV T group_sum(T v) {
 // to the i128 kernel's same mode through p.fallback, as in mode 0.
 // CONS = false: unconstrained rounds (contract.cairo:370-434): signed values, pass-2 consensus = the reliable
 // mean (no second network), reliabilities W - wsad_div(min(ms, sqrt(mean qr)), ms).  Domain (else the
-// i128 kernel): int32 values within 2^25 (33.55 in real units) of their column's smooth median and of
-// its reliable mean -- the bound under which the fp64 forms of qdev / wsad_div are exact (wsad_fast.hpp);
-// the qr butterfly then sums 64-bit partials.
+// i128 kernel): values within 2^30 of 0 (1073.7 in real units) and within 2^25 (33.55) of their column's
+// smooth median and of its reliable mean -- the bound under which the fp64 forms of qdev / wsad_div are
+// exact (wsad_fast.hpp); the qr butterfly then sums 64-bit partials.
 template <int NSEG, int WAVES, bool V32, int MODE, bool CONS>
 __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams p) {
   constexpr int P = 64 / NSEG;      // columns per wave
@@ -183,7 +190,6 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   const int seg_off = seg * 64 * rowb;
   const uint32_t pol = group_polarity<NSEG>(seg);
   uint32_t badv = 0;                     // a value outside [0, 1e6]
-  uint32_t hw_;                          // (high words of re-read values: validated in pass 1)
 
   uint64_t acc[KEEP];
 #pragma unroll
@@ -203,11 +209,11 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       uint32_t r[64];
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
-        uint32_t hw;
-        const uint32_t x = wload<V32>(rs, vo, i * rowb, hw);
+        // (the low word only: int64 rows get their high words checked below, 8 rows at a time -- loaded
+        // here they held 64 more VGPRs and cost the int64 kernels their second wave per SIMD)
+        const uint32_t x = bload(rs, vo, i * rowb);
         const bool real = i < nv;
-        if constexpr (CONS) badv |= (vc && real && (x > kWsadMax || hw != 0)) ? 1u : 0u;   // outside [0, 1e6]
-        else if constexpr (!V32) badv |= (vc && real && hw != (uint32_t)((int32_t)x >> 31)) ? 1u : 0u;   // not an int32
+        if constexpr (CONS) badv |= (vc && real && x > kWsadMax) ? 1u : 0u;   // outside [0, 1e6]
         r[i] = (real ? x ^ kSign : (i < nl ? 0u : ~0u)) ^ pol;
       }
       uint32_t lo, hi;
@@ -229,19 +235,35 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bound the fp64 temporaries in flight
-        if (!CONS) badv |= (vc && i < nv && !(fabs(xv(q[i]) - cd) < 33554432.0)) ? 1u : 0u;   // 2^25
+        if (!CONS) badv |= (vc && i < nv && !near25(q[i], c1)) ? 1u : 0u;   // |x - c1| < 2^25
         q[i] = (vc && i < nv) ? (uint32_t)qdev_d(xv(q[i]), cd) : 0u;
       }
     } else {
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
-        const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
-        if (!CONS) badv |= (vc && i < nv && !(fabs(xv(x) - cd) < 33554432.0)) ? 1u : 0u;
+        const uint32_t x = bload(rs, vo, i * rowb);   // (low word; int64 high words are checked below)
+        if (!CONS) badv |= (vc && i < nv && !near25(x, c1)) ? 1u : 0u;
         q[i] = (vc && i < nv) ? (uint32_t)qdev_d(xv(x), cd) : 0u;
       }
     }
     if constexpr (CONS) qtree_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
     else qtree64_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
+    if constexpr (!V32) {
+      // int64 storage: the high words, 8 rows in flight -- 0 (constrained: [0, 1e6]) or the sign extension
+      // of the low word (unconstrained: an int32)
+#pragma nounroll
+      for (int g = 0; g < 64; g += 8) {
+        uint32_t hw[8], lw[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          hw[k] = bload(rs, vo + 4, (g + k) * rowb);
+          lw[k] = CONS ? 0u : bload(rs, vo, (g + k) * rowb);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          badv |= (vc && g + k < nv && hw[k] != (CONS ? 0u : (uint32_t)((int32_t)lw[k] >> 31))) ? 1u : 0u;
+      }
+    }
   }
   {
     int base = 0;
@@ -389,8 +411,8 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       } else {
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
-          uint32_t hw;
-          const uint32_t x = wload<V32>(rs, vo, i * rowb, hw);
+          uint32_t hw = 0u;
+          const uint32_t x = MODE == 2 ? wload<V32>(rs, vo, i * rowb, hw) : bload(rs, vo, i * rowb);
           if (MODE == 2) badv |= (vc && i < nv && (x > kWsadMax || hw != 0)) ? 1u : 0u;   // no pass 1 here
           const uint32_t mk = bit_mask(mm, i), low = bit_mask(ml, i);
           r[i] = ((x & mk) | (~low & ~mk)) ^ pol;   // reliable: key; else -inf (low) / +inf
@@ -422,7 +444,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
         for (int i = 0; i < 64; ++i) sx += xr[i] & bit_mask(mm, i);
       } else {
 #pragma unroll 16
-        for (int i = 0; i < 64; ++i) sx += wload<V32>(rs, vo, i * rowb, hw_) & bit_mask(mm, i);
+        for (int i = 0; i < 64; ++i) sx += bload(rs, vo, i * rowb) & bit_mask(mm, i);
       }
       sx = group_sum<NSEG, P>(sx);
       mu = floor_div_d((double)sx, Rd, invR);
@@ -449,7 +471,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       } else {
 #pragma unroll 16
         for (int i = 0; i < 64; ++i) {
-          const uint32_t x = wload<V32>(rs, vo, i * rowb, hw_);
+          const uint32_t x = bload(rs, vo, i * rowb);
           sv += bit_mask(mm, i) & (uint32_t)qdev_d((double)x, mu);
         }
       }
@@ -458,13 +480,14 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     } else {   // fp64 sums (exact: every term < 2^31 under the |x - mu| < 2^25 bound checked here)
       double svd = 0.0;
       if constexpr (BATCH) load_lo(rs, after(vo, mu), rowb, xr);
+      const uint32_t mui = (uint32_t)(int32_t)mu;   // (an int32: the mean of int32 values)
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
-        const double xi = xv(BATCH ? xr[i] : wload<V32>(rs, vo, i * rowb, hw_));
+        const uint32_t xw = BATCH ? xr[i] : bload(rs, vo, i * rowb);
         const bool mk = bit_mask(mm, i) != 0u;
-        if (vc && mk && !(fabs(xi - mu) < 33554432.0)) bad = true;
-        svd += mk ? qdev_d(xi, mu) : 0.0;
+        if (vc && mk && !near25(xw, mui)) bad = true;
+        svd += mk ? qdev_d(xv(xw), mu) : 0.0;
       }
       svd = group_sum<NSEG, P>(svd);
       var = floor_div_d(svd, Rd, invR);
@@ -497,7 +520,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       }
     } else {
 #pragma unroll 8
-      for (int i = 0; i < 64; ++i) zpow(wload<V32>(rs, vo, i * rowb, hw_), bit_mask(mm, i));
+      for (int i = 0; i < 64; ++i) zpow(bload(rs, vo, i * rowb), bit_mask(mm, i));
     }
     // a column with outlier rows (rare; a reliable row far from the mean) is summed again, row by row: the
     // same z and z^2 (exact in fp64), and for the outliers wsad_mul(z^2, z) / wsad_mul(z^2, z^2) in int64
@@ -511,8 +534,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
         uint32_t xg[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          uint32_t hwo;
-          xg[k] = wload<V32>(rs, vo, (g + k) * rowb, hwo);
+          xg[k] = bload(rs, vo, (g + k) * rowb);
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
