@@ -404,3 +404,29 @@ def test_wsad_kernel_unconstrained_stage_order(f, ms):
     comb = _run(v.to(DEV), f, None, constrained=False, ms=ms)
     for k in OUTS:
         assert torch.equal(comb[k], cpu[k]), k
+
+
+@pytest.mark.parametrize("dtype", [torch.int64, torch.int32])
+def test_wsad_kernel_unconstrained_domain_boundaries(dtype):
+    """Values at the column kernel's declared unconstrained domain edges (|x| = 2^30 - 1 / 2^30, deviations
+    2^25 - 1 / 2^25 from the median): whatever the kernel accepts equals the CPU engine bit for bit, and the
+    dispatcher (column kernel + i128 fallback) equals it everywhere."""
+    B, N, D, f = 8, 64, 40, 8
+    v = _signed(B, N, D, f, seed=77, honest_sd=2e5, fail_span=2e6, centre=0.0)
+    big = (1 << 30) - 1
+    v[0] += big - 3_000_000                    # everything near +2^30 (inside)
+    v[1] -= big - 3_000_000                    # near -2^30 (inside)
+    v[2, 3, 5] = 1 << 30                       # one value at 2^30 (outside)
+    v[3, 4, 6] = v[3, :, 6].median().item() + (1 << 25) - 1   # a deviation of 2^25 - 1 (inside)
+    v[4, 4, 6] = v[4, :, 6].median().item() + (1 << 25) + 100_000   # past 2^25 (outside)
+    v[5, 9, 2] = -(1 << 31)                    # int32 minimum
+    vg = v.to(DEV, dtype)
+    cpu = _cpu(v, f, False, MS)
+    only = _run(vg, f, {"SVOC_EXACT_WSAD_ONLY": "1"}, constrained=False, ms=MS)
+    took = only["status"] != -1
+    assert took[0] and took[1] and not took[2] and not took[4], only["status"]
+    for k in OUTS:
+        assert torch.equal(only[k][took], cpu[k][took]), k
+    comb = _run(vg, f, None, constrained=False, ms=MS)
+    for k in OUTS:
+        assert torch.equal(comb[k], cpu[k]), k
