@@ -79,19 +79,21 @@ struct QrCtx {
 template <int L, int I, int P, bool MASKROWS>
 SVOC_DEV float qr_tree(const QrCtx& c, const uint32_t (&wv)[64], f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
   // (no implicit contraction: every instantiation must round identically -- only the explicit fmas below;
-  // left to the backend, y * y + s2 was fused in some instantiations and not in others)
+  // left to the backend, y * y + s2 was fused in some instantiations and not in others.  The fmas are
+  // written out: unfused mul + add took the N <= 64 kernel from 5 to 36 VGPR spills,
+  // profiles/r4_win_bf16_qr_fma_ab.txt)
 #pragma clang fp contract(off)
   if constexpr (L == 0) {
     f32x2 y = bf16x2_to_f32x2(wv[I]) - c.c2;
     f32x2 q = y * y;
-    const float part = q.x + q.y;
+    const float part = __builtin_fmaf(y.x, y.x, q.y);
     if (MASKROWS) {
       const uint32_t rm = lt_mask(I, c.nvl);
       y = fand2(y, rm);
       q = fand2(q, rm);
     }
     s1 += y;
-    s2 += q;
+    s2 = __builtin_elementwise_fma(y, y, s2);
     s3 = __builtin_elementwise_fma(q, y, s3);
     s4 = __builtin_elementwise_fma(q, q, s4);
     return part;
