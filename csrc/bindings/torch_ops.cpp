@@ -323,7 +323,7 @@ void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& 
   p.values = values.data_ptr();
   p.val32 = values.scalar_type() == at::kInt ? 1 : 0;
   p.B = (int)values.size(0); p.N = (int)values.size(1); p.D = (int)values.size(2);
-  TORCH_CHECK(p.N >= 1 && p.N <= 1024, "GPU exact path supports N <= 1024");
+  TORCH_CHECK(p.N >= 1 && p.N <= kExactMaxN, "GPU exact path supports N <= ", kExactMaxN);
   p.active = active_ptr(active, p.B, values.device());
   p.n_failing = (int)n_failing;
   p.constrained = constrained ? 1 : 0;

@@ -30,5 +30,7 @@ enum Status : int {
 // D-sharded exact rounds (split mode 1): bound on |qr partial|, so the int64 all-reduce of up to 32
 // shards' partials cannot wrap; a larger partial reverts the round with OVERFLOW.
 constexpr long long kExactQrPartialMax = 1ll << 58;
+// oracles per instance on the GPU exact path (the i128 kernel's 64 rows per lane); fast mode: 4096 too
+constexpr int kExactMaxN = 4096;
 
 }  // namespace svoc

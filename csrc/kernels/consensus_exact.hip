@@ -15,6 +15,10 @@
 
 namespace svoc {
 
+// loops over a lane's rows: unrolled (arrays in VGPRs) up to 16 rows per lane (N <= 1024); the 32 / 64
+// rows-per-lane instantiations for N <= 4096 keep them in private memory and loop
+#define SVOC_UNROLL_RPL _Pragma("unroll (RPL <= 16 ? RPL : 1)")
+
 __device__ __forceinline__ int64_t shfl64(int64_t v, int src) {
   const int lo = __shfl((int)(uint32_t)v, src), hi = __shfl((int)(uint32_t)(v >> 32), src);
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
@@ -47,18 +51,20 @@ struct Grp {
     for (int o = GS / 2; o >= 1; o >>= 1) v |= __shfl_xor(v, o);
     return v;
   }
-  // checked i128 sum over the group.  The contract adds in row order and reverts on any i128
-  // overflow of a partial sum; when every term is below 2^118 in magnitude no partial sum of <= 256
-  // terms can overflow in ANY order, so a butterfly gives the identical integer.  Otherwise the sum
-  // runs sequentially in lane order, as the CPU engine, for exact overflow detection.
-  __device__ i128 sum(i128 v, int& st) const {
-    const i128 lim = (i128)1 << 118;
-    if (all(v < lim && v > -lim)) {
+  // s + the group's values in lane (= row) order, checked as the contract's running sum: it adds in row
+  // order and reverts on any i128 overflow of a partial sum.  With |s| < 2^126 and every term below
+  // 2^120 in magnitude no partial sum of the <= 64 terms can overflow in ANY order, so a butterfly gives
+  // the identical integer; otherwise the terms are added one by one onto s, as the CPU engine does.
+  // (Summing each group from 0 and adding the group total to s would miss an overflow of a partial
+  // sum inside a group once s is large -- possible with several rows per lane.)
+  __device__ i128 accum(i128 s, i128 v, int& st) const {
+    const i128 lim = (i128)1 << 120, slim = (i128)1 << 126;
+    if (s < slim && s > -slim && all(v < lim && v > -lim)) {
 #pragma unroll
       for (int o = GS / 2; o >= 1; o >>= 1) v += shfl128(v, lane ^ o);
-      return v;
+      return s + v;
     }
-    i128 acc = 0;
+    i128 acc = s;
     for (int l = 0; l < GS; ++l) acc = add(acc, shfl128(v, base + l), st);
     return acc;
   }
@@ -83,7 +89,7 @@ struct ColScratch {
 template <int RPL, int GS>
 __device__ void middle_values(const Rows<RPL>& r, const Grp<GS>& g, int n_rows, int mid, ColScratch<RPL * GS>& cs,
                               i128& a, i128& b) {
-#pragma unroll
+SVOC_UNROLL_RPL
   for (int j = 0; j < RPL; ++j) {
     const int row = j * GS + g.gl;
     if (row < n_rows) {
@@ -92,7 +98,7 @@ __device__ void middle_values(const Rows<RPL>& r, const Grp<GS>& g, int n_rows, 
     }
   }
   __syncthreads();
-#pragma unroll
+SVOC_UNROLL_RPL
   for (int j = 0; j < RPL; ++j) {
     const int me = j * GS + g.gl;
     if (me < n_rows && r.on[j]) {
@@ -152,7 +158,7 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
     // failed has already set the (all-reduced) status
     if (p.status[b] != ST_OK) return;
     for (int d = gl; d < D; d += GS) c1[d] = p.c1[(int64_t)b * D + d];
-#pragma unroll
+SVOC_UNROLL_RPL
     for (int j = 0; j < RPL; ++j) {
       const int row = j * GS + gl;
       qr[j] = row < N ? (i128)p.qr[(int64_t)b * N + row] : 0;
@@ -161,7 +167,7 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
   } else {
     // ---- pass 1: c1 per column
     for (int d = 0; d < D && st == ST_OK; ++d) {
-#pragma unroll
+SVOC_UNROLL_RPL
       for (int j = 0; j < RPL; ++j) {
         const int row = j * GS + gl;
         rows.on[j] = row < N;
@@ -174,7 +180,7 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
     if (st != ST_OK) { if (gl == 0) p.status[b] = st; return; }
     // quadratic risk per row (lane-local), then the checked mean
     int lst = ST_OK;
-#pragma unroll
+SVOC_UNROLL_RPL
     for (int j = 0; j < RPL; ++j) {
       const int row = j * GS + gl;
       i128 acc = 0;
@@ -186,12 +192,12 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
     if (g.any_or(lst != ST_OK)) st = ST_OVERFLOW;
     if (p.mode == 1) {   // D-sharded first half: c1 and the qr partials out, nothing else
       bool big = false;
-#pragma unroll
+SVOC_UNROLL_RPL
       for (int j = 0; j < RPL; ++j) big = big || qr[j] >= (i128)kExactQrPartialMax || qr[j] <= -(i128)kExactQrPartialMax;
       if (g.any_or(big)) st = ST_OVERFLOW;
       if (st == ST_OK) {
         for (int d = gl; d < D; d += GS) p.c1[(int64_t)b * D + d] = c1[d];
-#pragma unroll
+SVOC_UNROLL_RPL
         for (int j = 0; j < RPL; ++j) {
           const int row = j * GS + gl;
           if (row < N) p.qr[(int64_t)b * N + row] = (int64_t)qr[j];
@@ -202,8 +208,8 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
     }
   }
   i128 sum_qr = 0;
-#pragma unroll
-  for (int j = 0; j < RPL; ++j) sum_qr = add(sum_qr, g.sum(qr[j], st), st);
+SVOC_UNROLL_RPL
+  for (int j = 0; j < RPL; ++j) sum_qr = g.accum(sum_qr, qr[j], st);
   const i128 mean_qr = idiv(sum_qr, (i128)N, st);
   // obsolete contracts: no /D (contract_nd.cairo:418); D-sharded rounds: the global D
   const int64_t rdim = p.legacy ? 1 : (p.rel_dim > 0 ? p.rel_dim : D);
@@ -215,11 +221,11 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
   // rank mask: (qr asc, idx desc) (sort.cairo:96-101)
   const int threshold = N - p.n_failing;
   bool rel[RPL];
-#pragma unroll
+SVOC_UNROLL_RPL
   for (int j = 0; j < RPL; ++j) {
     const int me = j * GS + gl;
     int rank = 0;
-#pragma unroll
+SVOC_UNROLL_RPL
     for (int jj = 0; jj < RPL; ++jj)
       for (int l = 0; l < GS; ++l) {
         const int k = jj * GS + l;
@@ -229,11 +235,11 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
     rel[j] = me < N && rank < threshold;
   }
   int R = 0;
-#pragma unroll
+SVOC_UNROLL_RPL
   for (int j = 0; j < RPL; ++j) R += g.count(rel[j]);
   // ---- pass 2: consensus per column over the reliable rows
   for (int d = 0; d < D && st == ST_OK; ++d) {
-#pragma unroll
+SVOC_UNROLL_RPL
     for (int j = 0; j < RPL; ++j) {
       const int row = j * GS + gl;
       rows.on[j] = rel[j];
@@ -244,15 +250,15 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
       c = smooth_median_w<RPL, GS>(rows, g, N, R, cs, st);
     } else {
       i128 s = 0;
-#pragma unroll
-      for (int j = 0; j < RPL; ++j) s = add(s, g.sum(rows.on[j] ? (i128)rows.x[j] : 0, st), st);
+SVOC_UNROLL_RPL
+      for (int j = 0; j < RPL; ++j) s = g.accum(s, rows.on[j] ? (i128)rows.x[j] : 0, st);
       c = idiv(s, (i128)R, st);
     }
     if (gl == 0) cons[d] = (int64_t)c;
   }
   i128 s2 = 0;
-#pragma unroll
-  for (int j = 0; j < RPL; ++j) s2 = add(s2, g.sum(rel[j] ? qr[j] : 0, st), st);
+SVOC_UNROLL_RPL
+  for (int j = 0; j < RPL; ++j) s2 = g.accum(s2, rel[j] ? qr[j] : 0, st);
   const i128 mean_qr2 = idiv(s2, (i128)R, st);
   const i128 rel2 = p.constrained ? constrained_reliability(mean_qr2, rdim, st)
                                   : unconstrained_reliability(wsqrt(mean_qr2, st), p.max_spread, st);
@@ -263,10 +269,10 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
   // ---- moments (math.cairo:208-222, 320-398), stage by stage like the CPU engine
   for (int d = 0; d < D && st == ST_OK && !p.legacy; ++d) {
     i128 s = 0;
-#pragma unroll
+SVOC_UNROLL_RPL
     for (int j = 0; j < RPL; ++j) {
       const int row = j * GS + gl;
-      s = add(s, g.sum(rel[j] ? (i128)X[(int64_t)row * D + d] : 0, st), st);
+      s = g.accum(s, rel[j] ? (i128)X[(int64_t)row * D + d] : 0, st);
     }
     const i128 mu = idiv(s, (i128)R, st);
     if (gl == 0) means[d] = (int64_t)mu;
@@ -275,12 +281,12 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
   for (int d = 0; d < D && st == ST_OK && !p.legacy; ++d) {
     i128 s = 0;
     int l2 = ST_OK;
-#pragma unroll
+SVOC_UNROLL_RPL
     for (int j = 0; j < RPL; ++j) {
       const int row = j * GS + gl;
       const i128 q = rel[j] ? qdev(X[(int64_t)row * D + d], means[d], l2) : 0;
       if (g.any_or(l2 != ST_OK)) fail(st, ST_OVERFLOW);
-      s = add(s, g.sum(q, st), st);
+      s = g.accum(s, q, st);
     }
     const i128 v = idiv(s, (i128)R, st);
     if (gl == 0) vars[d] = (int64_t)v;
@@ -291,7 +297,7 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
       const i128 sd = wsqrt(vars[d], st);
       i128 s = 0;
       int l2 = ST_OK;
-#pragma unroll
+SVOC_UNROLL_RPL
       for (int j = 0; j < RPL; ++j) {
         const int row = j * GS + gl;
         i128 t = 0;
@@ -305,7 +311,7 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
           const int c = __shfl(l2, g.base + l);
           if (c != ST_OK) { fail(st, c); break; }
         }
-        s = add(s, g.sum(t, st), st);
+        s = g.accum(s, t, st);
       }
       const i128 out = pass == 0 ? skew_from_sum(s, R, st) : kurt_from_sum(s, R, st);
       if (gl == 0) (pass == 0 ? sk : ku)[d] = (int64_t)out;
@@ -321,7 +327,7 @@ __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
     p.kurt[o] = ku[d];
     if (p.c1) p.c1[o] = c1[d];
   }
-#pragma unroll
+SVOC_UNROLL_RPL
   for (int j = 0; j < RPL; ++j) {
     const int row = j * GS + gl;
     if (row < N) {
@@ -368,7 +374,9 @@ static int exact_round_i128(const ExactParams* p, hipStream_t stream) {
   if (p->N <= 64) return launch_exact<1, 64>(*p, stream);
   if (p->N <= 256) return launch_exact<4, 64>(*p, stream);
   if (p->N <= 512) return launch_exact<8, 64>(*p, stream);
-  return launch_exact<16, 64>(*p, stream);
+  if (p->N <= 1024) return launch_exact<16, 64>(*p, stream);
+  if (p->N <= 2048) return launch_exact<32, 64>(*p, stream);
+  return launch_exact<64, 64>(*p, stream);
 }
 
 // Exact round: the column-parallel kernel (consensus_wsad.hip) takes every instance it can prove
@@ -377,7 +385,7 @@ static int exact_round_i128(const ExactParams* p, hipStream_t stream) {
 // flagged and run through the i128 kernel right after it on the same stream.
 extern "C" int svoc_exact_round(const ExactParams* p, hipStream_t stream) {
   if (p->B <= 0) return 0;
-  if (p->N < 1 || p->N > 1024 || p->D < 1) return -1;
+  if (p->N < 1 || p->N > kExactMaxN || p->D < 1) return -1;
   if (p->stage && p->fallback) {
     const int rc = svoc_exact_round_wsad(p, stream);
     if (rc != -2) {

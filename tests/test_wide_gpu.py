@@ -1,7 +1,8 @@
 """N > 256 oracles on the GPU: the register-streaming fast kernels (bf16 and fp32 storage) with 8 .. 64
 lanes per column (pair) -- N up to 4096, full cross-lane bitonic sort, sortnet.hpp median_group_wide
--- and the i128 exact kernel with 8 / 16 rows per lane (N <= 1024).  The reference has no oracle cap
-beyond gas (contract.cairo:310-329)."""
+-- and the i128 exact kernel with 8 / 16 rows per lane in registers (N <= 1024) and 32 / 64 rows per
+lane in private memory (N <= 4096).  The reference has no oracle cap beyond gas
+(contract.cairo:310-329)."""
 import pytest
 import torch
 
@@ -36,16 +37,51 @@ def test_fast_wide_n_vs_torch(N, D, f, constrained, storage):
     assert torch.equal(oc["status"], o["status"].cpu())
 
 
-@pytest.mark.parametrize("N,D,f", [(512, 8, 50), (1024, 4, 100)])
-def test_exact_wide_n_matches_cpu(N, D, f):
+@pytest.mark.parametrize("N,D,f,constrained", [
+    (512, 8, 50, True), (1024, 4, 100, True), (1500, 5, 100, True), (2048, 4, 200, True),
+    (2048, 3, 150, False), (3000, 3, 300, True), (4096, 2, 300, True), (4096, 2, 400, False)])
+def test_exact_wide_n_matches_cpu(N, D, f, constrained):
     B = 3
-    x, _ = beta_oracles(B, N, D, f, seed=N, dtype=torch.float64)
+    x, _ = beta_oracles(B, N, D, f, seed=N + D, dtype=torch.float64)
     v = (x[:, :, :D] * 1e6).to(torch.int64).contiguous()
-    g = run_exact(v.to(DEV), f, True)
-    c = run_exact(v, f, True)
+    ms = 0 if constrained else 2_000_000
+    g = run_exact(v.to(DEV), f, constrained, ms)
+    c = run_exact(v, f, constrained, ms)
     for k in ("consensus", "skew", "kurt", "rel", "qr", "reliable", "status", "c1"):
         assert torch.equal(g[k].cpu(), c[k]), k
-    assert (c["status"] == 0).all()
+    assert (c["status"] == 0).all(), c["status"]
+
+
+@pytest.mark.parametrize("N", [2048, 4096])
+def test_exact_wide_n_reverts_match_cpu(N):
+    """Reverting rounds at N > 1024 (too many failing oracles; a zero-variance column; an interval
+    error from a huge max_spread) give the CPU engine's first-error status and no outputs."""
+    B, D = 3, 3
+    x, _ = beta_oracles(B, N, D, 100, seed=7, dtype=torch.float64)
+    v = (x[:, :, :D] * 1e6).to(torch.int64).contiguous()
+    v[1, :, 2] = 500_000   # every row equal in one column: zero variance
+    for f, constrained, ms in ((N + 1, True, 0), (100, True, 0), (100, False, 1)):
+        g = run_exact(v.to(DEV), f, constrained, ms)
+        c = run_exact(v, f, constrained, ms)
+        for k in ("consensus", "skew", "kurt", "rel", "qr", "reliable", "status", "c1"):
+            assert torch.equal(g[k].cpu(), c[k]), (f, constrained, k)
+
+
+def test_engine_exact_n4096_round():
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    cfg = ConsensusConfig(n_oracles=4096, dimension=4, n_failing_oracles=512, constrained=True)
+    e = ConsensusEngine(cfg, batch=2, device=DEV, mode="exact")
+    e.randomize(seed=3)
+    e.run_round()
+    c = ConsensusEngine(cfg, batch=2, device="cpu", mode="exact")
+    c.randomize(seed=3)
+    c.values.copy_(e.values.cpu())   # (the device generators differ: same values on both engines)
+    c.run_round()
+    torch.cuda.synchronize()
+    assert torch.equal(e.status.cpu(), c.status) and (c.status == 0).all()
+    assert torch.equal(e.consensus.cpu(), c.consensus)
+    assert int(e.reliable.sum()) == 2 * (4096 - 512)
 
 
 def test_engine_n1024_streaming_round():
