@@ -339,8 +339,8 @@ void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& 
   p.reliable = reliable.data_ptr<uint8_t>();
   p.status = status.data_ptr<int32_t>();
   at::Tensor work;
-  if ((int64_t)p.D * 6 * 8 > 64 * 1024) {  // wide instances: per-column intermediates in HBM
-    work = at::empty({(int64_t)p.B, 6, (int64_t)p.D}, values.options().dtype(at::kLong));
+  if ((int64_t)p.D * kExactWsCols * 8 > 64 * 1024) {  // wide instances: per-column intermediates in HBM
+    work = at::empty({(int64_t)p.B, kExactWsCols, (int64_t)p.D}, values.options().dtype(at::kLong));
     p.work = work.data_ptr<int64_t>();
   }
   // column-parallel kernel (consensus_wsad.hip), the i128 kernel for the instances it flags;

@@ -32,5 +32,7 @@ enum Status : int {
 constexpr long long kExactQrPartialMax = 1ll << 58;
 // oracles per instance on the GPU exact path (the i128 kernel's 64 rows per lane); fast mode: 4096 too
 constexpr int kExactMaxN = 4096;
+// i128 exact kernel: per-column int64 intermediates (c1, consensus, mean, variance as i128, skew, kurt)
+constexpr int kExactWsCols = 7;
 
 }  // namespace svoc

@@ -17,6 +17,7 @@ namespace svoc {
 
 // loops over a lane's rows: unrolled (arrays in VGPRs) up to 16 rows per lane (N <= 1024); the 32 / 64
 // rows-per-lane instantiations for N <= 4096 keep them in private memory and loop
+#pragma clang diagnostic ignored "-Wcuda-compat"   // (a parenthesised, template-dependent unroll count)
 #define SVOC_UNROLL_RPL _Pragma("unroll (RPL <= 16 ? RPL : 1)")
 
 __device__ __forceinline__ int64_t shfl64(int64_t v, int src) {
@@ -104,6 +105,7 @@ SVOC_UNROLL_RPL
     if (me < n_rows && r.on[j]) {
       const int64_t xm = r.x[j];
       int rank = 0;
+#pragma unroll 8   // (several broadcast LDS reads in flight: one wave per SIMD at large N)
       for (int k = 0; k < n_rows; ++k) {
         const int64_t xk = cs.x[k];
         rank += (cs.on[k] && (xk < xm || (xk == xm && k < me))) ? 1 : 0;
@@ -118,13 +120,59 @@ SVOC_UNROLL_RPL
   __syncthreads();  // the scratch is reused by the next column
 }
 
-template <int RPL, int GS>
+// N > 256 (8+ rows per lane, a whole wave per instance): ranking every row against the column costs
+// N^2 / 64 LDS reads per lane; instead the k-th smallest (0-based) value of the on-rows comes from an
+// 8-bit radix select over the order-preserving unsigned image of the int64 keys (a 256-bin LDS
+// histogram per byte, the bin holding rank k found by a wave prefix scan).  Tied keys are equal
+// values, so the picked value is the stable sort's value at that rank.
+constexpr int kRadixRpl = 8;
+// per-column int64 workspace slots: c1, consensus, mean, variance (two for int64 values), skew, kurt
+__host__ __device__ constexpr int ws_cols(bool v128) { return v128 ? kExactWsCols : kExactWsCols - 1; }
+template <int RPL>
+__device__ int64_t radix_select(const Rows<RPL>& r, int lane, int k, uint32_t* hist) {
+  uint64_t prefix = 0, pmask = 0;
+#pragma unroll 1
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int t = lane; t < 256; t += 64) hist[t] = 0u;
+    __syncthreads();
+SVOC_UNROLL_RPL
+    for (int j = 0; j < RPL; ++j) {
+      const uint64_t u = (uint64_t)r.x[j] ^ 0x8000000000000000ull;
+      if (r.on[j] && (u & pmask) == prefix) atomicAdd(&hist[(uint32_t)(u >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    const uint32_t c = hist[4 * lane] + hist[4 * lane + 1] + hist[4 * lane + 2] + hist[4 * lane + 3];
+    int incl = (int)c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o);
+      if (lane >= o) incl += v;
+    }
+    const int L = __builtin_ctzll(__ballot(incl > k));   // exists: k < the number of on-rows
+    int below = __shfl(incl, L) - __shfl((int)c, L);
+    int bin = 4 * L;
+    for (int hb = (int)hist[bin]; below + hb <= k; hb = (int)hist[bin]) { below += hb; ++bin; }
+    k -= below;
+    prefix |= (uint64_t)bin << shift;
+    pmask |= 0xffull << shift;
+    __syncthreads();   // every lane's reads done before the next byte clears the histogram
+  }
+  return (int64_t)(prefix ^ 0x8000000000000000ull);
+}
+
+template <int RPL, int GS, int NR>
 __device__ i128 smooth_median_w(const Rows<RPL>& r, const Grp<GS>& g, int n_rows, int count,
-                                ColScratch<RPL * GS>& cs, int& st) {
+                                ColScratch<NR>& cs, uint32_t* hist, int& st) {
   if (count == 0) { fail(st, ST_USIZE_UNDERFLOW); return 0; }
   if (count == 1) { fail(st, ST_INDEX_OOB); return 0; }
   i128 a, b;
-  middle_values<RPL, GS>(r, g, n_rows, count / 2, cs, a, b);
+  if constexpr (RPL >= kRadixRpl) {
+    static_assert(GS == 64, "radix select: one wave per instance");
+    a = radix_select<RPL>(r, g.gl, count / 2 - 1, hist);
+    b = radix_select<RPL>(r, g.gl, count / 2, hist);
+  } else {
+    middle_values<RPL, GS>(r, g, n_rows, count / 2, cs, a, b);
+  }
   return idiv_pos64(add(a, b, st), 2, st);
 }
 
@@ -132,22 +180,27 @@ template <int RPL, int GS, class T>
 __global__ __launch_bounds__(64) void consensus_exact_kernel(ExactParams p) {
   constexpr int IPW = 64 / GS;  // instances per wave (= per workgroup)
   extern __shared__ __attribute__((aligned(16))) int64_t lds[];
-  __shared__ ColScratch<RPL * GS> css[IPW];
+  constexpr bool RADIX = RPL >= kRadixRpl;
+  __shared__ ColScratch<RADIX ? 1 : RPL * GS> css[IPW];
+  __shared__ __attribute__((aligned(16))) uint32_t hist[RADIX ? 256 : 1];
   const Grp<GS> g;
   const int gi = threadIdx.x / GS;
   const int b = blockIdx.x * IPW + gi;
   if (b >= p.B || (p.active && !p.active[b])) return;
   const int gl = g.gl;
-  ColScratch<RPL * GS>& cs = css[gi];
+  auto& cs = css[gi];
   const int N = p.N, D = p.D;
-  // per-column intermediates: LDS, or a [B, 6, D] global workspace when 6*D int64 exceed the LDS
-  int64_t* const ws = p.work ? p.work + (int64_t)b * 6 * D : lds + (int64_t)gi * 6 * D;
+  // per-column intermediates: LDS, or a [B, kExactWsCols, D] global workspace when they exceed the LDS
+  // (int64 values: the variance can pass 2^63 and takes two slots; int32 values: one)
+  constexpr bool V128 = sizeof(T) == 8;
+  constexpr int WSC = ws_cols(V128);
+  int64_t* const ws = p.work ? p.work + (int64_t)b * kExactWsCols * D : lds + (int64_t)gi * WSC * D;
   int64_t* c1 = ws;
   int64_t* cons = ws + D;
   int64_t* means = ws + 2 * D;
-  int64_t* vars = ws + 3 * D;
-  int64_t* sk = ws + 4 * D;
-  int64_t* ku = ws + 5 * D;
+  int64_t* vars = ws + 3 * D;   // V128: (lo, hi) per column
+  int64_t* sk = ws + (WSC - 2) * D;
+  int64_t* ku = ws + (WSC - 1) * D;
   const T* X = (const T*)p.values + (int64_t)b * N * D;
   int st = ST_OK;  // group-uniform by construction (every lane runs the same checked reductions)
 
@@ -173,7 +226,7 @@ SVOC_UNROLL_RPL
         rows.on[j] = row < N;
         rows.x[j] = row < N ? X[(int64_t)row * D + d] : 0;
       }
-      const i128 c = smooth_median_w<RPL, GS>(rows, g, N, N, cs, st);
+      const i128 c = smooth_median_w<RPL, GS>(rows, g, N, N, cs, hist, st);
       if (gl == 0) c1[d] = (int64_t)c;
     }
     __syncthreads();
@@ -247,7 +300,7 @@ SVOC_UNROLL_RPL
     }
     i128 c;
     if (p.constrained) {
-      c = smooth_median_w<RPL, GS>(rows, g, N, R, cs, st);
+      c = smooth_median_w<RPL, GS>(rows, g, N, R, cs, hist, st);
     } else {
       i128 s = 0;
 SVOC_UNROLL_RPL
@@ -289,12 +342,20 @@ SVOC_UNROLL_RPL
       s = g.accum(s, q, st);
     }
     const i128 v = idiv(s, (i128)R, st);
-    if (gl == 0) vars[d] = (int64_t)v;
+    if (gl == 0) {
+      if constexpr (V128) {
+        vars[2 * d] = (int64_t)(uint64_t)(u128)v;
+        vars[2 * d + 1] = (int64_t)(v >> 64);
+      } else {
+        vars[d] = (int64_t)v;
+      }
+    }
   }
   __syncthreads();
   for (int pass = 0; pass < 2 && !p.legacy; ++pass) {  // 0: skewness for all d, 1: kurtosis for all d
     for (int d = 0; d < D && st == ST_OK; ++d) {
-      const i128 sd = wsqrt(vars[d], st);
+      const i128 var = V128 ? (i128)(((u128)(uint64_t)vars[2 * d + 1] << 64) | (uint64_t)vars[2 * d]) : (i128)vars[d];
+      const i128 sd = wsqrt(var, st);
       i128 s = 0;
       int l2 = ST_OK;
 SVOC_UNROLL_RPL
@@ -345,7 +406,7 @@ SVOC_UNROLL_RPL
 template <int RPL, int GS>
 static int launch_exact(const ExactParams& p, hipStream_t stream) {
   constexpr int IPW = 64 / GS;
-  const size_t lds = p.work ? 0 : (size_t)IPW * p.D * 6 * sizeof(int64_t);
+  const size_t lds = p.work ? 0 : (size_t)IPW * p.D * ws_cols(!p.val32) * sizeof(int64_t);
   if (lds > 64 * 1024) return -2;  // the binding passes a global workspace for wide instances
   auto k = p.val32 ? consensus_exact_kernel<RPL, GS, int32_t> : consensus_exact_kernel<RPL, GS, int64_t>;
   hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -365,7 +426,7 @@ extern "C" int svoc_exact_round_wsad(const ExactParams* p, hipStream_t stream);
 // the deployed 7 x 6 config runs 8 per wave), else a full wave with 1 or 4 rows per lane.  Wide
 // instances (6*D int64 > LDS budget) use the HBM workspace and a full wave.
 static int exact_round_i128(const ExactParams* p, hipStream_t stream) {
-  const size_t per_inst = (size_t)p->D * 6 * sizeof(int64_t);
+  const size_t per_inst = (size_t)p->D * ws_cols(!p->val32) * sizeof(int64_t);
   if (!p->work) {
     if (p->N <= 8 && 8 * per_inst <= 64 * 1024) return launch_exact<1, 8>(*p, stream);
     if (p->N <= 16 && 4 * per_inst <= 64 * 1024) return launch_exact<1, 16>(*p, stream);

@@ -52,6 +52,35 @@ def test_exact_wide_n_matches_cpu(N, D, f, constrained):
     assert (c["status"] == 0).all(), c["status"]
 
 
+@pytest.mark.parametrize("N,RPL", [(300, 8), (1000, 16), (2000, 32), (4000, 64)])
+def test_exact_wide_n_ties_and_signs_match_cpu(N, RPL):
+    """The radix-select medians (8+ rows per lane) on tie-heavy columns (21 distinct values), negative
+    keys (unconstrained) and one column of int64 extremes, against the CPU engine."""
+    B, D = 2, 4
+    x, _ = beta_oracles(B, N, D, N // 8, seed=N, dtype=torch.float64)
+    v = (((x[:, :, :D] - 0.5) * 20).round() * 100_000).to(torch.int64).contiguous()
+    v[0, :, 3] = torch.randint(-(1 << 62), 1 << 62, (N,), generator=torch.Generator().manual_seed(N))
+    for constrained, ms in ((False, 3_000_000), (True, 0)):
+        g = run_exact(v.to(DEV), N // 8, constrained, ms)
+        c = run_exact(v, N // 8, constrained, ms)
+        for k in ("consensus", "skew", "kurt", "rel", "qr", "reliable", "status", "c1"):
+            assert torch.equal(g[k].cpu(), c[k]), (constrained, k)
+
+
+@pytest.mark.parametrize("N", [7, 50, 200])
+def test_exact_int64_extremes_variance_match_cpu(N):
+    """Unconstrained int64 values near +-2^62: the column variance passes 2^63 (the i128 kernel keeps it
+    as i128), skewness / kurtosis against the CPU engine."""
+    B, D = 2, 3
+    g0 = torch.Generator().manual_seed(N)
+    v = torch.randint(-(1 << 62), 1 << 62, (B, N, D), generator=g0)
+    v[1, :, 0] = torch.randint(-1000, 1000, (N,), generator=g0)
+    g = run_exact(v.to(DEV), 1, False, 1 << 62)
+    c = run_exact(v, 1, False, 1 << 62)
+    for k in ("consensus", "skew", "kurt", "rel", "qr", "reliable", "status", "c1"):
+        assert torch.equal(g[k].cpu(), c[k]), k
+
+
 @pytest.mark.parametrize("N", [2048, 4096])
 def test_exact_wide_n_reverts_match_cpu(N):
     """Reverting rounds at N > 1024 (too many failing oracles; a zero-variance column; an interval

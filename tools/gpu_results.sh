@@ -37,6 +37,7 @@ run wide512 300 --config-file configs/wide512.yaml --steps 10 --warmup 2 &&
 run wide512_fp32 300 --config-file configs/wide512.yaml --storage fp32 --steps 10 --warmup 2 &&
 run wide2048 300 --config-file configs/wide2048.yaml --steps 5 --warmup 1 &&
 run wide2048_fp32 300 --config-file configs/wide2048.yaml --storage fp32 --steps 5 --warmup 1 &&
+run wide4096_exact 300 --config-file configs/wide4096_exact.yaml --steps 3 --warmup 1 &&
 run c1 300 --config c1 --steps 50 --warmup 3 || exit 1
 for spec in "c3:--storage fp32" "c2:--storage bf16" "c4:"; do   # one storage per trace (no alt run)
   cfg=${spec%%:*}; extra=${spec#*:}

@@ -46,6 +46,7 @@ ROWS = [
     ("wide512_fp32", "512 × 2048, fast mode over fp32 storage", "—"),
     ("wide2048", "2048 oracles × 512 dims (N > 1024)", "—"),
     ("wide2048_fp32", "2048 × 512, fast mode over fp32 storage", "—"),
+    ("wide4096_exact", "4096 oracles × 64 dims, exact wsad rounds (N > 1024), 1024 instances", "—"),
 ]
 
 
