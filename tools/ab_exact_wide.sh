@@ -1,3 +1,5 @@
+# A/B of two builds of svoc/_C.so for the i128 exact kernel (build them into ab/ first, as for ab_so.sh):
+#   bash tools/ab_exact_wide.sh   -> old/new rounds/s for configs/wide4096_exact.yaml and c5 exact, then the exact GPU tests
 set -u
 for rep in 1 2; do for v in old new; do
   cp ab/_C_$v.so svoc/_C.so
