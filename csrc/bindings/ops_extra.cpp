@@ -4,6 +4,8 @@
 #include <torch/library.h>
 
 #include <cmath>
+#include <initializer_list>
+#include <utility>
 #include <cstring>
 
 #include "svoc/launch.hpp"
@@ -12,6 +14,14 @@
 
 namespace svoc {
 namespace {
+
+// every tensor a kernel dereferences must live on the state's device (a CPU index tensor handed to a GPU
+// kernel would be read through a host pointer)
+void same_device(const at::Tensor& ref, std::initializer_list<std::pair<const at::Tensor*, const char*>> ts) {
+  for (const auto& t : ts)
+    TORCH_CHECK(t.first->device() == ref.device(), t.second, " must be on ", ref.device(), " (got ",
+                t.first->device(), ")");
+}
 
 int dtype_code(at::ScalarType t) {
   if (t == at::kBFloat16) return 0;
@@ -40,6 +50,8 @@ UpdateParams make_update_params(at::Tensor& values, at::Tensor& enabled, at::Ten
               "n_active: int32 [B]");
   TORCH_CHECK(touched.scalar_type() == at::kByte && touched.numel() == B, "touched: uint8 [B]");
   TORCH_CHECK(upd_status.scalar_type() == at::kInt && upd_status.numel() == U, "upd_status: int32 [U]");
+  same_device(values, {{&enabled, "enabled"}, {&n_active, "n_active"}, {&touched, "touched"}, {&inst, "inst"},
+                       {&oracle, "oracle"}, {&upd, "upd"}, {&upd_status, "upd_status"}});
   UpdateParams p{};
   p.values = values.data_ptr();
   p.enabled = enabled.data_ptr<uint8_t>();
@@ -84,6 +96,7 @@ void set_saved(UpdateParams& p, const c10::optional<at::Tensor>& saved, const c1
               "saved: contiguous [U, D] in the values' dtype");
   TORCH_CHECK(saved_en->scalar_type() == at::kByte && saved_en->is_contiguous() && saved_en->numel() == upd.size(0),
               "saved_en: uint8 [U]");
+  same_device(upd, {{&*saved, "saved"}, {&*saved_en, "saved_en"}});
   p.saved = saved->data_ptr();
   p.saved_en = saved_en->data_ptr<uint8_t>();
 }
@@ -166,6 +179,9 @@ RestoreParams make_restore_params(at::Tensor& values, at::Tensor& enabled, at::T
   TORCH_CHECK(active.scalar_type() == at::kByte && active.numel() == B && active.is_contiguous(), "active: uint8 [B]");
   TORCH_CHECK(enabled.scalar_type() == at::kByte && enabled.numel() == B * N && n_active.scalar_type() == at::kInt &&
                   n_active.numel() == B, "enabled uint8 [B, N], n_active int32 [B]");
+  same_device(values, {{&enabled, "enabled"}, {&n_active, "n_active"}, {&inst, "inst"}, {&oracle, "oracle"},
+                       {&upd_status, "upd_status"}, {&saved, "saved"}, {&saved_en, "saved_en"}, {&status, "status"},
+                       {&active, "active"}});
   RestoreParams p{};
   p.values = values.data_ptr();
   p.enabled = enabled.data_ptr<uint8_t>();
@@ -227,6 +243,7 @@ void commit_updates_hip(const at::Tensor& rows, const at::Tensor& oracle, const 
   TORCH_CHECK(upd_status.scalar_type() == at::kInt && upd_status.numel() == n, "upd_status: int32 [n]");
   TORCH_CHECK(upd_per_inst > 0 && n <= values.size(0) * upd_per_inst, "upd_per_inst: rows b * U .. b * U + U - 1 "
               "belong to instance b");
+  same_device(values, {{&rows, "rows"}, {&oracle, "oracle"}, {&upd_status, "upd_status"}});
   auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
   const int rc = svoc_commit_updates(rows.data_ptr(), oracle.data_ptr<int64_t>(), upd_status.data_ptr<int32_t>(),
                                      values.data_ptr(), values.stride(0), (int)values.size(1), (int)rows.size(1),

@@ -204,6 +204,10 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
                 "stats: int32 [>= 1] on the values' device ([0] += pruned-network fallbacks)");
     p.net_fallbacks = (unsigned int*)stats->data_ptr();
   }
+  for (const c10::optional<at::Tensor>* t : {&upd_rows, &upd_oracle, &upd_status, &rst_saved, &rst_saved_en,
+                                              &rst_enabled, &rst_n_active})
+    TORCH_CHECK(!t->has_value() || !(*t)->defined() || (*t)->device() == values.device(),
+                "fast_round: every update / rollback tensor must be on the values' device");
   if (upd_rows.has_value() && upd_rows->defined()) {
     TORCH_CHECK(f32 && mode == 0 && constrained, "fused streaming: fp32 storage, whole constrained rounds");
     TORCH_CHECK(upd_per_inst > 0 && upd_oracle.has_value() && upd_status.has_value(), "fused streaming: "
@@ -252,7 +256,39 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
     p.rst_U = (int)upd_per_inst;
     const int rc = f32 ? svoc_fast_round_f32(&p, stream) : svoc_fast_round_bf16(&p, stream);
     TORCH_CHECK(rc == 0 || rc == -3, f32 ? "svoc_fast_round_f32" : "svoc_fast_round_bf16", " launch failed: ", rc);
-    TORCH_CHECK(rc == 0, "in-kernel rollback does not apply to this round (use restore_updates)");
+    if (rc == -3) {
+      // the kernel that runs this round cannot roll back (the dispatcher returns -3 before any launch): the
+      // plain round, then the restore kernel over the same saved batch -- the updates are already stored, so
+      // the round must run and the reverted instances must be rolled back here, not left to the caller
+      p.rst_saved = nullptr;
+      p.rst_saved_en = nullptr;
+      p.rst_oracle = nullptr;
+      p.rst_status = nullptr;
+      p.rst_enabled = nullptr;
+      p.rst_n_active = nullptr;
+      p.rst_U = 0;
+      const int rc2 = f32 ? svoc_fast_round_f32(&p, stream) : svoc_fast_round_bf16(&p, stream);
+      TORCH_CHECK(rc2 == 0, f32 ? "svoc_fast_round_f32" : "svoc_fast_round_bf16", " launch failed: ", rc2);
+      TORCH_CHECK(active.has_value() && active->defined(), "rollback fallback: needs the round's active mask");
+      // instance-grouped batch: update u belongs to instance u / U
+      at::Tensor inst = at::arange(n, upd_oracle->options()).div(upd_per_inst, "floor");
+      RestoreParams r{};
+      r.values = values.data_ptr();
+      r.enabled = rst_enabled->data_ptr<uint8_t>();
+      r.n_active = rst_n_active->data_ptr<int32_t>();
+      r.inst = inst.data_ptr<int64_t>();
+      r.oracle = upd_oracle->data_ptr<int64_t>();
+      r.upd_status = upd_status->data_ptr<int32_t>();
+      r.saved = rst_saved->data_ptr();
+      r.saved_en = rst_saved_en->data_ptr<uint8_t>();
+      r.status = status.data_ptr<int32_t>();
+      r.active = active->data_ptr<uint8_t>();
+      r.inst_stride = values.stride(0);
+      r.B = (int)B; r.N = (int)N; r.D = (int)D; r.ld = (int)ld; r.U = (int)n;
+      r.elem_bytes = (int)values.element_size();
+      const int rc3 = svoc_restore_updates(&r, stream);
+      TORCH_CHECK(rc3 == 0, "svoc_restore_updates failed: ", rc3);
+    }
     return;
   }
   const int rc = f32 ? svoc_fast_round_f32(&p, stream) : svoc_fast_round_bf16(&p, stream);

@@ -60,6 +60,39 @@ SVOC_HD double wdiv_d(double a, double b, double inv) {
   return trunc_div_d(fma(a, kW, floor(b * 0.5)), b, inv);
 }
 
+// ---- Half-offset forms (no remainder test) -------------------------------------------------------
+// For an integer t and an integer divisor d >= 1, (t + 1/2) / d lies at least 1 / (2d) away from every
+// integer, and floor((t + 1/2) / d) = floor(t / d).  A product with a reciprocal correctly rounded to
+// nearest (the fp64 1e-6 is 0.41 ulp off; 1.0 / d is IEEE division) carries at most 2^-52 relative error
+// in total, which moves (t + 1/2) / d by less than 1 / (2d) while |t| < 2^51 (for d = 1e6: while the
+// quotient is below 2.25e9) -- so the floor (trunc, for negative t - 1/2) is the exact quotient with no
+// remainder correction: 3-4 fp64 instructions per wsad operation instead of 8-10.  The half is folded
+// into the fma's addend (exact: every fma result below is a half-integer below 2^52).
+constexpr double kInv6 = 1e-6;   // nearest double to 10^-6 (relative error 0.41 * 2^-53)
+
+// quadratic_deviation(a, b) = floor((d^2 + 500000) / 1e6) for d = a - b, |d| < 4.7e7 (math.cairo:170-173)
+SVOC_HD double qdev_h(double d) { return floor(fma(d, d, 500000.5) * kInv6); }
+// the same as an unsigned word (v_cvt_u32_f64 truncates, which is the floor of a positive value)
+SVOC_HD uint32_t qdev_u(double d) { return (uint32_t)(fma(d, d, 500000.5) * kInv6); }
+
+// wsad_mul(a, b) = trunc((a b + 500000) / 1e6) (signed_decimal.cairo:110-112) for integral a, b with
+// |a b| < 2.25e15, given neg = (a b < 0): the half goes away from zero.  (a b < 0 but a b + 500000 >= 0:
+// both offsets give 0.)
+SVOC_HD double wmul_h(double a, double b, bool neg) {
+  return trunc(fma(a, b, neg ? 499999.5 : 500000.5) * kInv6);
+}
+// wsad_mul(a, b) for a b >= 0 (a square, a product of two non-negative values)
+SVOC_HD double wmul_pos_h(double a, double b) { return floor(fma(a, b, 500000.5) * kInv6); }
+
+// I128Div(A, b) = trunc(A / b) for integral |A| < 2^51, integral b >= 1, given ib = 1.0 / b (IEEE) and
+// hb = 0.5 * ib: trunc((A + sign(A) / 2) / b).  wsad_div(a, b) is this with A = a * 1e6 + floor(b / 2)
+// (signed_decimal.cairo:114-116).
+SVOC_HD double tdiv_h(double A, double ib, double hb) { return trunc(fma(A, ib, copysign(hb, A))); }
+SVOC_HD double wdiv_h(double a, double b) {
+  const double ib = 1.0 / b;
+  return tdiv_h(fma(a, kW, floor(b * 0.5)), ib, 0.5 * ib);
+}
+
 // sqrt (math.cairo:271-292) for integral 0 <= v < 2^31: the same Newton steps and stop rule
 // (g == previous g, at most 50 iterations).  Returns false where the contract reverts: a zero
 // divisor (sqrt(1) -- g = 0 after the first halving).

@@ -233,7 +233,23 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
   // every update's transaction status once the round's outcome is known (contract.cairo:588-603)
   auto upd_out = [&](int st) __attribute__((always_inline)) {
     if (fused)
-      for (int t = tid; t < U; t += NT) p.upd_status[(int64_t)b * U + t] = bad_slot(t) ? ST_INTERVAL_INPUT : st;
+      for (int t = tid; t < U; t += NT) {
+        int s = bad_slot(t) ? ST_INTERVAL_INPUT : st;
+        const int64_t o = p.upd_oracle[(int64_t)b * U + t];
+        if (o < 0 || o >= N) {
+          // never mapped to a row (so never interval-checked by the round): the contract's order, the
+          // prediction's interval check, then the caller's oracle lookup (contract.cairo:588-596)
+          s = ST_NOT_ORACLE;
+          for (int d = 0; d < D; ++d) {
+            const float v = urows[(int64_t)t * D + d];
+            if (!(v >= 0.f && v <= 1.f)) {
+              s = ST_INTERVAL_INPUT;
+              break;
+            }
+          }
+        }
+        p.upd_status[(int64_t)b * U + t] = s;
+      }
   };
   const int lo1 = (NPAD - N + 1) >> 1;
   const int nv = N - seg * 64;

@@ -236,14 +236,14 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       for (int i = 0; i < 64; ++i) {
         if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bound the fp64 temporaries in flight
         if (!CONS) badv |= (vc && i < nv && !near25(q[i], c1)) ? 1u : 0u;   // |x - c1| < 2^25
-        q[i] = (vc && i < nv) ? (uint32_t)qdev_d(xv(q[i]), cd) : 0u;
+        q[i] = (vc && i < nv) ? qdev_u(xv(q[i]) - cd) : 0u;
       }
     } else {
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         const uint32_t x = bload(rs, vo, i * rowb);   // (low word; int64 high words are checked below)
         if (!CONS) badv |= (vc && i < nv && !near25(x, c1)) ? 1u : 0u;
-        q[i] = (vc && i < nv) ? (uint32_t)qdev_d(xv(x), cd) : 0u;
+        q[i] = (vc && i < nv) ? qdev_u(xv(x) - cd) : 0u;
       }
     }
     if constexpr (CONS) qtree_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
@@ -466,13 +466,13 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
           if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
-          sv += bit_mask(mm, i) & (uint32_t)qdev_d((double)xr[i], mu);
+          sv += bit_mask(mm, i) & qdev_u((double)xr[i] - mu);
         }
       } else {
 #pragma unroll 16
         for (int i = 0; i < 64; ++i) {
           const uint32_t x = bload(rs, vo, i * rowb);
-          sv += bit_mask(mm, i) & (uint32_t)qdev_d((double)x, mu);
+          sv += bit_mask(mm, i) & qdev_u((double)x - mu);
         }
       }
       sv = group_sum<NSEG, P>(sv);
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
         const uint32_t xw = BATCH ? xr[i] : bload(rs, vo, i * rowb);
         const bool mk = bit_mask(mm, i) != 0u;
         if (vc && mk && !near25(xw, mui)) bad = true;
-        svd += mk ? qdev_d(xv(xw), mu) : 0.0;
+        svd += mk ? qdev_h(xv(xw) - mu) : 0.0;
       }
       svd = group_sum<NSEG, P>(svd);
       var = floor_div_d(svd, Rd, invR);
@@ -498,18 +498,22 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     double sd = 1.0;
     const bool ok_sd = var >= 2.0 && wsqrt_d(var, sd);
     if (vc && !ok_sd) dz = true;   // sqrt(0) -> wsad_div by 0, sqrt(1) divides by 0: DIV_BY_ZERO
-    const double isd = recip_lo(sd);
-    // z-score powers (math.cairo:320-363), reliable rows only (a masked row has z = 0: all powers 0)
+    // z = wsad_div(x - mu, sd) = I128Div((x - mu) 1e6 + floor(sd / 2), sd): A = x 1e6 + C0 (exact integers
+    // below 2^51), then the half-offset forms of wsad_fast.hpp -- no remainder tests in the row loop
+    const double isd = 1.0 / sd, hisd = 0.5 * isd;
+    const double C0 = fma(-mu, kW, floor(sd * 0.5));
+    const uint32_t mu_u = (uint32_t)(int32_t)mu;
+    // z-score powers (math.cairo:320-363), reliable rows only
     double s3 = 0.0, s4 = 0.0;
     bool outl = false;   // a row with z^2 >= 2^25 (|z| >= 5.79): this column's sums are redone below
-    // z-score powers of one row (a masked row has z = 0: all powers 0)
+    // z-score powers of one row (a masked row reads as mu: z = 0, all powers 0)
     auto zpow = [&](uint32_t x, uint32_t mk) {
-      const double dx = mk ? xv(x) - mu : 0.0;
-      const double z = wdiv_d(dx, sd, isd);
-      const double z2 = wmul_d(z, z);
-      outl = outl || !(z2 < 33554432.0);   // 2^25: keeps every product below wmul_d's 2^50 bound
-      s3 += wmul_d(z2, z);
-      s4 += wmul_d(z2, z2);
+      const uint32_t xm = (x & mk) | (mu_u & ~mk);
+      const double z = tdiv_h(fma(xv(xm), kW, C0), isd, hisd);
+      const double z2 = wmul_pos_h(z, z);
+      outl = outl || !(z2 < 33554432.0);   // 2^25: keeps z^2 z and z^2 z^2 below the forms' 2.25e9 quotients
+      s3 += wmul_h(z2, z, z < 0.0);
+      s4 += wmul_pos_h(z2, z2);
     };
     if constexpr (BATCH) {
       load_lo(rs, after(vo, sd), rowb, xr);
@@ -539,11 +543,12 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const uint32_t mk = bit_mask(mm, g + k);
-          const double z = wdiv_d(mk ? xv(xg[k]) - mu : 0.0, sd, isd);
-          const double z2 = wmul_d(z, z);
+          const uint32_t xm = (xg[k] & mk) | (mu_u & ~mk);
+          const double z = tdiv_h(fma(xv(xm), kW, C0), isd, hisd);
+          const double z2 = wmul_pos_h(z, z);
           if (z2 < 33554432.0) {
-            s3 += wmul_d(z2, z);
-            s4 += wmul_d(z2, z2);
+            s3 += wmul_h(z2, z, z < 0.0);
+            s4 += wmul_pos_h(z2, z2);
           } else {
             const int64_t zi = (int64_t)z, z2i = (int64_t)z2;
             if (z2i > (1ll << 40)) bad = true;   // (impossible for |z| <= sqrt(R - 1); kept as a guard)

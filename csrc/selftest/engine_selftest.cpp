@@ -197,10 +197,65 @@ static void wsad_fast_paths() {
   CHECK(bad == 0);
 }
 
+// The half-offset forms (wsad_fast.hpp: no remainder test) against the i128 routines: random operands
+// over the whole stated ranges, plus dividends whose remainder is 0 or d - 1 at the largest quotients
+// (the two fractional parts closest to an integer, where a product error would show).
+static void wsad_half_paths() {
+  std::mt19937_64 rng(777);
+  auto uni = [&](int64_t lo, int64_t hi) { return lo + (int64_t)(rng() % (uint64_t)(hi - lo + 1)); };
+  int bad = 0;
+  for (int it = 0; it < 4000000 && bad < 10; ++it) {
+    int st = ST_OK;
+    // quadratic deviation: |d| up to 4.7e7 (quotients to 2.2e9)
+    const int64_t d = it & 1 ? uni(-1000000, 1000000) : uni(-47000000, 47000000);
+    const int64_t qd = (int64_t)qdev(d, 0, st);
+    if ((int64_t)qdev_h((double)d) != qd) ++bad;
+    if (qd < (1ll << 32) && (int64_t)qdev_u((double)d) != qd) ++bad;
+    // z^2, z^2 * z, z^2 * z^2 of the z-power loop (z2 < 2^25, |z| < 5.8e6)
+    const int64_t z = uni(-5800000, 5800000), z2 = uni(0, (1 << 25) - 1);
+    if ((int64_t)wmul_pos_h((double)z, (double)z) != (int64_t)wmul(z, z, st)) ++bad;
+    if ((int64_t)wmul_h((double)z2, (double)z, z < 0) != (int64_t)wmul(z2, z, st)) ++bad;
+    if ((int64_t)wmul_pos_h((double)z2, (double)z2) != (int64_t)wmul(z2, z2, st)) ++bad;
+    // small products of either sign (a b + 500000 changes sign)
+    const int64_t a = uni(-2000, 2000), b = uni(-2000, 2000);
+    if ((int64_t)wmul_h((double)a, (double)b, a * b < 0) != (int64_t)wmul(a, b, st)) ++bad;
+    // wsad_div by a standard deviation, |a| < 2^26, b up to 2^31
+    const int64_t num = it & 2 ? uni(-1000000, 1000000) : uni(-(1 << 26), 1 << 26);
+    const int64_t sd = it & 4 ? uni(1, 2000000) : uni(1, (1ll << 31) - 1);
+    if ((int64_t)wdiv_h((double)num, (double)sd) != (int64_t)wdiv(num, sd, st)) ++bad;
+    CHECK(st == ST_OK);
+  }
+  CHECK(bad == 0);
+  // remainders 0 and d - 1 (and their negatives) at the largest quotients each form takes
+  for (int64_t dv : {(int64_t)1, (int64_t)2, (int64_t)3, (int64_t)1414, (int64_t)999983, (int64_t)1000000,
+                     (int64_t)46341000, (int64_t)((1ll << 31) - 1)}) {
+    const double ib = 1.0 / (double)dv;
+    for (int64_t q : {(int64_t)0, (int64_t)1, (int64_t)777, (int64_t)((1ll << 51) / dv - 2), (int64_t)((1ll << 51) / dv / 3)}) {
+      for (int64_t r : {(int64_t)0, (int64_t)1, dv - 1}) {
+        const int64_t t = q * dv + r;
+        if (t >= (1ll << 51) || t < 0) continue;
+        int st = ST_OK;
+        CHECK((int64_t)tdiv_h((double)t, ib, 0.5 * ib) == (int64_t)idiv(t, dv, st));
+        CHECK((int64_t)tdiv_h(-(double)t, ib, 0.5 * ib) == (int64_t)idiv(-t, dv, st));
+      }
+    }
+  }
+  // wsad_mul quotients next to 2.25e9 with remainders 0 / 999999 (a b + 500000 = q 1e6 + r)
+  for (int64_t q : {(int64_t)2249999999ll, (int64_t)1125899906ll, (int64_t)33554431, (int64_t)1}) {
+    for (int64_t r : {(int64_t)0, (int64_t)1, (int64_t)999999}) {
+      const int64_t t = q * 1000000 + r - 500000;   // = a * b with b = 1
+      int st = ST_OK;
+      CHECK((int64_t)wmul_pos_h((double)t, 1.0) == (int64_t)wmul(t, 1, st));
+      CHECK((int64_t)wmul_h((double)-t, 1.0, true) == (int64_t)wmul(-t, 1, st));
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   const int threads = argc > 1 ? std::atoi(argv[1]) : 8;
   golden_fixture();
   wsad_fast_paths();
+  wsad_half_paths();
   batch_vs_single(threads);
   governance_flow();
   io_roundtrip();

@@ -47,6 +47,71 @@ def _round_up(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
+class _PendingBatches:
+    """Rollback information of the fast engine's update batches that await their round (transactional steps).
+
+    Each ``apply_updates`` call adds its saved rows / ``enabled`` flags ([U, D] + [U]); the next round restores
+    them for the instances it reverts (latest batch first) and gives those updates the round's status.  Many
+    batches before one round are folded into one dense pre-image of the state -- ``values``, ``enabled`` and
+    ``n_active`` as they were before the first pending batch -- so the memory held stays bounded by one state
+    copy (the folded batches keep only their [U] instance ids and status tensors).  A checkpoint written while
+    batches are pending stores that pre-image (svoc.state), so a round after a reload reverts to the same rows.
+    """
+
+    FOLD_AT = 8   # pending batches kept as saved rows before they are folded into the dense pre-image
+
+    def __init__(self, eng: "ConsensusEngine"):
+        self.e = eng
+        self.entries = []      # (inst, oracle, st, saved, saved_en), batch order
+        self.dense = None      # (values, enabled, n_active) before the first folded batch
+        self.folded_st = []    # (inst, st) of the folded batches
+
+    def __bool__(self) -> bool:
+        return bool(self.entries) or self.dense is not None
+
+    def add(self, inst: torch.Tensor, oracle: torch.Tensor, st: torch.Tensor):
+        saved, saved_en, _ = self.e._save_buffer(("pending", len(self.entries)), inst.numel())
+        self.entries.append((inst, oracle, st, saved, saved_en))
+        return saved, saved_en
+
+    def maybe_fold(self) -> None:
+        if len(self.entries) > self.FOLD_AT:
+            self.fold()
+
+    def fold(self) -> None:
+        """Fold the saved rows of every pending batch into the dense pre-image (one state copy)."""
+        e = self.e
+        if self.dense is None:
+            pv, pe, pn = e.values.clone(), e.enabled.clone(), e.n_active.clone()
+            revert_all = torch.full_like(e.status, int(Status.ZERO_VARIANCE))
+            every = torch.ones_like(e._active)
+            for inst, oracle, st, saved, saved_en in reversed(self.entries):
+                e._ops.restore_updates(pv, pe, pn, inst, oracle, st.clone(), saved, saved_en, revert_all, every)
+            self.dense = (pv, pe, pn)
+        self.folded_st += [(inst, st) for inst, _, st, _, _ in self.entries]
+        self.entries = []
+
+    def restore(self, status: torch.Tensor, active: torch.Tensor) -> None:
+        """Roll back the pending batches of the instances whose round ran (``active``) and reverted."""
+        e = self.e
+        e._all_active = False   # (a reverted first commit lowers n_active: the fused path re-checks)
+        if self.dense is None:
+            for inst, oracle, st, saved, saved_en in reversed(self.entries):
+                e._ops.restore_updates(e.values, e.enabled, e.n_active, inst, oracle, st, saved, saved_en,
+                                       status, active)
+        else:
+            rev = (active != 0) & (status != int(Status.OK))
+            pv, pe, pn = self.dense
+            e.values.copy_(torch.where(rev[:, None, None], pv, e.values))
+            e.enabled.copy_(torch.where(rev[:, None], pe, e.enabled))
+            e.n_active.copy_(torch.where(rev, pn, e.n_active))
+            for inst, st in self.folded_st + [(x[0], x[2]) for x in self.entries]:
+                ok = (inst >= 0) & (inst < e.B)
+                ic = inst.clamp(0, e.B - 1)
+                st.copy_(torch.where((st == int(Status.OK)) & ok & rev[ic], status[ic].to(st.dtype), st))
+        self.entries, self.dense, self.folded_st = [], None, []
+
+
 class ConsensusEngine:
     def __init__(self, cfg: ConsensusConfig, batch: int, device="cuda", mode: str = "fast",
                  storage: Optional[str] = None):
@@ -102,7 +167,7 @@ class ConsensusEngine:
         # pruned window network (fp32, N = 256): slab networks that failed the exact check and reran the
         # full network, counted by the kernel (net_stats)
         self._net_fb = torch.zeros(1, dtype=torch.int32, device=dev) if (mode == "fast" and dev.type == "cuda") else None
-        self._pending_restore = []
+        self._pending = _PendingBatches(self)
         self._save_bufs: Dict[tuple, tuple] = {}
         # health counters folded in by every round's epilogue: [rel2 sum (2^-32 units fast / wsad
         # exact), committed, processed, reverted]
@@ -148,6 +213,11 @@ class ConsensusEngine:
             # (streams only: a pending D-shard round's commit writes outputs, not the stored rows, and
             # its pass 2 has already read them -- updates may land before it)
             self._join_streams()
+            if self.transactional and getattr(self, "_dshard_pending", None) is not None:
+                # ... unless the pending round's reverted instances must roll their rows back: its verdict
+                # (one status all-reduce) and the restore come first, then this batch lands on the
+                # restored rows (svoc.parallel.dshard, deferred rounds)
+                self.pipeline_join()
         vals = self._as_storage(torch.as_tensor(vals))
         if vals.dim() != 2 or vals.shape[1] != self.D:
             raise ValueError(f"predictions must be [U, {self.D}]")
@@ -157,10 +227,11 @@ class ConsensusEngine:
         else:
             st = torch.empty(inst.numel(), dtype=torch.int32, device=self.device)
             if self.transactional:
-                saved, saved_en, _ = self._save_buffer(("pending", len(self._pending_restore)), inst.numel())
-                self._pending_restore.append((inst, oracle, st, saved, saved_en))
+                saved, saved_en = self._pending.add(inst, oracle, st)
         self._ops.apply_updates(self.values, self.enabled, self.n_active, self.touched, self._winner,
                                 inst, oracle, vals, self.cfg.constrained, st, bool(unique), saved, saved_en)
+        if save is None and self.transactional:
+            self._pending.maybe_fold()
         return st
 
     def _save_buffer(self, key, U: int):
@@ -183,9 +254,8 @@ class ConsensusEngine:
                                       status, self._active)
 
     def _restore_pending(self, status=None) -> None:
-        if self._pending_restore:
-            self._restore(self._pending_restore, status)
-            self._pending_restore = []
+        if self._pending:
+            self._pending.restore(self.status if status is None else status, self._active)
 
     # ------------------------------------------------------------------ rounds
     def run_round(self, only_touched: bool = True) -> None:
@@ -316,8 +386,13 @@ class ConsensusEngine:
         every other engine method) joins the streams into the current stream before anything else
         touches the state."""
         U = int(updates_per_instance)
+        # the batch goes to kernels that dereference it directly (the fused round, the commit and restore
+        # kernels): indices as int64 and rows in the storage dtype, all on the state's device
+        inst = torch.as_tensor(inst, dtype=torch.int64, device=self.device).reshape(-1).contiguous()
+        oracle = torch.as_tensor(oracle, dtype=torch.int64, device=self.device).reshape(-1).contiguous()
+        vals = self._as_storage(torch.as_tensor(vals))
         # (a lone apply_updates before this step is still awaiting its round: one round must cover both)
-        if self.mode != "fast" or self.device.type != "cuda" or chunks <= 1 or self._pending_restore:
+        if self.mode != "fast" or self.device.type != "cuda" or chunks <= 1 or self._pending:
             self.pipeline_join()
             self.apply_updates(inst, oracle, vals, unique=True)
             self.run_round()

@@ -197,6 +197,49 @@ class SentimentEncoder(nn.Module):
         return torch.sigmoid(self.head(h).float())
 
 
+def config_from_hf(hf_cfg) -> EncoderConfig:
+    """EncoderConfig of a HF ``RobertaConfig`` (e.g. SamLowe/roberta-base-go_emotions's), ``<s>`` pooling."""
+    if getattr(hf_cfg, "hidden_act", "gelu") != "gelu":
+        raise ValueError(f"only erf GELU encoders map onto SentimentEncoder (got {hf_cfg.hidden_act})")
+    if getattr(hf_cfg, "type_vocab_size", 1) != 1:
+        raise ValueError("RoBERTa has one token type")
+    return EncoderConfig(vocab_size=hf_cfg.vocab_size, hidden=hf_cfg.hidden_size, layers=hf_cfg.num_hidden_layers,
+                         heads=hf_cfg.num_attention_heads, ffn=hf_cfg.intermediate_size,
+                         max_positions=hf_cfg.max_position_embeddings, n_labels=hf_cfg.num_labels,
+                         layer_norm_eps=hf_cfg.layer_norm_eps, pad_id=hf_cfg.pad_token_id, pool="cls")
+
+
+@torch.no_grad()
+def load_hf_roberta(model: SentimentEncoder, sd) -> SentimentEncoder:
+    """Copy a HF ``RobertaForSequenceClassification`` state dict into ``model`` (same sizes): separate
+    query / key / value projections -> the fused QKV projection ([q; k; v] rows, the layout
+    attention_qkv reads), the classification head (dense-tanh-out_proj on the <s> state) -> dense / head.
+    With such weights the encoder computes the reference's classifier (client/oracle_scheduler.py:23-40:
+    sigmoid over the 28 go_emotions logits) -- tests/test_sentiment.py pins it against transformers."""
+    p = "roberta."
+    g = lambda k: sd[k]  # noqa: E731
+    model.tok.weight.copy_(g(p + "embeddings.word_embeddings.weight"))
+    model.pos.weight.copy_(g(p + "embeddings.position_embeddings.weight"))
+    model.typ.weight.copy_(g(p + "embeddings.token_type_embeddings.weight"))
+    model.ln.weight.copy_(g(p + "embeddings.LayerNorm.weight"))
+    model.ln.bias.copy_(g(p + "embeddings.LayerNorm.bias"))
+    for i, L in enumerate(model.layers):
+        q = f"{p}encoder.layer.{i}."
+        L.qkv.weight.copy_(torch.cat([g(q + f"attention.self.{n}.weight") for n in ("query", "key", "value")]))
+        L.qkv.bias.copy_(torch.cat([g(q + f"attention.self.{n}.bias") for n in ("query", "key", "value")]))
+        for dst, src in ((L.out, "attention.output.dense"), (L.fc1, "intermediate.dense"), (L.fc2, "output.dense")):
+            dst.weight.copy_(g(q + src + ".weight"))
+            dst.bias.copy_(g(q + src + ".bias"))
+        for dst, src in ((L.ln1, "attention.output.LayerNorm"), (L.ln2, "output.LayerNorm")):
+            dst.weight.copy_(g(q + src + ".weight"))
+            dst.bias.copy_(g(q + src + ".bias"))
+    model.dense.weight.copy_(g("classifier.dense.weight"))
+    model.dense.bias.copy_(g("classifier.dense.bias"))
+    model.head.weight.copy_(g("classifier.out_proj.weight"))
+    model.head.bias.copy_(g("classifier.out_proj.bias"))
+    return model
+
+
 def scores_to_oracle_vectors(scores: torch.Tensor) -> torch.Tensor:
     """prediction_to_vector + normalize (oracle_scheduler.py:20-34): [..., 28] -> [..., 6], sum 1."""
     v = scores[..., ORACLE_LABEL_IDX]

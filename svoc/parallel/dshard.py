@@ -135,16 +135,26 @@ def run_round_sharded(engine, d_global: int, group=None, world: int = 1, defer: 
         N = sh.qr.shape[1]
         sh.qr.copy_(buf[:, :N])
         if pend is not None:     # the previous (deferred) round: every rank's pass-2 verdict, then commit
-            _commit(e, sh, pend[0], buf[:, N:N + world].amax(1).to(e.status.dtype), pend[2], pend[3])
+            pst = buf[:, N:N + world].amax(1).to(e.status.dtype)
+            _commit(e, sh, pend[0], pst, pend[2], pend[3])
+            rows = getattr(e, "_dshard_pending_rows", None)
+            if rows:
+                # (only reached with no batch applied since that round: apply_updates flushes a transactional
+                # engine first, so this round's pass 1 read exactly the rows the restore puts back -- none)
+                rows.restore(pst, pend[0])
+            e._dshard_pending_rows = None
             e._dshard_pending = pend = None
         e.status.copy_(buf[:, N + world:].amax(1).to(e.status.dtype))
     # pass 2 from the global qr on the instances every shard passed, into the shadow outputs
     half(2)
     if defer and world > 1:
         # (active, local pass-2 status, global qr, c1): pass 1 of the next round rewrites the qr / c1 shadows.
-        # A deferred round's verdict arrives after the next round has read the rows, so the transactional
-        # row restore (engine docstring) does not apply here: its update batches stay coalesced as stored.
-        e._pending_restore = []
+        # Transactional fast engines keep the round's update batches (saved rows) until the verdict: the
+        # next apply_updates flushes first (engine.apply_updates -> pipeline_join -> flush_sharded), so a
+        # reverted instance's rows, enabled flags and n_active are restored before any new row lands.
+        if e.mode == "fast":
+            from ..engine import _PendingBatches
+            e._dshard_pending_rows, e._pending = e._pending, _PendingBatches(e)
         sh.p_active.copy_(e._active)
         sh.p_status.copy_(e.status)
         sh.p_qr.copy_(sh.qr)
@@ -173,4 +183,8 @@ def flush_sharded(engine, group=None, world: int = 1) -> None:
         dist.all_reduce(st, op=dist.ReduceOp.MAX, group=group)
     _commit(e, e._dshard_shadow, pend[0], st, pend[2], pend[3])
     e.status.copy_(st)
+    rows = getattr(e, "_dshard_pending_rows", None)
+    if rows:   # every rank rolls back its column slice of the reverted instances' update batches
+        rows.restore(st, pend[0])
+    e._dshard_pending_rows = None
     e._dshard_pending = None

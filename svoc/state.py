@@ -50,7 +50,14 @@ def save(svc, path: str) -> None:
         ("essence_first_pass", e.c1, num),
         ("quadratic_risk", e.qr, num),
         ("status", e.status, ""),
+        ("touched", e.touched, ""),   # instances whose stored updates still await their round
     ]
+    if e.mode == "fast" and e._pending:
+        # update batches awaiting their round (transactional steps): the pre-image their revert restores
+        e._pending.fold()
+        pv, pe, pn = e._pending.dense
+        secs += [("pending_pre_values", pv[:, :, :D].contiguous(), ""), ("pending_pre_enabled", pe, ""),
+                 ("pending_pre_n_active", pn, "")]
     svops.ops().save_state(path, json.dumps(meta), [s[0] for s in secs],
                            [s[1].detach().cpu().contiguous() for s in secs], [s[2] for s in secs])
 
@@ -105,4 +112,10 @@ def load(path: str, device="cpu"):
     e.qr.copy_(t["quadratic_risk"].to(dev, e.qr.dtype))
     e.status.copy_(t["status"].to(dev))
     e.rounds = int(meta.get("rounds", 0))
+    if "touched" in t:
+        e.touched.copy_(t["touched"].to(dev))
+    if "pending_pre_values" in t and e.mode == "fast":
+        pv = e.values.clone()
+        pv[:, :, : e.D].copy_(t["pending_pre_values"].to(dev, e.vdtype))
+        e._pending.dense = (pv, t["pending_pre_enabled"].to(dev).clone(), t["pending_pre_n_active"].to(dev).clone())
     return svc

@@ -9,6 +9,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from svoc import ops as svops
+from svoc.status import Status
 
 pytestmark = pytest.mark.skipif(not svops.available(), reason="svoc/_C.so not built")
 
@@ -234,6 +235,68 @@ def test_dsharding_deferred_commit_one_collective_per_round(mode):
         assert eager["status"].tolist()[1] == 0 and eager["status"].tolist()[3] != 0
         # one collective per round, the packed [B, N + 2 * world] buffer; the flush's status MAX last
         assert s["calls"] == [(B, N + 2 * world), "round"] * 3 + [(B,)], s["calls"]
+
+
+def _ds_defer_txn_worker(rank, world, port, outdir, xs, ups, cfgd):
+    """Transactional fast engines, D-sharded: the same update batches and rounds committed eagerly and
+    deferred.  A deferred round's revert must restore its batch's rows / enabled / n_active before the next
+    batch lands (apply_updates flushes the pending verdict first)."""
+    _init(rank, world, port)
+    from svoc.config import ConsensusConfig
+    from svoc.engine import ConsensusEngine
+    from svoc.parallel import dshard
+    cfg = ConsensusConfig(**cfgd)
+    lo, hi = dshard.shard_bounds(cfg.dimension, rank, world)
+    lcfg = ConsensusConfig(**{**cfgd, "dimension": hi - lo})
+    out = []
+    for defer in (False, True):
+        e = ConsensusEngine(lcfg, xs.shape[0], device="cpu", mode="fast", storage="fp32")
+        e.values[:, :, : hi - lo] = xs[:, :, lo:hi]
+        e.enabled.fill_(1); e.n_active.fill_(cfg.n_oracles); e.touched.fill_(1)
+        dshard.run_round_sharded(e, cfg.dimension, world=world, defer=defer)
+        sts, snaps = [], []
+        for inst, orc, rows in ups:
+            sts.append(e.apply_updates(inst, orc, rows[:, lo:hi].contiguous()))
+            snaps.append({k: getattr(e, k).clone() for k in ("values", "enabled", "n_active")})
+            dshard.run_round_sharded(e, cfg.dimension, world=world, defer=defer)
+        dshard.flush_sharded(e, world=world)
+        out.append(dict(st=[s.clone() for s in sts], snaps=snaps,
+                        **{k: getattr(e, k).clone() for k in ("values", "enabled", "n_active", "status", "consensus",
+                                                             "rel", "reliable", "c1")}))
+    torch.save(dict(out=out, lo=lo, hi=hi), os.path.join(outdir, f"dt{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_dsharding_deferred_rounds_are_transactional():
+    """A deferred D-shard round that reverts (zero variance in ONE shard's column) leaves no trace: its update
+    batch's rows, enabled flags and n_active are restored on every rank before the next batch is stored, and
+    the result equals the eagerly committed rounds bit for bit (statuses of every update included)."""
+    from helpers import beta_oracles
+    B, N, D, f, world = 4, 16, 24, 2, 2
+    x, _ = beta_oracles(B, N, D, f, seed=41)
+    x = x[:, :, :D].contiguous().float()
+    g = torch.Generator().manual_seed(3)
+    # batch 1: instance 1 -> every oracle, column 2 (shard 0) at one value: its round reverts; instance 0: two rows
+    rows1 = torch.rand(N + 2, D, generator=g)
+    rows1[:N, 2] = 0.5
+    ups = [(torch.tensor([1] * N + [0, 0]), torch.cat([torch.arange(N), torch.tensor([3, 9])]), rows1),
+           # batch 2: ordinary rows for instances 1 and 2 (lands on instance 1's restored rows)
+           (torch.tensor([1, 2]), torch.tensor([3, 5]), torch.rand(2, D, generator=g))]
+    cfgd = dict(n_oracles=N, dimension=D, n_failing_oracles=f, constrained=True)
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_ds_defer_txn_worker, args=(world, _free_port(), d, x, ups, cfgd), nprocs=world, join=True)
+        r = [torch.load(os.path.join(d, f"dt{i}.pt"), weights_only=True) for i in range(world)]
+    for s in r:
+        eager, deferred = s["out"]
+        for k in ("values", "enabled", "n_active", "status", "consensus", "rel", "reliable", "c1"):
+            assert torch.equal(eager[k], deferred[k]), k
+        for a, b in zip(eager["st"], deferred["st"]):
+            assert torch.equal(a, b)
+        assert (eager["st"][0][:N] == int(Status.ZERO_VARIANCE)).all() and eager["st"][0][N:].tolist() == [0, 0]
+        # instance 1: batch 1 rolled back, then batch 2's row for oracle 3 stored on the original rows
+        v1 = x[1, :, s["lo"]:s["hi"]].clone()
+        v1[3] = ups[1][2][0, s["lo"]:s["hi"]]
+        assert torch.equal(deferred["values"][1, :, : s["hi"] - s["lo"]], v1)
 
 
 def _ds_exact_worker(rank, world, port, outdir, xs, cfgd):

@@ -163,6 +163,11 @@ def test_fused_streaming_matches_generic_path(storage, N, D, f, U):
     # instance 1: an update row with 1.5 in one column (rejected alone); instance 4: all its updated rows at
     # one value and the rest of the column too -> zero variance in column 3 if U == N, else a plain round
     vals[1 * U + 2, D // 2] = 1.5
+    # instance 2: two updates name no oracle (one of them with an out-of-interval row as well): the first
+    # reports NOT_ORACLE, the second INTERVAL_INPUT (the contract checks the interval first), neither is stored
+    orc[2 * U + 1] = N + 5
+    orc[2 * U + 3] = -1
+    vals[2 * U + 3, 0] = 2.0
     fz.values[4, :, 3] = 0.625
     gen.values[4, :, 3] = 0.625
     vals[4 * U:5 * U, 3] = 0.625
@@ -175,6 +180,7 @@ def test_fused_streaming_matches_generic_path(storage, N, D, f, U):
     torch.cuda.synchronize()
     assert torch.equal(st_f, st_g), (st_f.view(B, U), st_g.view(B, U))
     assert st_f[1 * U + 2].item() == int(Status.INTERVAL_INPUT)
+    assert st_f[2 * U + 1].item() == int(Status.NOT_ORACLE) and st_f[2 * U + 3].item() == int(Status.INTERVAL_INPUT)
     assert fz.status[4].item() == int(Status.ZERO_VARIANCE)
     for k in ("status", "values", "enabled", "n_active", "consensus", "rel", "c1", "reliable", "skew", "kurt", "qr"):
         a, b_ = getattr(fz, k), getattr(gen, k)
@@ -219,3 +225,43 @@ def test_bf16_kernel_rollback_matches_restore_kernel(N, D, f, U):
     assert (st_k.view(B, U)[1] == int(Status.ZERO_VARIANCE)).all()
     for k in ("status", "values", "enabled", "n_active", "consensus", "rel", "c1", "reliable", "skew", "kurt", "qr"):
         assert torch.equal(getattr(kr, k), getattr(rk, k)), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("storage", ["fp32", "bf16"])
+def test_pipelined_step_takes_host_batches(storage):
+    """step_pipelined with the batch on the host (int32 indices, float64 rows): converted to the state's
+    device and dtypes before any kernel reads it -- the same result as the device batch."""
+    N, D, B, U = 64, 256, 4, 16
+    dev_e, host_e = _engine("cuda", storage, N=N, D=D, B=B), _engine("cuda", storage, N=N, D=D, B=B)
+    for e in (dev_e, host_e):
+        e.randomize(seed=11)
+        e.run_round()
+    g = torch.Generator().manual_seed(2)
+    inst = torch.arange(B).repeat_interleave(U)
+    orc = torch.stack([torch.randperm(N, generator=g)[:U] for _ in range(B)]).reshape(-1)
+    vals = torch.rand(B * U, D, generator=g, dtype=torch.float64)
+    dev_e.step_pipelined(inst.cuda(), orc.cuda(), vals.cuda().to(dev_e.vdtype), U, chunks=2)
+    host_e.step_pipelined(inst.int(), orc.int(), vals, U, chunks=2)
+    dev_e.pipeline_join()
+    host_e.pipeline_join()
+    torch.cuda.synchronize()
+    for k in ("status", "values", "enabled", "n_active", "consensus", "rel", "c1"):
+        assert torch.equal(getattr(dev_e, k), getattr(host_e, k)), k
+
+
+@pytest.mark.gpu
+def test_kernels_reject_host_index_tensors():
+    """The update / restore / commit bindings refuse index tensors that are not on the state's device
+    (a host pointer handed to a GPU kernel)."""
+    from svoc import ops as svops
+    e = _engine("cuda", "fp32", N=16, D=64, B=2)
+    e.randomize(seed=1)
+    o = svops.ops()
+    rows = torch.rand(2, 64, device="cuda")
+    st = torch.zeros(2, dtype=torch.int32, device="cuda")
+    with pytest.raises(RuntimeError, match="must be on|device"):
+        o.commit_updates(rows, torch.tensor([0, 1]), st, e.values, 1)
+    with pytest.raises(RuntimeError, match="must be on|device"):
+        o.apply_updates(e.values, e.enabled, e.n_active, e.touched, e._winner, torch.tensor([0, 1]),
+                        torch.tensor([0, 1], device="cuda"), rows, True, st, True, None, None)

@@ -90,3 +90,40 @@ def test_pipeline_gpu_bert_base():
     assert (st == 0).all()
     assert eng.consensus_active.all()
     assert torch.isfinite(eng.consensus).all()
+
+
+def test_encoder_matches_hf_roberta_classifier():
+    """SentimentEncoder(pool="cls") loaded with a HF RobertaForSequenceClassification's weights computes that
+    classifier's 28 sigmoid scores (the reference's pipeline: client/oracle_scheduler.py:23-40 runs
+    SamLowe/roberta-base-go_emotions, a multi-label RoBERTa-base) -- random-init weights at full RoBERTa-base
+    size (no download), right-padded batches, fp32 on the CPU."""
+    transformers = pytest.importorskip("transformers")
+    from svoc.models.encoder import SentimentEncoder, config_from_hf, load_hf_roberta
+    torch.manual_seed(0)
+    hc = transformers.RobertaConfig(vocab_size=50265, num_labels=28, problem_type="multi_label_classification",
+                                    max_position_embeddings=514, type_vocab_size=1, layer_norm_eps=1e-5,
+                                    pad_token_id=1)
+    hf = transformers.RobertaForSequenceClassification(hc).eval()
+    with torch.no_grad():   # spread the scores (the default init leaves every logit near 0)
+        for n, p in hf.named_parameters():
+            if n.endswith("LayerNorm.weight"):
+                p.uniform_(0.8, 1.2)
+            elif n.endswith("bias"):
+                p.normal_(0.0, 0.02)
+            elif "classifier" in n:
+                p.normal_(0.0, 0.2)
+    ours = load_hf_roberta(SentimentEncoder(config_from_hf(hc)), hf.state_dict()).eval()
+    g = torch.Generator().manual_seed(1)
+    B, S = 6, 40
+    lens = torch.tensor([40, 7, 23, 2, 31, 12])
+    ids = torch.randint(3, 50265, (B, S), generator=g)
+    mask = (torch.arange(S)[None] < lens[:, None]).long()
+    ids[:, 0] = 0                                                    # <s>
+    ids[torch.arange(B), lens - 1] = 2                               # </s>
+    ids = torch.where(mask.bool(), ids, torch.ones_like(ids))        # <pad> = 1
+    with torch.no_grad():
+        ref = torch.sigmoid(hf(input_ids=ids, attention_mask=mask).logits)
+        got = ours(ids, mask)
+    assert got.shape == (B, 28)
+    assert float(ref.std()) > 0.05                                   # the comparison is not between constants
+    torch.testing.assert_close(got, ref, rtol=0, atol=1e-5)

@@ -125,3 +125,61 @@ def test_old_checkpoint_without_storage_key(tmp_path, monkeypatch):
     b = state.load(p)
     assert b.engine.storage == "fp32"
     assert torch.equal(a.engine.values, b.engine.values)
+
+
+def _pending_engine_pair():
+    cfg = ConsensusConfig(n_oracles=16, dimension=20, n_failing_oracles=2, n_admins=2)
+    svc = ConsensusService(cfg, 4, ADMINS[:2], [100 + i for i in range(16)], device="cpu", mode="fast",
+                           storage="fp32")
+    svc.engine.randomize(0)
+    svc.engine.run_round()
+    return svc
+
+
+def test_checkpoint_with_pending_batch_reverts_the_same(tmp_path):
+    """apply_updates, checkpoint, reload, run_round: the reverted instance goes back to its pre-batch rows
+    in the reloaded engine exactly as in the one that wrote the checkpoint (the rollback info
+    used to live only in Python and was lost by a checkpoint)."""
+    a = _pending_engine_pair()
+    e = a.engine
+    N, D = e.N, e.D
+    before = e.values.clone()
+    e.apply_updates(torch.full((N,), 1), torch.arange(N), torch.full((N, D), 0.5))   # instance 1: zero variance
+    e.apply_updates(torch.tensor([0, 0]), torch.tensor([3, 4]), torch.rand(2, D, generator=torch.Generator().manual_seed(4)))
+    p = os.path.join(tmp_path, "pending.svoc")
+    state.save(a, p)
+    b = state.load(p)
+    for eng in (a.engine, b.engine):
+        eng.run_round()
+        assert eng.status[1].item() != 0 and eng.status[0].item() == 0
+    assert torch.equal(a.engine.values, b.engine.values)
+    assert torch.equal(a.engine.values[1], before[1])                 # reverted: pre-batch rows
+    assert not torch.equal(a.engine.values[0], before[0])             # kept its update
+    for k in ("enabled", "n_active", "consensus", "rel"):
+        assert torch.equal(getattr(a.engine, k), getattr(b.engine, k)), k
+
+
+def test_many_pending_batches_fold_into_one_preimage():
+    """More than FOLD_AT batches before one round: the saved rows fold into one dense pre-image (bounded
+    memory) and the revert still restores the state from before the FIRST batch, statuses included."""
+    from svoc.engine import _PendingBatches
+    a = _pending_engine_pair()
+    e = a.engine
+    N, D = e.N, e.D
+    before = {k: getattr(e, k).clone() for k in ("values", "enabled", "n_active")}
+    sts = []
+    g = torch.Generator().manual_seed(5)
+    for k in range(_PendingBatches.FOLD_AT + 3):
+        # instance 2 collapses to one point over the batches (reverts); instance 3 gets ordinary rows
+        sts.append(e.apply_updates(torch.tensor([2, 2, 3]), torch.tensor([k % N, (k + 5) % N, k % N]),
+                                   torch.cat([torch.full((2, D), 0.5), torch.rand(1, D, generator=g)])))
+    assert e._pending.dense is not None and len(e._pending.entries) < _PendingBatches.FOLD_AT
+    e.values[2, :, :D] = 0.5                                           # (a direct write: every row of 2 at 0.5)
+    e.touched[2] = 1
+    e.run_round()
+    assert e.status[2].item() != 0 and e.status[3].item() == 0
+    assert torch.equal(e.values[2], before["values"][2]) and torch.equal(e.enabled, before["enabled"])
+    assert torch.equal(e.n_active, before["n_active"])
+    for st in sts:
+        assert st[:2].tolist() == [e.status[2].item()] * 2 and st[2].item() == 0
+    assert not e._pending
