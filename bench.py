@@ -136,12 +136,15 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
         from svoc.models.sentiment_oracle import SentimentOraclePipeline
         enc = None
         if enc_dtype is not None:
-            # the reference's precision (HF pipeline, fp32 weights: oracle_scheduler.py:23-25): fp32 GEMMs and
-            # the padded path (ATen attention; the MFMA attention kernel is bf16)
+            # the reference's precision (HF pipeline, fp32 weights: oracle_scheduler.py:23-25): fp32 GEMMs over the
+            # packed tokens, the fp32 encoder kernels (mfma_f32_32x32x2_f32 attention, fp32 LayerNorms)
             from svoc.models.encoder import build as build_encoder
             enc = build_encoder(dev, enc_dtype, 0)
-            enc.packed = False
         pipe = SentimentOraclePipeline(eng, encoder=enc, seed=0)
+        from svoc.models import encoder as _encm
+        extra["encoder_pool"] = pipe.encoder.cfg.pool
+        extra["encoder_gelu"] = "tanh (GEMM epilogue)" if _encm.GELU_EPILOGUE else "erf"
+        extra["encoder_packed"] = bool(pipe.encoder.packed)
         g = torch.Generator(device=dev).manual_seed(rank)
         toks = [corpus.synthetic_token_batch(B * 30, c["seq_len"], 50265, g, dev) for _ in range(2)]
         from svoc.models.encoder import flops_for_lengths
@@ -154,7 +157,13 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
     elif U_per_inst:
         from svoc.stream import SyntheticUpdateStream
         # D-sharding: every rank streams the same updates (same seed), its own column slice of them
-        stream = SyntheticUpdateStream(B, c["N"], D_local, U_per_inst, c["f"], pool=2, device=dev,
+        # one distinct batch per timed step (a period-2 stream would let any cross-round reuse
+        # measure cached answers), within a 96 GB budget for the resident pool
+        elem = 8 if mode == "exact" else eng.values.element_size()
+        per_batch = B * U_per_inst * (D_local * elem + 16)
+        pool = max(2, min(args.steps, int(96e9 // max(1, per_batch)))) if dev.type == "cuda" else 2
+        extra["stream_pool"] = pool
+        stream = SyntheticUpdateStream(B, c["N"], D_local, U_per_inst, c["f"], pool=pool, device=dev,
                                        seed=(0 if dshard else rank),
                                        dtype=torch.int64 if mode == "exact" else eng.vdtype,
                                        # the state's failing oracles stay the failing ones (D-shard:
@@ -241,9 +250,12 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
     if graph_ok:
         # the stream cycles with period `pool`: capture one period and replay it
         period = 1
-        for k in (stream.pool if stream is not None else 1, len(gov_batches) if gov is not None else 1,
-                  2 if pipe is not None else 1, 4 if pipeline > 1 else 1):   # (pipelined: 3 of 4 step
-            period = period * k // math.gcd(period, k)                        # boundaries overlap)
+        # (pipelined: a graph of at least 4 steps, so 3 of 4 step boundaries overlap; a pool of >= 4 steps
+        # already overlaps all but one)
+        sp = stream.pool if stream is not None else 1
+        for k in (sp, len(gov_batches) if gov is not None else 1,
+                  2 if pipe is not None else 1, 4 if (pipeline > 1 and sp < 4) else 1):
+            period = period * k // math.gcd(period, k)
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         # (D-shard at world > 1: the streams only -- pipeline_join would commit the deferred round with a
@@ -450,7 +462,7 @@ def main():
         out["config"]["alt_precision"] = {
             "encoder_dtype": "fp32", "value": rp["B"] * scale * args.steps / rp["elapsed"],
             "ms_per_step": 1e3 * rp["elapsed"] / args.steps, "ok_fraction": rp["ok"],
-            "path": "padded tokens, fp32 GEMMs (hipBLASLt), ATen attention"}
+            "path": "packed tokens, fp32 GEMMs (hipBLASLt), fp32 MFMA attention + fp32 LayerNorm kernels"}
         log_eng, log_step = rp["eng"], rp["step"]
     if rank == 0:
         print(json.dumps(out))

@@ -14,6 +14,14 @@ extern "C" int svoc_embed_layernorm_bf16(const int64_t* ids, const int64_t* pos_
                                          const void* typ, const void* w, const void* b, void* out, int64_t rows, int H,
                                          float eps, hipStream_t stream);
 extern "C" int svoc_segment_mean_bf16(const void* x, const int* cu, void* out, int64_t B, int H, hipStream_t stream);
+extern "C" int svoc_add_layernorm_f32(const float* x, const float* y, const float* w, const float* b, float* out,
+                                      int64_t rows, int H, float eps, int64_t y_stride, hipStream_t stream);
+extern "C" int svoc_embed_layernorm_f32(const int64_t* ids, const int64_t* pos_ids, const float* tok, const float* pos,
+                                        const float* typ, const float* w, const float* b, float* out, int64_t rows, int H,
+                                        float eps, hipStream_t stream);
+extern "C" int svoc_segment_mean_f32(const float* x, const int* cu, float* out, int64_t B, int H, hipStream_t stream);
+extern "C" int svoc_attention_short_f32(const float* qkv, const void* kmask, const int* cu_seqlens, int64_t rows_total,
+                                        float* out, int64_t B, int S, int H, int DH, hipStream_t stream);
 
 namespace svoc {
 namespace {
@@ -37,11 +45,20 @@ at::Tensor add_layernorm_hip(const at::Tensor& x, const at::Tensor& y, const at:
   const bool y_row = y.dim() == 1 && y.numel() == H;   // one [H] row broadcast over x's rows
   TORCH_CHECK(y_row || x.sizes() == y.sizes(), "add_layernorm: y must have x's shape or be one [H] row");
   TORCH_CHECK(w.numel() == H && b.numel() == H, "add_layernorm: weight/bias must have H elements");
-  const bool fast = x.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 &&
-                    w.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16 && hip_supported(H);
+  const auto dt = x.scalar_type();
+  const bool same = y.scalar_type() == dt && w.scalar_type() == dt && b.scalar_type() == dt;
+  const bool fast = same && (dt == at::kBFloat16 || dt == at::kFloat) && hip_supported(H);
   if (!fast) return add_layernorm_ref(x, y, w, b, eps);  // other dtypes / widths: ATen (documented)
   auto xc = x.contiguous(), yc = y.contiguous(), wc = w.contiguous(), bc = b.contiguous();
   auto out = at::empty_like(xc);
+  if (dt == at::kFloat) {
+    const int rc = svoc_add_layernorm_f32(xc.data_ptr<float>(), yc.data_ptr<float>(), wc.data_ptr<float>(),
+                                          bc.data_ptr<float>(), out.data_ptr<float>(), xc.numel() / H, (int)H,
+                                          (float)eps, y_row ? 0 : H,
+                                          c10::hip::getCurrentHIPStream(x.device().index()).stream());
+    TORCH_CHECK(rc == 0, "svoc_add_layernorm_f32 failed: ", rc);
+    return out;
+  }
   const int rc = svoc_add_layernorm_bf16(xc.data_ptr(), yc.data_ptr(), wc.data_ptr(), bc.data_ptr(), out.data_ptr(),
                                          xc.numel() / H, (int)H, (float)eps, y_row ? 0 : H,
                                          c10::hip::getCurrentHIPStream(x.device().index()).stream());
@@ -72,13 +89,21 @@ at::Tensor embed_layernorm_hip(const at::Tensor& ids, const at::Tensor& pos_ids,
   TORCH_CHECK(tok.dim() == 2 && pos.dim() == 2 && pos.size(1) == tok.size(1), "tok / pos tables: [V, H]");
   const int64_t H = tok.size(1);
   TORCH_CHECK(typ.numel() >= H && w.numel() == H && b.numel() == H, "typ / weight / bias: H elements");
-  const auto bf = at::kBFloat16;
-  const bool fast = tok.scalar_type() == bf && pos.scalar_type() == bf && typ.scalar_type() == bf &&
+  const auto bf = tok.scalar_type();
+  const bool fast = (bf == at::kBFloat16 || bf == at::kFloat) && pos.scalar_type() == bf && typ.scalar_type() == bf &&
                     w.scalar_type() == bf && b.scalar_type() == bf && hip_supported(H);
   if (!fast) return embed_layernorm_ref(ids, pos_ids, tok, pos, typ, w, b, eps);
   auto ic = ids.to(at::kLong).contiguous(), pc = pos_ids.to(at::kLong).contiguous();
   auto tc = tok.contiguous(), qc = pos.contiguous(), yc = typ.contiguous(), wc = w.contiguous(), bc = b.contiguous();
   auto out = at::empty({ids.size(0), H}, tc.options());
+  if (bf == at::kFloat) {
+    const int rc = svoc_embed_layernorm_f32(ic.data_ptr<int64_t>(), pc.data_ptr<int64_t>(), tc.data_ptr<float>(),
+                                            qc.data_ptr<float>(), yc.data_ptr<float>(), wc.data_ptr<float>(),
+                                            bc.data_ptr<float>(), out.data_ptr<float>(), ids.size(0), (int)H, (float)eps,
+                                            c10::hip::getCurrentHIPStream(tok.device().index()).stream());
+    TORCH_CHECK(rc == 0, "svoc_embed_layernorm_f32 failed: ", rc);
+    return out;
+  }
   const int rc = svoc_embed_layernorm_bf16(ic.data_ptr<int64_t>(), pc.data_ptr<int64_t>(), tc.data_ptr(), qc.data_ptr(),
                                            yc.data_ptr(), wc.data_ptr(), bc.data_ptr(), out.data_ptr(), ids.size(0),
                                            (int)H, (float)eps, c10::hip::getCurrentHIPStream(tok.device().index()).stream());
@@ -103,6 +128,14 @@ at::Tensor segment_mean_hip(const at::Tensor& x, const at::Tensor& cu) {
   TORCH_CHECK(cu.scalar_type() == at::kInt && cu.is_contiguous() && cu.device() == x.device(),
               "cu_seqlens: int32 on the device");
   const int64_t B = cu.numel() - 1, H = x.size(1);
+  if (x.scalar_type() == at::kFloat && H % 4 == 0 && H / 4 <= 256) {
+    auto xc = x.contiguous();
+    auto out = at::empty({B, H}, xc.options());
+    const int rc = svoc_segment_mean_f32(xc.data_ptr<float>(), cu.data_ptr<int>(), out.data_ptr<float>(), B, (int)H,
+                                         c10::hip::getCurrentHIPStream(x.device().index()).stream());
+    TORCH_CHECK(rc == 0, "svoc_segment_mean_f32 failed: ", rc);
+    return out;
+  }
   if (x.scalar_type() != at::kBFloat16 || H % 8 != 0 || H / 8 > 256) return segment_mean_ref(x, cu);
   auto xc = x.contiguous();
   auto out = at::empty({B, H}, xc.options());
@@ -168,7 +201,8 @@ at::Tensor attention_cpu(const at::Tensor& qkv, const c10::optional<at::Tensor>&
 at::Tensor attention_hip(const at::Tensor& qkv, const c10::optional<at::Tensor>& key_mask, int64_t heads) {
   TORCH_CHECK(qkv.dim() == 3 && qkv.size(2) % (3 * heads) == 0, "qkv: [B, S, 3*H*DH]");
   const int64_t B = qkv.size(0), S = qkv.size(1), HD = qkv.size(2) / 3, DH = HD / heads;
-  const bool ok = qkv.scalar_type() == at::kBFloat16 && DH == 64 && S % 32 == 0 && S >= 32 && S <= 128;
+  const bool f32 = qkv.scalar_type() == at::kFloat;
+  const bool ok = (qkv.scalar_type() == at::kBFloat16 || f32) && DH == 64 && S % 32 == 0 && S >= 32 && S <= 128;
   if (!ok) return attention_ref(qkv, key_mask, heads);  // other shapes: ATen (documented)
   auto x = qkv.contiguous();
   at::Tensor m;
@@ -177,6 +211,13 @@ at::Tensor attention_hip(const at::Tensor& qkv, const c10::optional<at::Tensor>&
     m = key_mask->to(at::kByte).contiguous();
   }
   auto out = at::empty({B, S, HD}, x.options());
+  if (f32) {
+    const int rc = svoc_attention_short_f32(x.data_ptr<float>(), key_mask.has_value() ? m.data_ptr() : nullptr, nullptr,
+                                            0, out.data_ptr<float>(), B, (int)S, (int)heads, (int)DH,
+                                            c10::hip::getCurrentHIPStream(x.device().index()).stream());
+    TORCH_CHECK(rc == 0, "svoc_attention_short_f32 failed: ", rc);
+    return out;
+  }
   const int rc = svoc_attention_short_bf16(x.data_ptr(), key_mask.has_value() ? m.data_ptr() : nullptr, nullptr, 0,
                                            out.data_ptr(), B, (int)S, (int)heads, (int)DH,
                                            c10::hip::getCurrentHIPStream(x.device().index()).stream());
@@ -211,11 +252,19 @@ at::Tensor attention_varlen_hip(const at::Tensor& qkv, const at::Tensor& cu, int
               "cu_seqlens: int32 [B+1] on the device");
   const int64_t T = qkv.size(0), HD = qkv.size(1) / 3, DH = HD / heads, B = cu.numel() - 1;
   const int64_t S = (max_len + 31) / 32 * 32;
-  const bool ok = qkv.scalar_type() == at::kBFloat16 && DH == 64 && S >= 32 && S <= 128;
+  const bool f32 = qkv.scalar_type() == at::kFloat;
+  const bool ok = (qkv.scalar_type() == at::kBFloat16 || f32) && DH == 64 && S >= 32 && S <= 128;
   if (!ok) return attention_varlen_ref(qkv, cu, max_len, heads);
   auto x = qkv.contiguous();
   auto out = at::empty({T, HD}, x.options());
   if (T == 0) return out;
+  if (f32) {
+    const int rc = svoc_attention_short_f32(x.data_ptr<float>(), nullptr, cu.data_ptr<int>(), T, out.data_ptr<float>(),
+                                            B, (int)S, (int)heads, (int)DH,
+                                            c10::hip::getCurrentHIPStream(x.device().index()).stream());
+    TORCH_CHECK(rc == 0, "svoc_attention_short_f32 (varlen) failed: ", rc);
+    return out;
+  }
   const int rc = svoc_attention_short_bf16(x.data_ptr(), nullptr, cu.data_ptr<int>(), T, out.data_ptr(), B, (int)S,
                                            (int)heads, (int)DH,
                                            c10::hip::getCurrentHIPStream(x.device().index()).stream());

@@ -444,3 +444,313 @@ extern "C" int svoc_segment_mean_bf16(const void* x, const int* cu, void* out, i
                      (uint16_t*)out, H, G);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// fp32 variants (the reference's precision: the HF pipeline runs the classifier in fp32,
+// client/oracle_scheduler.py:23-40).  Same one-wave-per-row layout as the bf16 kernels, 16-B loads
+// of 4 floats; the adds happen in fp32 in the order of the PyTorch expressions they replace.
+// ---------------------------------------------------------------------------------------------
+namespace svoc {
+
+template <int EPL>
+__device__ __forceinline__ void ln_store_f32(const float (&v)[EPL], float s, const float* __restrict__ w,
+                                             const float* __restrict__ bias, float* __restrict__ orow, float eps,
+                                             int lane) {
+  constexpr int H = 64 * EPL, V = EPL / 4;
+  const float mean = wave_sum(s) * (1.f / H);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < EPL; ++i) {
+    const float d = v[i] - mean;
+    q += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(q) * (1.f / H) + eps);
+  const float4* wr = (const float4*)w;
+  const float4* br = (const float4*)bias;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int c = k * 64 + lane;
+    const float4 gw = wr[c], gb = br[c];
+    float4 o;
+    o.x = (v[4 * k] - mean) * rstd * gw.x + gb.x;
+    o.y = (v[4 * k + 1] - mean) * rstd * gw.y + gb.y;
+    o.z = (v[4 * k + 2] - mean) * rstd * gw.z + gb.z;
+    o.w = (v[4 * k + 3] - mean) * rstd * gw.w + gb.w;
+    ((float4*)orow)[c] = o;
+  }
+}
+
+template <int EPL>
+__global__ __launch_bounds__(256) void add_layernorm_f32_kernel(const float* __restrict__ x, const float* __restrict__ y,
+                                                                const float* __restrict__ w,
+                                                                const float* __restrict__ bias, float* __restrict__ out,
+                                                                int64_t rows, float eps, int64_t y_stride) {
+  constexpr int H = 64 * EPL, V = EPL / 4;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float4* xr = (const float4*)(x + row * H);
+  const float4* yr = (const float4*)(y + row * y_stride);
+  float v[EPL];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int c = k * 64 + lane;
+    const float4 a = xr[c], b = yr[c];
+    v[4 * k] = a.x + b.x;
+    v[4 * k + 1] = a.y + b.y;
+    v[4 * k + 2] = a.z + b.z;
+    v[4 * k + 3] = a.w + b.w;
+    s += (v[4 * k] + v[4 * k + 1]) + (v[4 * k + 2] + v[4 * k + 3]);
+  }
+  ln_store_f32<EPL>(v, s, w, bias, out + row * H, eps, lane);
+}
+
+template <int EPL>
+__global__ __launch_bounds__(256) void embed_layernorm_f32_kernel(const int64_t* __restrict__ ids,
+                                                                  const int64_t* __restrict__ pos_ids,
+                                                                  const float* __restrict__ tok,
+                                                                  const float* __restrict__ pos,
+                                                                  const float* __restrict__ typ,
+                                                                  const float* __restrict__ w,
+                                                                  const float* __restrict__ bias,
+                                                                  float* __restrict__ out, int64_t rows, float eps) {
+  constexpr int H = 64 * EPL, V = EPL / 4;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float4* tr = (const float4*)(tok + ids[row] * H);
+  const float4* pr = (const float4*)(pos + pos_ids[row] * H);
+  const float4* yr = (const float4*)typ;
+  float v[EPL];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int c = k * 64 + lane;
+    const float4 a = tr[c], b = pr[c], t = yr[c];
+    v[4 * k] = (a.x + b.x) + t.x;
+    v[4 * k + 1] = (a.y + b.y) + t.y;
+    v[4 * k + 2] = (a.z + b.z) + t.z;
+    v[4 * k + 3] = (a.w + b.w) + t.w;
+    s += (v[4 * k] + v[4 * k + 1]) + (v[4 * k + 2] + v[4 * k + 3]);
+  }
+  ln_store_f32<EPL>(v, s, w, bias, out + row * H, eps, lane);
+}
+
+// segment mean of fp32 rows: thread (g, c) sums 4 columns (one 16-B load per row) of rows g, g + G, ...
+__global__ __launch_bounds__(256) void segment_mean_f32_kernel(const float* __restrict__ x, const int* __restrict__ cu,
+                                                               float* __restrict__ out, int H, int G) {
+  __shared__ float4 part[256];
+  const int b = blockIdx.x, chunks = H / 4;
+  const int tid = threadIdx.x, g = tid / chunks, c = tid % chunks;
+  const int lo = cu[b], hi = cu[b + 1];
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (g < G) {
+    for (int t = lo + g; t < hi; t += G) {
+      const float4 w = *(const float4*)(x + (int64_t)t * H + 4 * c);
+      acc.x += w.x;
+      acc.y += w.y;
+      acc.z += w.z;
+      acc.w += w.w;
+    }
+    part[tid] = acc;
+  }
+  __syncthreads();
+  if (g == 0) {
+    const float inv = 1.f / (float)(hi - lo > 1 ? hi - lo : 1);
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int gg = 0; gg < G; ++gg) {
+      const float4 p = part[gg * chunks + c];
+      a.x += p.x;
+      a.y += p.y;
+      a.z += p.z;
+      a.w += p.w;
+    }
+    *(float4*)(out + (int64_t)b * H + 4 * c) = make_float4(a.x * inv, a.y * inv, a.z * inv, a.w * inv);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// attn_f32_kernel: fp32 softmax(Q Kᵀ / 8) V for S <= 128, head dim 64, on v_mfma_f32_32x32x2_f32 (exact
+// fp32 products, fp32 accumulation).  Same orientation as the bf16 kernel: X = K·Qᵀ puts one query per lane
+// (its 64 key scores in the accumulator registers, the other 64 in lane ^ 32), so the softmax is
+// lane-local plus one xor-32 exchange.  The 64 head dims are split between the two lane halves
+// (instruction t sums dims t and 32 + t): every lane reads one contiguous half row of Q / K.
+// Z is computed transposed, Zᵀ = Vᵀ·Pᵀ: the B operand of instruction (key block, register i) is exactly
+// accumulator register x[kb][i] (keys (i&3) + 8(i>>2) + 4·hh), so P never moves; Vᵀ rows are read from
+// LDS one dim per lane (conflict-free).  K / V rows are staged with a 4-float pad (272-B stride).
+// ---------------------------------------------------------------------------------------------
+template <int NQB>
+__global__ __launch_bounds__(64 * NQB) void attn_f32_kernel(const float* __restrict__ qkv,
+                                                            const uint8_t* __restrict__ kmask,
+                                                            const int* __restrict__ cu_seqlens, int64_t rows_total,
+                                                            float* __restrict__ out, int H, float scale_log2) {
+  constexpr int S = 32 * NQB, DH = 64, RS = DH + 4;   // RS: padded LDS row stride (floats)
+  __shared__ __attribute__((aligned(16))) float Ks[S * RS];
+  __shared__ __attribute__((aligned(16))) float Vs[S * RS];
+  __shared__ uint8_t km[S];
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int64_t ts = (int64_t)3 * H * DH;
+  const int64_t base = cu_seqlens ? cu_seqlens[b] : (int64_t)b * S;
+  const int L = cu_seqlens ? cu_seqlens[b + 1] - cu_seqlens[b] : S;
+  const int nkb = (L + 31) >> 5;
+  auto row = [&](int k) -> int64_t {
+    const int64_t t = base + k;
+    return t < rows_total ? t : rows_total - 1;
+  };
+  const float* Qb = qkv + h * DH;
+  const float* Kb = Qb + H * DH;
+  const float* Vb = Qb + 2 * H * DH;
+  // stage K and V (16 float4 per row)
+  const int nchunks = nkb * 32 * (DH / 4);
+  for (int c = tid; c < nchunks; c += 64 * NQB) {
+    const int key = c >> 4, ch = c & 15;
+    const int64_t g = row(key) * ts + ch * 4;
+    *(float4*)(Ks + key * RS + ch * 4) = *(const float4*)(Kb + g);
+    *(float4*)(Vs + key * RS + ch * 4) = *(const float4*)(Vb + g);
+  }
+  for (int k = tid; k < S; k += 64 * NQB)
+    km[k] = cu_seqlens ? (uint8_t)(k < L) : (kmask ? kmask[(int64_t)b * S + k] : (uint8_t)1);
+  const int q0 = wave * 32;
+  const bool active = q0 < L;
+  float qf[32];
+  if (active) {
+    const float4* qp = (const float4*)(Qb + row(q0 + r) * ts + 32 * hh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float4 v = qp[j];
+      qf[4 * j] = v.x;
+      qf[4 * j + 1] = v.y;
+      qf[4 * j + 2] = v.z;
+      qf[4 * j + 3] = v.w;
+    }
+  }
+  __syncthreads();
+  if (!active) return;
+  f32x16 x[NQB];
+#pragma unroll
+  for (int kb = 0; kb < NQB; ++kb) {
+    x[kb] = f32x16{};
+    if (kb < nkb) {
+      const float* kr = Ks + (kb * 32 + r) * RS + 32 * hh;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float4 kv = *(const float4*)(kr + 4 * j);
+        x[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.x, qf[4 * j], x[kb], 0, 0, 0);
+        x[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.y, qf[4 * j + 1], x[kb], 0, 0, 0);
+        x[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.z, qf[4 * j + 2], x[kb], 0, 0, 0);
+        x[kb] = __builtin_amdgcn_mfma_f32_32x32x2f32(kv.w, qf[4 * j + 3], x[kb], 0, 0, 0);
+      }
+    }
+  }
+  // softmax over this lane's query (keys (i&3) + 8(i>>2) + 4hh of each block; lane ^ 32 the others)
+  float m = -__builtin_inff();
+#pragma unroll
+  for (int kb = 0; kb < NQB; ++kb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+      const bool on = kb < nkb && km[key];
+      const float v = on ? x[kb][i] * scale_log2 : -__builtin_inff();
+      x[kb][i] = v;
+      m = fmaxf(m, v);
+    }
+  m = fmaxf(m, __shfl_xor(m, 32));
+  float sum = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < NQB; ++kb)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const float p = exp2f(x[kb][i] - m);
+      x[kb][i] = p;
+      sum += p;
+    }
+  sum += __shfl_xor(sum, 32);
+  const float inv = 1.f / sum;
+  // Zᵀ[e][query] = sum over keys of V[key][e] P[query][key]
+  f32x16 z[2] = {f32x16{}, f32x16{}};
+#pragma unroll
+  for (int kb = 0; kb < NQB; ++kb) {
+    if (kb >= nkb) continue;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int key = kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+#pragma unroll
+      for (int eb = 0; eb < 2; ++eb)
+        z[eb] = __builtin_amdgcn_mfma_f32_32x32x2f32(Vs[key * RS + eb * 32 + r], x[kb][i], z[eb], 0, 0, 0);
+    }
+  }
+  // z[eb][i] = Zᵀ[e = eb*32 + (i&3) + 8(i>>2) + 4hh][query q0 + r]: four consecutive dims per float4
+  const int q = q0 + r;
+  if (q < L) {
+    float* orow = out + (base + q) * H * DH + h * DH;
+#pragma unroll
+    for (int eb = 0; eb < 2; ++eb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int e = eb * 32 + 8 * g + 4 * hh;
+        *(float4*)(orow + e) = make_float4(z[eb][4 * g] * inv, z[eb][4 * g + 1] * inv, z[eb][4 * g + 2] * inv,
+                                           z[eb][4 * g + 3] * inv);
+      }
+  }
+}
+
+}  // namespace svoc
+
+extern "C" int svoc_add_layernorm_f32(const float* x, const float* y, const float* w, const float* b, float* out,
+                                      int64_t rows, int H, float eps, int64_t y_stride, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  switch (H) {
+    case 256: hipLaunchKernelGGL(add_layernorm_f32_kernel<4>, grid, block, 0, stream, x, y, w, b, out, rows, eps, y_stride); break;
+    case 512: hipLaunchKernelGGL(add_layernorm_f32_kernel<8>, grid, block, 0, stream, x, y, w, b, out, rows, eps, y_stride); break;
+    case 768: hipLaunchKernelGGL(add_layernorm_f32_kernel<12>, grid, block, 0, stream, x, y, w, b, out, rows, eps, y_stride); break;
+    case 1024: hipLaunchKernelGGL(add_layernorm_f32_kernel<16>, grid, block, 0, stream, x, y, w, b, out, rows, eps, y_stride); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int svoc_embed_layernorm_f32(const int64_t* ids, const int64_t* pos_ids, const float* tok, const float* pos,
+                                        const float* typ, const float* w, const float* b, float* out, int64_t rows, int H,
+                                        float eps, hipStream_t stream) {
+  if (rows <= 0) return 0;
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+  switch (H) {
+    case 256: hipLaunchKernelGGL(embed_layernorm_f32_kernel<4>, grid, block, 0, stream, ids, pos_ids, tok, pos, typ, w, b, out, rows, eps); break;
+    case 512: hipLaunchKernelGGL(embed_layernorm_f32_kernel<8>, grid, block, 0, stream, ids, pos_ids, tok, pos, typ, w, b, out, rows, eps); break;
+    case 768: hipLaunchKernelGGL(embed_layernorm_f32_kernel<12>, grid, block, 0, stream, ids, pos_ids, tok, pos, typ, w, b, out, rows, eps); break;
+    case 1024: hipLaunchKernelGGL(embed_layernorm_f32_kernel<16>, grid, block, 0, stream, ids, pos_ids, tok, pos, typ, w, b, out, rows, eps); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+extern "C" int svoc_segment_mean_f32(const float* x, const int* cu, float* out, int64_t B, int H, hipStream_t stream) {
+  if (B <= 0) return 0;
+  if (H % 4 != 0 || H / 4 > 256 || B > 0x7fffffffll) return -1;
+  const int chunks = H / 4;
+  int G = 256 / chunks;
+  if (G > 8) G = 8;
+  hipLaunchKernelGGL(segment_mean_f32_kernel, dim3((unsigned)B), dim3(chunks * G), 0, stream, x, cu, out, H, G);
+  return (int)hipGetLastError();
+}
+
+// fp32 twin of svoc_attention_short_bf16 (same layouts and packed / padded modes)
+extern "C" int svoc_attention_short_f32(const float* qkv, const void* kmask, const int* cu_seqlens, int64_t rows_total,
+                                        float* out, int64_t B, int S, int H, int DH, hipStream_t stream) {
+  if (DH != 64 || S % 32 != 0 || S < 32 || S > 128 || B * H > 0x7fffffffll) return -1;
+  if (B == 0) return 0;
+  const float scale_log2 = 1.4426950408889634f / 8.f;
+  const auto* M = (const uint8_t*)kmask;
+  const int64_t R = cu_seqlens ? rows_total : B * S;
+  const dim3 grid((unsigned)(B * H));
+  switch (S / 32) {
+    case 1: hipLaunchKernelGGL(attn_f32_kernel<1>, grid, dim3(64), 0, stream, qkv, M, cu_seqlens, R, out, H, scale_log2); break;
+    case 2: hipLaunchKernelGGL(attn_f32_kernel<2>, grid, dim3(128), 0, stream, qkv, M, cu_seqlens, R, out, H, scale_log2); break;
+    case 3: hipLaunchKernelGGL(attn_f32_kernel<3>, grid, dim3(192), 0, stream, qkv, M, cu_seqlens, R, out, H, scale_log2); break;
+    default: hipLaunchKernelGGL(attn_f32_kernel<4>, grid, dim3(256), 0, stream, qkv, M, cu_seqlens, R, out, H, scale_log2); break;
+  }
+  return (int)hipGetLastError();
+}

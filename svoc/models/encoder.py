@@ -7,15 +7,19 @@ head, sigmoid scores for all 28 go_emotions labels; the client keeps 6 labels
 
 There is no network on the GPU boxes, so the weights are random-initialised with a fixed seed and
 the architecture is BERT-base sized (12 layers, hidden 768, 12 heads, FFN 3072, vocab 50265,
-512 positions).  The implementation is plain PyTorch-ROCm: bf16 weights, fused QKV projection
-(one hipBLASLt GEMM), a hand-written MFMA attention kernel for the short windows (S <= 128) that
-reads the QKV projection in place, GELU in the FC1 GEMM epilogue, fused residual-add + LayerNorm;
-pre-sized buffers so the forward can be captured in a HIP graph.
+512 positions).  The implementation is plain PyTorch-ROCm: bf16 (or fp32, the reference's precision)
+weights, fused QKV projection (one hipBLASLt GEMM), hand-written MFMA attention kernels for the short
+windows (S <= 128: mfma_f32_32x32x16_bf16 / mfma_f32_32x32x2_f32) that read the QKV projection in place
+over the packed (unpadded) tokens, erf GELU after the FC1 GEMM, fused residual-add + LayerNorm, fused
+embeddings + LayerNorm and segment pooling (encoder_ops.hip, bf16 and fp32); pre-sized buffers so the
+forward can be captured in a HIP graph.  ``load_hf_roberta`` maps a HF RobertaForSequenceClassification
+checkpoint (e.g. SamLowe/roberta-base-go_emotions, if present locally) onto it.
 """
 from __future__ import annotations
 
 import dataclasses
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -97,11 +101,21 @@ class PackPlan:
     max_len: int
 
 
+# RoBERTa's FFN activation is the erf GELU (HF hidden_act "gelu").  The hipBLASLt GELU epilogue of
+# torch._addmm_activation computes the tanh approximation (tools/probe_gelu_kind.py on the MI355X: fp32
+# epilogue - tanh GELU 4.8e-7, - erf GELU 4.7e-4), so the default is the GEMM (bias epilogue) followed by
+# an in-place erf GELU over the [tokens, 3072] activation; SVOC_GELU_EPILOGUE=1 selects the tanh epilogue.
+GELU_EPILOGUE = os.environ.get("SVOC_GELU_EPILOGUE", "0") == "1"
+
+
 def _linear_gelu(x: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
-    """fc1 + GELU; on the GPU the GELU runs in the hipBLASLt GEMM epilogue (one pass over the
-    [tokens, 3072] activation instead of two)."""
+    """fc1 + erf GELU (the GPU: hipBLASLt GEMM with the bias epilogue, then the GELU in place)."""
     if x.is_cuda:
-        y = torch._addmm_activation(fc.bias, x.reshape(-1, x.shape[-1]), fc.weight.t(), use_gelu=True)
+        x2 = x.reshape(-1, x.shape[-1])
+        if GELU_EPILOGUE:
+            y = torch._addmm_activation(fc.bias, x2, fc.weight.t(), use_gelu=True)
+        else:
+            y = torch.ops.aten.gelu_(torch.addmm(fc.bias, x2, fc.weight.t()))
         return y.view(*x.shape[:-1], -1)
     return F.gelu(fc(x))
 

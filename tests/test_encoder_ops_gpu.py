@@ -103,16 +103,18 @@ def test_encoder_oracle_vectors_match_cpu_fp32_bert_base(packed):
         vg = scores_to_oracle_vectors(enc_g(ids.cuda(), mask.cuda()).float().cpu())
         vc = scores_to_oracle_vectors(enc_c(ids, mask))
     err = (vg - vc).abs().max().item()
-    assert err <= 0.01, err
+    assert err <= 0.005, err
 
 
-def test_encoder_fp32_gpu_matches_cpu():
-    """The fp32 GPU encoder (bench.py's reference-precision c4 field: the padded path, ATen attention)
-    equals the CPU fp32 encoder to fp32 rounding: the GEMMs sum in a different order (hipBLASLt vs the CPU
-    BLAS) through 12 layers; measured max |delta| of the normalised 6-vectors 0.8e-4 - 1.13e-4 across boxes."""
+@pytest.mark.parametrize("packed", [True, False])
+def test_encoder_fp32_gpu_matches_cpu(packed):
+    """The fp32 GPU encoder (bench.py's reference-precision c4 field: packed tokens, the fp32 MFMA attention and
+    LayerNorm kernels; or the padded path) equals the CPU fp32 encoder to fp32 rounding: the GEMMs sum in a
+    different order (hipBLASLt vs the CPU BLAS) through 12 layers; round 4 measured max |delta| of the
+    normalised 6-vectors 0.8e-4 - 1.13e-4 across boxes."""
     from svoc.models.encoder import build, scores_to_oracle_vectors
     enc_g = build("cuda", torch.float32, seed=12)
-    enc_g.packed = False
+    enc_g.packed = packed
     enc_c = build("cpu", torch.float32, seed=12)
     g = torch.Generator().manual_seed(6)
     ids = torch.randint(3, enc_c.cfg.vocab_size, (4, 128), generator=g)
@@ -183,3 +185,82 @@ def test_segment_mean_bf16():
     assert torch.equal(out[1].float(), torch.zeros(H, device="cuda"))
     cpu = svops.ops().segment_mean(x.cpu(), cu.cpu())
     torch.testing.assert_close(out.cpu().float(), cpu.float(), rtol=1e-2, atol=1e-2)
+
+
+# ---------------------------------------------------------------- fp32 kernels (the reference's precision)
+@pytest.mark.parametrize("rows,H", [(1, 768), (1023, 768), (257, 256), (64, 1024)])
+def test_add_layernorm_f32(rows, H):
+    g = torch.Generator(device="cuda").manual_seed(rows + H + 1)
+    x = torch.randn(rows, H, device="cuda", generator=g)
+    y = 0.5 * torch.randn(rows, H, device="cuda", generator=g) + 0.1
+    w = 1 + 0.1 * torch.randn(H, device="cuda", generator=g)
+    b = 0.1 * torch.randn(H, device="cuda", generator=g)
+    out = svops.ops().add_layernorm(x, y, w, b, 1e-5)
+    ref = F.layer_norm((x + y).double(), (H,), w.double(), b.double(), 1e-5)
+    assert out.dtype == torch.float32
+    torch.testing.assert_close(out.double(), ref, rtol=0, atol=2e-5)
+    row = svops.ops().add_layernorm(x, y[0], w, b, 1e-5)                      # broadcast [H] row
+    torch.testing.assert_close(row.double(), F.layer_norm((x + y[0]).double(), (H,), w.double(), b.double(), 1e-5),
+                               rtol=0, atol=2e-5)
+
+
+def test_embed_layernorm_f32():
+    V, P, T, H = 300, 130, 999, 768
+    g = torch.Generator(device="cuda").manual_seed(11)
+    tok = 0.02 * torch.randn(V, H, device="cuda", generator=g)
+    pos = 0.02 * torch.randn(P, H, device="cuda", generator=g)
+    typ = 0.02 * torch.randn(1, H, device="cuda", generator=g)
+    w = 1 + 0.1 * torch.randn(H, device="cuda", generator=g)
+    b = 0.1 * torch.randn(H, device="cuda", generator=g)
+    ids = torch.randint(0, V, (T,), device="cuda", generator=g)
+    pid = torch.randint(0, P, (T,), device="cuda", generator=g)
+    out = svops.ops().embed_layernorm(ids, pid, tok, pos, typ, w, b, 1e-5)
+    ref = F.layer_norm((tok[ids] + pos[pid] + typ[0]).double(), (H,), w.double(), b.double(), 1e-5)
+    torch.testing.assert_close(out.double(), ref, rtol=0, atol=2e-5)
+
+
+def test_segment_mean_f32():
+    lens = [5, 0, 1, 128, 77, 3]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device="cuda")
+    T, H = int(cu[-1]), 768
+    x = torch.randn(T, H, device="cuda", generator=torch.Generator(device="cuda").manual_seed(8))
+    out = svops.ops().segment_mean(x, cu)
+    ref = torch.stack([x[int(cu[i]):int(cu[i + 1])].double().sum(0) / max(lens[i], 1) for i in range(len(lens))])
+    torch.testing.assert_close(out.double(), ref, rtol=0, atol=1e-5)
+    assert torch.equal(out[1], torch.zeros(H, device="cuda"))
+
+
+def _attn_ref64(qkv, mask, heads):
+    B, S, H3 = qkv.shape
+    DH = H3 // 3 // heads
+    t = qkv.double().view(B, S, 3, heads, DH).permute(2, 0, 3, 1, 4)
+    s = t[0] @ t[1].transpose(-1, -2) / DH ** 0.5
+    if mask is not None:
+        s = s.masked_fill(~mask.bool()[:, None, None, :], float("-inf"))
+    return (torch.softmax(s, -1) @ t[2]).transpose(1, 2).reshape(B, S, H3 // 3)
+
+
+@pytest.mark.parametrize("S", [32, 64, 96, 128])
+def test_attention_qkv_f32_mfma(S):
+    """fp32 attention on mfma_f32_32x32x2_f32 vs an fp64 reference (fp32 products, fp32 sums)."""
+    B, heads = 5, 12
+    g = torch.Generator(device="cuda").manual_seed(S + 7)
+    qkv = torch.randn(B, S, 3 * heads * 64, device="cuda", generator=g)
+    lens = torch.randint(1, S + 1, (B,), device="cuda", generator=g)
+    mask = (torch.arange(S, device="cuda")[None] < lens[:, None]).to(torch.uint8)
+    out = svops.ops().attention_qkv(qkv, mask, heads)
+    assert out.dtype == torch.float32 and out.shape == (B, S, heads * 64)
+    torch.testing.assert_close(out.double(), _attn_ref64(qkv, mask, heads), rtol=0, atol=2e-5)
+    out2 = svops.ops().attention_qkv(qkv, None, heads)
+    torch.testing.assert_close(out2.double(), _attn_ref64(qkv, None, heads), rtol=0, atol=2e-5)
+
+
+def test_attention_varlen_f32_mfma():
+    heads = 12
+    lens = [128, 1, 33, 64, 95, 7, 128, 32]
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device="cuda")
+    T = int(cu[-1])
+    qkv = torch.randn(T, 3 * heads * 64, device="cuda", generator=torch.Generator(device="cuda").manual_seed(3))
+    out = svops.ops().attention_varlen(qkv, cu, max(lens), heads)
+    ref = svops.ops().attention_varlen(qkv.cpu().double(), cu.cpu(), max(lens), heads)
+    torch.testing.assert_close(out.double().cpu(), ref, rtol=0, atol=2e-5)
