@@ -122,7 +122,19 @@ struct ExactParams {
   // reliability's dimension (the GLOBAL D; 0 = D).
   int mode;
   int rel_dim;
+  int win_h;                // the column kernel's window half-width (exact_win_h; the stage holds 4 + 2 win_h rows)
 };
+
+// Window half-width of the column-parallel exact kernel's one-network path (consensus_wsad.hip): the
+// smallest of {5, 17} covering ranks R/2 - 1 .. R/2 + f of the full column, i.e. >= max(a + 1, f - a + 1)
+// with a = N/2 - R/2; 0 = no window (two median networks).
+inline int exact_win_h(int N, int f) {
+  if (N < 4 || f < 0 || f > N - 2) return 0;
+  const int R = N - f, a = N / 2 - R / 2;
+  const int need = a + 1 > f - a + 1 ? a + 1 : f - a + 1;
+  // (N <= 64 with 17: the one-lane-group kernel goes past 256 VGPRs, one wave per SIMD -- two networks win)
+  return need <= 5 ? 5 : (need <= 17 && N > 64) ? 17 : 0;
+}
 
 
 }  // namespace svoc

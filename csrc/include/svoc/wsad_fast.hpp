@@ -93,6 +93,59 @@ SVOC_HD double wdiv_h(double a, double b) {
   return tdiv_h(fma(a, kW, floor(b * 0.5)), ib, 0.5 * ib);
 }
 
+// ---- Wide forms (unconstrained values far from each other: price-like columns) ------------------------
+// quadratic_deviation(a, b) for |d| = |a - b| < 2^31 (d^2 < 2^62, quotient < 2^43): the square as the exact
+// double-double p + e, the quotient estimated from p (within 2 of the truth), then corrected with the exact
+// remainder p - q0 1e6 (an fma: the difference is a small integer) plus e + 500000, floored by the half-offset form.
+SVOC_HD double qdev_wide(double d) {
+  const double p = d * d;
+  const double e = fma(d, d, -p);                      // d^2 = p + e exactly
+  const double q0 = floor(p * kInv6);
+  const double r = fma(-q0, kW, p) + (e + 500000.0);   // exact: |r| < 2^23
+  return q0 + floor((r + 0.5) * kInv6);
+}
+
+// floor(A / g) for 0 <= A < 2^63, 1 <= g < 2^53 in int64 (fp64 estimate, exact remainder correction)
+SVOC_HD int64_t floor_div_i64(int64_t A, int64_t g) {
+  int64_t q = (int64_t)((double)A / (double)g);
+  int64_t r = A - q * g;
+  while (r < 0) { --q; r += g; }
+  while (r >= g) { ++q; r -= g; }
+  return q;
+}
+
+// sqrt (math.cairo:271-292) for integral 0 <= v < 2^43: wsad_div(v, g) = trunc((v 1e6 + g / 2) / g) in int64
+// (the dividend passes 2^53).  Same Newton steps and stop rule as wsqrt; false where the contract divides by 0.
+SVOC_HD bool wsqrt_wide(int64_t v, int64_t& out) {
+  if (v == 0) {
+    out = 0;
+    return true;
+  }
+  int64_t g = v / 2, g2 = g + 1000000;
+  for (int i = 0; i < MAX_SQRT_ITERATIONS; ++i) {
+    if (g == g2) break;
+    if (g == 0) return false;
+    const int64_t n = floor_div_i64(v * 1000000 + g / 2, g);
+    g2 = g;
+    g = (g + n) / 2;
+  }
+  out = g;
+  return true;
+}
+
+// trunc((S + k B) / k) - B for k >= 1, |S| < 2^51, |k B + S| < 2^63: the truncated quotient of a sum taken
+// relative to a base B (the smooth median and the mean of a column stored relative to its first row,
+// math.cairo:113-126, 240-254, with I128Div's truncation toward zero, signed_decimal.cairo:52-63).
+SVOC_HD int64_t tdiv_rel(int64_t S, int64_t B, int64_t k) {
+  int64_t q = S / k;                                     // trunc(S / k)
+  if (q * k != S) {
+    const int64_t T = k * B + S;                         // sign of the absolute quotient (never 0 here)
+    if (S < 0 && T > 0) q -= 1;                          // floor instead of trunc
+    else if (S > 0 && T < 0) q += 1;                     // ceil instead of trunc
+  }
+  return q;
+}
+
 // sqrt (math.cairo:271-292) for integral 0 <= v < 2^31: the same Newton steps and stop rule
 // (g == previous g, at most 50 iterations).  Returns false where the contract reverts: a zero
 // divisor (sqrt(1) -- g = 0 after the first halving).

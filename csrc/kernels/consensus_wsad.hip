@@ -144,8 +144,18 @@ SVOC_DEV T group_sum(T v) {
 // i128 kernel): values within 2^30 of 0 (1073.7 in real units) and within 2^25 (33.55) of their column's
 // smooth median and of its reliable mean -- the bound under which the fp64 forms of qdev / wsad_div are
 // exact (wsad_fast.hpp); the qr butterfly then sums 64-bit partials.
-template <int NSEG, int WAVES, bool V32, int MODE, bool CONS>
+// WINH > 0 (whole constrained rounds, launch_wsad_c): ONE median network per column.  Pass 1 keeps the
+// 2 WINH keys around the median (window_group, sortnet.hpp) in the staging buffer; the pass-2 smooth
+// median over the reliable rows is then read off that window by ranking the f removed rows' keys
+// against it (one lane per column, f + 2 WINH loads):  with G the sorted column, U the sorted removed
+// keys (u_f = +inf) and A = G \ U, the r-th smallest of A is  min over j in [0, f] of { g_{r+j} : g_{r+j} <
+// u_j }  (multisets, ties included: with Q = #{U <= a_r}, g_{r+Q} = a_r and u_Q > a_r; any qualifying
+// g_{r+j} has at least r + 1 elements of A at or below it).  Ranks R/2 - 1 and R/2 (math.cairo:113-126)
+// need g at positions R/2 - 1 .. R/2 + f, inside the window when WINH >= max(a + 1, f - a + 1),
+// a = N/2 - R/2.  The second network over the reliable rows (~30 % of the kernel's VALU) goes away.
+template <int NSEG, int WAVES, bool V32, int MODE, bool CONS, int WINH = 0>
 __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams p) {
+  static_assert(WINH == 0 || (MODE == 0 && CONS), "the window path is for whole constrained rounds");
   constexpr int P = 64 / NSEG;      // columns per wave
   constexpr int NPAD = 64 * NSEG;   // padded oracle rows
   constexpr int W = WAVES * P;      // columns per tile
@@ -164,6 +174,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   __shared__ int flag;
   __shared__ int early_st;   // a revert decided before the moments (its final status)
   __shared__ int div0;       // a moment stage divides by zero (the round reverts with DIV_BY_ZERO)
+  __shared__ int urow[WINH > 0 ? 2 * WINH : 1];   // window path: the removed rows, index order
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -182,7 +193,8 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   const int rowb = D * ESZ;
   const __amdgpu_buffer_rsrc_t rs =
       instance_rsrc((const unsigned char*)p.values + (int64_t)b * N * rowb, (uint32_t)(N * rowb));
-  int32_t* const stg = p.stage + (int64_t)b * 4 * D;   // [4][D]: c1, consensus, skewness, kurtosis
+  // [4 + 2 WINH][D]: c1, consensus, skewness, kurtosis, then the window keys (WINH > 0)
+  int32_t* const stg = p.stage + (int64_t)b * (4 + 2 * WINH) * D;
   const int nslab = (D + W - 1) / W;
   const int lo1 = (NPAD - N + 1) >> 1;   // pass-1 sentinel split (rows >= N): -inf first, then +inf
   const int nv = N - seg * 64;           // this lane's rows < nv are real
@@ -217,7 +229,29 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
         r[i] = (real ? x ^ kSign : (i < nl ? 0u : ~0u)) ^ pol;
       }
       uint32_t lo, hi;
-      median_group<NSEG>(r, lo, hi);   // smooth median: ranks N/2 - 1, N/2 (math.cairo:113-126)
+      if constexpr (WINH > 0) {
+        // the median pair and the window W[t] = key at padded position NPAD/2 - WINH + t (t < 2 WINH),
+        // staged at rows 4 .. 4 + 2 WINH of this instance's stage (true keys = the values)
+        constexpr int WN = NSEG == 1 ? 2 * WINH : WINH;
+        uint32_t w[WN];
+        window_group<NSEG, P, WINH>(r, seg, lane, w, lo, hi);
+        constexpr int SLO = NSEG == 4 ? 1 : 0;   // the lane holding the lower part (the upper: SLO + 1)
+        if (vc) {
+#pragma unroll
+          for (int m = 0; m < WINH; ++m) {
+            if (NSEG == 1) {
+              stg[(4 + m) * D + col] = (int32_t)w[m];
+              stg[(4 + 2 * WINH - 1 - m) * D + col] = (int32_t)~w[WINH + m];
+            } else if (seg == SLO) {
+              stg[(4 + m) * D + col] = (int32_t)w[m];
+            } else if (seg == SLO + 1) {
+              stg[(4 + 2 * WINH - 1 - m) * D + col] = (int32_t)~w[m];
+            }
+          }
+        }
+      } else {
+        median_group<NSEG>(r, lo, hi);   // smooth median: ranks N/2 - 1, N/2 (math.cairo:113-126)
+      }
       if constexpr (CONS) {
         c1 = (lo + hi) >> 1;           // idiv_pos64(a + b, 2) of non-negative values
       } else {                         // I128Div(a + b, 2): truncation toward zero
@@ -384,6 +418,47 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   }
 
   // ------------------------------------------------------------ pass 2 (contract.cairo:476-500)
+  if constexpr (WINH > 0) {
+    // the pass-2 smooth median from the window (see above): one lane per column
+    if (tid == 0) {
+      int k = 0;
+      for (int t = 0; t < N && k < 2 * WINH; ++t)
+        if (!((relmask[t >> 6] >> (t & 63)) & 1)) urow[k++] = t;
+    }
+    __syncthreads();
+    const int a = N / 2 - R / 2;
+    const int wb = WINH - a - 1;   // window index of position R/2 - 1 (>= 0: launch_wsad_c checked)
+    for (int col = tid; col < D; col += NT) {
+      uint32_t z[64];
+#pragma unroll
+      for (int t = 0; t < 64; ++t) {
+        if (t < 2 * WINH) {
+          const int ur = __builtin_amdgcn_readfirstlane(urow[t < f ? t : 0]);
+          const uint32_t x = bload(rs, col * ESZ, ur * rowb);
+          z[t] = t < f ? x : ~0u;   // u_f.. = +inf
+        } else {
+          z[t] = ~0u;
+        }
+      }
+      sort_oem<64>(z);
+      uint32_t gw[2 * WINH];
+#pragma unroll
+      for (int t = 0; t < 2 * WINH; ++t) {
+        const int wi = wb + t < 2 * WINH ? wb + t : 2 * WINH - 1;   // (t <= f + 1 < 2 WINH - wb)
+        gw[t] = (uint32_t)stg[(4 + wi) * D + col];
+      }
+      uint32_t lo = ~0u, hi = ~0u;
+#pragma unroll
+      for (int j = 0; j + 1 < 2 * WINH; ++j) {
+        if (j <= f) {   // (uniform)
+          lo = kmin(lo, gw[j] < z[j] ? gw[j] : ~0u);
+          hi = kmin(hi, gw[j + 1] < z[j] ? gw[j + 1] : ~0u);
+        }
+      }
+      stg[D + col] = (int32_t)((lo + hi) >> 1);
+    }
+    __syncthreads();   // (the slab loop reads other threads' columns)
+  }
   const uint64_t mymask = relmask[seg];
   const uint64_t mylow = lowmask[seg];
   const double Rd = (double)R, invR = recip_lo(Rd);
@@ -398,7 +473,9 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     uint64_t mm = mymask, ml = mylow;
     asm volatile("" : "+v"(mm), "+v"(ml));   // keep the 64 row masks out of the slab loop's live set
     uint32_t cons = 0;
-    if constexpr (CONS) {
+    if constexpr (CONS && WINH > 0) {
+      cons = (uint32_t)stg[D + (vc ? col : 0)];   // (the window phase above)
+    } else if constexpr (CONS) {
       uint32_t r[64];
       if constexpr (BATCH && (MODE != 2 || V32)) {   // values validated in pass 1 (or 32-bit): one batch
         load_lo(rs, vo, rowb, r);
@@ -439,7 +516,9 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     if constexpr (CONS) {
       uint32_t sx = 0;
       if constexpr (BATCH1) {
-        load_lo(rs, after(vo, cons), rowb, xr);
+        // (window path: no network in this loop, so the column is loaded once and kept for the mean,
+        // variance and z-power loops; otherwise re-read per statistic)
+        load_lo(rs, WINH > 0 ? vo : after(vo, cons), rowb, xr);
 #pragma unroll
         for (int i = 0; i < 64; ++i) sx += xr[i] & bit_mask(mm, i);
       } else {
@@ -461,8 +540,8 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     double var;
     if constexpr (CONS) {
       uint32_t sv = 0;
-      if constexpr (BATCH) {
-        load_lo(rs, after(vo, mu), rowb, xr);
+      if constexpr (BATCH || (WINH > 0 && BATCH1)) {
+        if constexpr (WINH == 0) load_lo(rs, after(vo, mu), rowb, xr);
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
           if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
@@ -515,8 +594,8 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       s3 += wmul_h(z2, z, z < 0.0);
       s4 += wmul_pos_h(z2, z2);
     };
-    if constexpr (BATCH) {
-      load_lo(rs, after(vo, sd), rowb, xr);
+    if constexpr (BATCH || (WINH > 0 && BATCH1)) {
+      if constexpr (WINH == 0) load_lo(rs, after(vo, sd), rowb, xr);
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bound the fp64 temporaries in flight
@@ -611,6 +690,13 @@ template <int NSEG, bool CONS>
 static int launch_wsad_c(const ExactParams& p, hipStream_t stream) {
   constexpr int WAVES = 4;
   auto k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 0, CONS> : consensus_wsad_kernel<NSEG, WAVES, false, 0, CONS>;
+  if constexpr (CONS) {
+    // whole constrained rounds: the one-network window path (exact_win_h: 0 = a second network)
+    const int h = p.mode == 0 && !p.legacy ? exact_win_h(p.N, p.n_failing) : 0;
+    if (h == 5) k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 0, true, 5> : consensus_wsad_kernel<NSEG, WAVES, false, 0, true, 5>;
+    if (h == 17) k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 0, true, 17> : consensus_wsad_kernel<NSEG, WAVES, false, 0, true, 17>;
+    if (h != p.win_h) return -3;   // (the caller sized the stage for p.win_h)
+  }
   if (p.mode == 1)
     k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 1, CONS> : consensus_wsad_kernel<NSEG, WAVES, false, 1, CONS>;
   if (p.mode == 2)

@@ -251,11 +251,51 @@ static void wsad_half_paths() {
   }
 }
 
+// The wide forms (wsad_fast.hpp: unconstrained price-like columns) against the i128 routines.
+static void wsad_wide_paths() {
+  std::mt19937_64 rng(4242);
+  auto uni = [&](int64_t lo, int64_t hi) { return lo + (int64_t)(rng() % (uint64_t)(hi - lo + 1)); };
+  int bad = 0;
+  for (int it = 0; it < 2000000 && bad < 10; ++it) {
+    int st = ST_OK;
+    const int64_t d = it & 1 ? uni(-(1ll << 31) + 1, (1ll << 31) - 1) : uni(-3000000, 3000000);
+    if ((int64_t)qdev_wide((double)d) != (int64_t)qdev(d, 0, st)) ++bad;
+    // relative truncated quotients: k = 2 (smooth median) and k = R (mean)
+    const int64_t B = uni(-(1ll << 52), 1ll << 52), k = it % 3 == 0 ? 2 : uni(1, 1024);   // |k B| < 2^62
+    const int64_t S = uni(-(1ll << 40), 1ll << 40);
+    const int64_t want = (int64_t)idiv((i128)S + (i128)k * B, (i128)k, st) - B;
+    if (tdiv_rel(S, B, k) != want) ++bad;
+    if (it % 8 == 0) {
+      const int64_t v = it % 16 == 0 ? uni(0, 1ll << 31) : uni(0, (1ll << 43) - 1);
+      int st2 = ST_OK;
+      const int64_t ref = (int64_t)wsqrt(v, st2);
+      int64_t out = -1;
+      const bool ok = wsqrt_wide(v, out);
+      if (ok != (st2 == ST_OK) || (ok && out != ref)) ++bad;
+    }
+    CHECK(st == ST_OK);
+  }
+  CHECK(bad == 0);
+  for (int64_t v : {(int64_t)0, (int64_t)1, (int64_t)2, (int64_t)3, (int64_t)1000000, (int64_t)((1ll << 43) - 1), (int64_t)4000000000ll}) {
+    int st2 = ST_OK;
+    const int64_t ref = (int64_t)wsqrt(v, st2);
+    int64_t out = -1;
+    const bool ok = wsqrt_wide(v, out);
+    CHECK(ok == (st2 == ST_OK) && (!ok || out == ref));
+  }
+  // exact multiples and neighbours of 1e6 in d^2 + 500000
+  for (int64_t d : {(int64_t)1000, (int64_t)999, (int64_t)1001, (int64_t)2147483647, (int64_t)-2147483647, (int64_t)46340950}) {
+    int st = ST_OK;
+    CHECK((int64_t)qdev_wide((double)d) == (int64_t)qdev(d, 0, st));
+  }
+}
+
 int main(int argc, char** argv) {
   const int threads = argc > 1 ? std::atoi(argv[1]) : 8;
   golden_fixture();
   wsad_fast_paths();
   wsad_half_paths();
+  wsad_wide_paths();
   batch_vs_single(threads);
   governance_flow();
   io_roundtrip();

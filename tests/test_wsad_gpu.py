@@ -430,3 +430,24 @@ def test_wsad_kernel_unconstrained_domain_boundaries(dtype):
     comb = _run(vg, f, None, constrained=False, ms=MS)
     for k in OUTS:
         assert torch.equal(comb[k], cpu[k]), k
+
+
+@pytest.mark.parametrize("N,D,f", [(64, 256, 8), (100, 260, 10), (256, 300, 32), (50, 129, 5), (7, 70, 2)])
+def test_wsad_window_median_with_ties(N, D, f):
+    """The one-network window path (pass-2 smooth median read off the pass-1 window by ranking the removed
+    keys, consensus_wsad.hip) on tie-heavy columns: values from a 6-point grid, so the median, the window
+    and the removed keys share values.  Bit-identical to the i128 kernel on every round it takes."""
+    B = 16
+    g = torch.Generator().manual_seed(N + D + f)
+    grid = torch.tensor([100000, 350000, 480000, 500000, 520000, 900000])
+    v = grid[torch.randint(0, 6, (B, N, D), generator=g)]
+    v[:, : N // 3] = grid[2 + torch.randint(0, 3, (B, N // 3, D), generator=g)]   # a dense middle
+    fast = _run(v.to(DEV, torch.int32), f, {"SVOC_EXACT_WSAD_ONLY": "1", "SVOC_EXACT_WSAD_MIN_D": "1"})
+    ref = _run(v.to(DEV), f, {"SVOC_EXACT_I128": "1"})
+    took = fast["status"] == 0
+    assert took.sum() >= B // 2, fast["status"]
+    for k in OUTS:
+        assert torch.equal(fast[k][took], ref[k][took]), k
+    comb = _run(v.to(DEV, torch.int32), f, {"SVOC_EXACT_WSAD_MIN_D": "1"})
+    for k in OUTS:
+        assert torch.equal(comb[k], ref[k]), k
