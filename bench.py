@@ -126,6 +126,10 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
         eng.transactional = bool(args.transactional)
     dp = DataParallelConsensus(eng, rank=rank, world=world)
     eng.randomize(seed=1000 + (0 if dshard else rank))
+    if c.get("price_centre") is not None and mode == "exact":
+        # price-like unconstrained columns: the [0, 1] draws mapped onto centre +- spread real units
+        sp, ce = float(c.get("price_spread", 200.0)), float(c["price_centre"])
+        eng.values.copy_(((eng.values.double() - 500_000.0) * (2.0 * sp) + ce * 1e6).round().to(eng.values.dtype))
 
     # synthetic update stream resident in HBM: `pool` steps of updates, cycled
     U_per_inst = int(round(c["update_frac"] * c["N"]))

@@ -385,7 +385,9 @@ void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& 
   const char* force = std::getenv("SVOC_EXACT_I128");
   if (p.N >= 4 && !(force && force[0] == '1')) {
     p.win_h = mode == 0 && constrained && !legacy ? exact_win_h(p.N, p.n_failing) : 0;
-    stage = at::empty({(int64_t)p.B, 4 + 2 * p.win_h, (int64_t)p.D}, values.options().dtype(at::kInt));
+    // (c1, consensus, skewness, kurtosis; the window keys; unconstrained: the columns' base words)
+    stage = at::empty({(int64_t)p.B, 4 + 2 * p.win_h + (constrained ? 0 : 2), (int64_t)p.D},
+                      values.options().dtype(at::kInt));
     fallback = at::empty({(int64_t)p.B}, values.options().dtype(at::kByte));
     p.stage = stage.data_ptr<int32_t>();
     p.fallback = fallback.data_ptr<uint8_t>();

@@ -146,6 +146,16 @@ SVOC_HD int64_t tdiv_rel(int64_t S, int64_t B, int64_t k) {
   return q;
 }
 
+// tdiv_rel from q = trunc(S / k) computed elsewhere (e.g. trunc_div_d with a per-instance reciprocal):
+// `exact` = k divides S, `neg` = S < 0.  B + y > 0 (y = S / k, not integral) <=> B + q > 0 for y < 0, and
+// B + y < 0 <=> B + q < 0 for y > 0: no multiplication by k.
+SVOC_HD int64_t tdiv_rel_fix(int64_t q, bool exact, bool neg, int64_t B) {
+  if (exact) return q;
+  if (neg && B + q > 0) return q - 1;
+  if (!neg && B + q < 0) return q + 1;
+  return q;
+}
+
 // sqrt (math.cairo:271-292) for integral 0 <= v < 2^31: the same Newton steps and stop rule
 // (g == previous g, at most 50 iterations).  Returns false where the contract reverts: a zero
 // divisor (sqrt(1) -- g = 0 after the first halving).

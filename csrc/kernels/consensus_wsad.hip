@@ -100,6 +100,17 @@ SVOC_DEV void qtree_all(const uint32_t (&q)[64], int lane, uint64_t* acc, std::i
   ((acc[Is] += qtree<__builtin_ctz(P), Is, P>(q, lane)), ...);
 }
 
+// the same butterfly for the high words of 43-bit terms (unconstrained wide deviations): acc += sum << 32
+template <int P, int... Is>
+SVOC_DEV void qtree_hi_all(const uint32_t (&q)[64], int lane, uint64_t* acc, std::integer_sequence<int, Is...>) {
+  ((acc[Is] += (uint64_t)qtree<__builtin_ctz(P), Is, P>(q, lane) << 32), ...);
+}
+// low / high 32-bit words of an integral double 0 <= q < 2^43
+SVOC_DEV uint32_t q_hi(double q) { return (uint32_t)(q * 0x1p-32); }
+SVOC_DEV uint32_t q_lo(double q) { return (uint32_t)(q - (double)q_hi(q) * 0x1p32); }
+// |d| >= 2^25 for an int32 d (the narrow qdev forms' bound)
+SVOC_DEV bool wide25(uint32_t d) { return d + (1u << 25) >= (1u << 26); }
+
 // |x - c| < 2^25 for int32 x, c, in integer arithmetic (the unconstrained domain check; fp64 forms of it
 // held the 64 rows' conversions live and cost ~120 VGPRs): both within 2^30 of 0, so x - c cannot wrap
 SVOC_DEV bool near25(uint32_t x, uint32_t c) {
@@ -139,11 +150,15 @@ SVOC_DEV T group_sum(T v) {
 // MODE (launch.hpp ExactParams::mode): 0 whole round; 1 D-sharded first half (c1 + qr partials out);
 // 2 D-sharded second half (c1 and the all-reduced qr in).  Instances it cannot take in mode 1 / 2 go
 // to the i128 kernel's same mode through p.fallback, as in mode 0.
-// CONS = false: unconstrained rounds (contract.cairo:370-434): signed values, pass-2 consensus = the reliable
-// mean (no second network), reliabilities W - wsad_div(min(ms, sqrt(mean qr)), ms).  Domain (else the
-// i128 kernel): values within 2^30 of 0 (1073.7 in real units) and within 2^25 (33.55) of their column's
-// smooth median and of its reliable mean -- the bound under which the fp64 forms of qdev / wsad_div are
-// exact (wsad_fast.hpp); the qr butterfly then sums 64-bit partials.
+// CONS = false: unconstrained rounds (contract.cairo:370-434): signed int64 values, pass-2 consensus = the
+// reliable mean (no second network), reliabilities W - wsad_div(min(ms, sqrt(mean qr)), ms).  Every column is
+// taken relative to its row-0 value B (keys, deviations and z-scores are translation invariant; the two
+// truncated quotients -- the smooth median and the mean -- are shifted back exactly by tdiv_rel, and c1 /
+// consensus are committed as B + the relative value).  Domain (else the i128 kernel): |B| < 2^52 and every
+// value within 2^30 of B (1,073 real units: price-like columns such as 60,000 +- 200 stay here; deviations
+// then stay below 2^31, the wide forms' bound, and their 43-bit quotients' high words below 2^11).  Deviations
+// below 2^25 take the fast half-offset forms; a wave with any larger one takes the wide forms (double-double
+// qdev with 43-bit quotients summed as two 32-bit butterflies, the int64 Newton sqrt) for that slab.
 // WINH > 0 (whole constrained rounds, launch_wsad_c): ONE median network per column.  Pass 1 keeps the
 // 2 WINH keys around the median (window_group, sortnet.hpp) in the staging buffer; the pass-2 smooth
 // median over the reliable rows is then read off that window by ranking the f removed rows' keys
@@ -154,7 +169,9 @@ SVOC_DEV T group_sum(T v) {
 // need g at positions R/2 - 1 .. R/2 + f, inside the window when WINH >= max(a + 1, f - a + 1),
 // a = N/2 - R/2.  The second network over the reliable rows (~30 % of the kernel's VALU) goes away.
 template <int NSEG, int WAVES, bool V32, int MODE, bool CONS, int WINH = 0>
-__global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams p) {
+// (unconstrained int64, 4-lane groups: the wide pass-1 branch lands 2 VGPRs past 256 without the hint)
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((!CONS && !V32 && NSEG == 4) ? 2 : 1)))
+void consensus_wsad_kernel(ExactParams p) {
   static_assert(WINH == 0 || (MODE == 0 && CONS), "the window path is for whole constrained rounds");
   constexpr int P = 64 / NSEG;      // columns per wave
   constexpr int NPAD = 64 * NSEG;   // padded oracle rows
@@ -193,8 +210,14 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   const int rowb = D * ESZ;
   const __amdgpu_buffer_rsrc_t rs =
       instance_rsrc((const unsigned char*)p.values + (int64_t)b * N * rowb, (uint32_t)(N * rowb));
-  // [4 + 2 WINH][D]: c1, consensus, skewness, kurtosis, then the window keys (WINH > 0)
-  int32_t* const stg = p.stage + (int64_t)b * (4 + 2 * WINH) * D;
+  // [SROWS][D]: c1, consensus, skewness, kurtosis, then the window keys (WINH > 0) or the columns' base
+  // values (unconstrained: low / high words)
+  constexpr int SROWS = 4 + 2 * WINH + (CONS ? 0 : 2);
+  int32_t* const stg = p.stage + (int64_t)b * SROWS * D;
+  auto stage_base = [&](const int32_t* sg, int c) __attribute__((always_inline)) -> int64_t {
+    if constexpr (CONS) return 0;
+    else return (int64_t)(((uint64_t)(uint32_t)sg[5 * D + c] << 32) | (uint32_t)sg[4 * D + c]);
+  };
   const int nslab = (D + W - 1) / W;
   const int lo1 = (NPAD - N + 1) >> 1;   // pass-1 sentinel split (rows >= N): -inf first, then +inf
   const int nv = N - seg * 64;           // this lane's rows < nv are real
@@ -206,6 +229,15 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   uint64_t acc[KEEP];
 #pragma unroll
   for (int k = 0; k < KEEP; ++k) acc[k] = 0;
+  // unconstrained: the base B of column c = its row-0 value (low / high words; int32 storage: sign-extended)
+  auto base_of = [&](int c, int ord) __attribute__((always_inline)) -> u32x2_t {
+    if constexpr (V32) {
+      const uint32_t l = bload(rs, after(c * 4, ord), 0);
+      return u32x2_t{l, (uint32_t)((int32_t)l >> 31)};
+    } else {
+      return __builtin_amdgcn_raw_buffer_load_b64(rs, after(c * 8, ord), 0, 0);
+    }
+  };
   // a stored low word as a number: [0, 1e6] (constrained) or an int32 (unconstrained)
   auto xv = [](uint32_t x) __attribute__((always_inline)) { return CONS ? (double)x : (double)(int32_t)x; };
   constexpr uint32_t kSign = CONS ? 0u : 0x80000000u;   // order-preserving key of an int32
@@ -217,15 +249,23 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
     const bool vc = col < D;
     const int vo = seg_off + (vc ? col : 0) * ESZ;
     uint32_t c1;
+    // unconstrained: the column's base B = its row-0 value (every lane of the group loads it)
+    uint32_t Bl = 0u, Bh = 0u;
+    if constexpr (!CONS) Bl = base_of(vc ? col : 0, s)[0];   // (the high word: after the network)
     {
       uint32_t r[64];
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         // (the low word only: int64 rows get their high words checked below, 8 rows at a time -- loaded
         // here they held 64 more VGPRs and cost the int64 kernels their second wave per SIMD)
-        const uint32_t x = bload(rs, vo, i * rowb);
+        const uint32_t x = bload(rs, vo, i * rowb) - Bl;   // (unconstrained: relative to B)
         const bool real = i < nv;
         if constexpr (CONS) badv |= (vc && real && x > kWsadMax) ? 1u : 0u;   // outside [0, 1e6]
+        if constexpr (!CONS && V32) {   // int32 storage: x - B without int32 overflow and within 2^30
+          const uint32_t xw = x + Bl;   // (the stored word)
+          const bool ovf = (((xw ^ Bl) & (xw ^ x)) >> 31) != 0u;
+          badv |= (vc && real && (ovf || x + (1u << 30) >= (1u << 31))) ? 1u : 0u;
+        }
         r[i] = (real ? x ^ kSign : (i < nl ? 0u : ~0u)) ^ pol;
       }
       uint32_t lo, hi;
@@ -254,37 +294,77 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       }
       if constexpr (CONS) {
         c1 = (lo + hi) >> 1;           // idiv_pos64(a + b, 2) of non-negative values
-      } else {                         // I128Div(a + b, 2): truncation toward zero
-        const int64_t sum = (int64_t)(int32_t)(lo ^ kSign) + (int64_t)(int32_t)(hi ^ kSign);
-        c1 = (uint32_t)(int32_t)(sum / 2);
+      } else {                         // I128Div(a + b, 2) of the absolute values, relative to B
+        const int32_t sum = (int32_t)(lo ^ kSign) + (int32_t)(hi ^ kSign);   // (|sum| < 2^30)
+        const u32x2_t bv = base_of(vc ? col : 0, (int)lo);
+        Bh = bv[1];
+        badv |= (vc && Bh + (1u << 20) >= (1u << 21)) ? 1u : 0u;   // |B| < 2^52
+        c1 = (uint32_t)(int32_t)tdiv_rel_fix(sum / 2, (sum & 1) == 0, sum < 0, (int64_t)(((uint64_t)Bh << 32) | Bl));
       }
     }
-    if (seg == 0 && vc) stg[col] = (int32_t)c1;
+    if (seg == 0 && vc) {
+      stg[col] = (int32_t)c1;
+      if constexpr (!CONS) {
+        stg[4 * D + col] = (int32_t)Bl;
+        stg[5 * D + col] = (int32_t)Bh;
+      }
+    }
     __builtin_amdgcn_sched_barrier(0);
     // quadratic risk (math.cairo:225-238): this column's qdev of every row, summed over the columns
     uint32_t q[64];
     const double cd = xv(c1);
-    if constexpr (BATCH1) {
+    if constexpr (!CONS) {
+      // d = x - c1 relative (|d| < 2^30 in the domain); the narrow form unless some |d| >= 2^25 in the wave
+      load_lo(rs, after(vo, c1), rowb, q);
+      bool wd = false;
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        q[i] = q[i] - Bl - c1;
+        wd = wd || (vc && i < nv && wide25(q[i]));
+      }
+      if (__ballot(wd) == 0) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
+          q[i] = (vc && i < nv) ? qdev_u((double)(int32_t)q[i]) : 0u;
+        }
+        qtree64_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
+      } else {
+        // 43-bit quotients: the low words through the 64-bit butterfly, then (recomputed from a second read)
+        // the high words through the 32-bit one, shifted
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          if ((i & 3) == 0) __builtin_amdgcn_sched_barrier(0);   // (4 rows of double-double temporaries)
+          q[i] = (vc && i < nv) ? q_lo(qdev_wide((double)(int32_t)q[i])) : 0u;
+        }
+        qtree64_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
+        __builtin_amdgcn_sched_barrier(0);   // (the re-read after the whole butterfly, not beside it)
+        load_lo(rs, after(vo, acc[KEEP - 1]), rowb, q);
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          if ((i & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+          q[i] = (vc && i < nv) ? q_hi(qdev_wide((double)(int32_t)(q[i] - Bl - c1))) : 0u;
+        }
+        qtree_hi_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
+      }
+    } else if constexpr (BATCH1) {
       load_lo(rs, after(vo, c1), rowb, q);
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bound the fp64 temporaries in flight
-        if (!CONS) badv |= (vc && i < nv && !near25(q[i], c1)) ? 1u : 0u;   // |x - c1| < 2^25
         q[i] = (vc && i < nv) ? qdev_u(xv(q[i]) - cd) : 0u;
       }
     } else {
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         const uint32_t x = bload(rs, vo, i * rowb);   // (low word; int64 high words are checked below)
-        if (!CONS) badv |= (vc && i < nv && !near25(x, c1)) ? 1u : 0u;
         q[i] = (vc && i < nv) ? qdev_u(xv(x) - cd) : 0u;
       }
     }
     if constexpr (CONS) qtree_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
-    else qtree64_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
     if constexpr (!V32) {
-      // int64 storage: the high words, 8 rows in flight -- 0 (constrained: [0, 1e6]) or the sign extension
-      // of the low word (unconstrained: an int32)
+      // int64 storage: the high words, 8 rows in flight -- 0 (constrained: [0, 1e6]); unconstrained: x - B
+      // is the sign extension of its low word and within 2^30
 #pragma nounroll
       for (int g = 0; g < 64; g += 8) {
         uint32_t hw[8], lw[8];
@@ -294,8 +374,15 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
           lw[k] = CONS ? 0u : bload(rs, vo, (g + k) * rowb);
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          badv |= (vc && g + k < nv && hw[k] != (CONS ? 0u : (uint32_t)((int32_t)lw[k] >> 31))) ? 1u : 0u;
+        for (int k = 0; k < 8; ++k) {
+          if constexpr (CONS) {
+            badv |= (vc && g + k < nv && hw[k] != 0u) ? 1u : 0u;
+          } else {
+            const uint32_t rl = lw[k] - Bl, rh = hw[k] - Bh - (lw[k] < Bl ? 1u : 0u);
+            const bool ok = rh == (uint32_t)((int32_t)rl >> 31) && rl + (1u << 30) < (1u << 31);
+            badv |= (vc && g + k < nv && !ok) ? 1u : 0u;
+          }
+        }
       }
     }
   }
@@ -326,7 +413,7 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       if (tid == 0) p.fallback[b] = 1;
       return;
     }
-    for (int c = tid; c < D; c += NT) p.c1[(int64_t)b * D + c] = stg[c];
+    for (int c = tid; c < D; c += NT) p.c1[(int64_t)b * D + c] = stg[c] + stage_base(stg, c);
     for (int t = tid; t < N; t += NT) p.qr[(int64_t)b * N + t] = (int64_t)qr_lds[t];
     if (tid == 0) {
       p.status[b] = ST_OK;
@@ -527,14 +614,22 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       }
       sx = group_sum<NSEG, P>(sx);
       mu = floor_div_d((double)sx, Rd, invR);
-    } else {   // signed sum (|sum| < 2^39: exact), I128Div toward zero; the mean is the consensus
+    } else {   // signed sum of the relative values (|sum| < 2^38: exact), I128Div of the absolute sum toward
+               // zero shifted back (tdiv_rel); the mean is the consensus.  The column is loaded once (no network
+               // in this loop) and kept for the variance and z-power loops.
+      const u32x2_t bv = base_of(vc ? col : 0, (int)mm);
       load_lo(rs, after(vo, mm), rowb, xr);
+#pragma unroll
+      for (int i = 0; i < 64; ++i) xr[i] -= bv[0];
       double sxd = 0.0;
 #pragma unroll
       for (int i = 0; i < 64; ++i) sxd += bit_mask(mm, i) ? xv(xr[i]) : 0.0;
       sxd = group_sum<NSEG, P>(sxd);
-      mu = trunc_div_d(sxd, Rd, invR);
-      cons = (uint32_t)(int32_t)mu;
+      const double qd = trunc_div_d(sxd, Rd, invR);
+      const int64_t mr = tdiv_rel_fix((int64_t)qd, fma(-qd, Rd, sxd) == 0.0, sxd < 0.0,
+                                      (int64_t)(((uint64_t)bv[1] << 32) | bv[0]));
+      mu = (double)mr;
+      cons = (uint32_t)(int32_t)mr;
     }
     // population variance (math.cairo:208-222): mean of qdev(x, mu) over the reliable rows
     double var;
@@ -556,26 +651,48 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       }
       sv = group_sum<NSEG, P>(sv);
       var = floor_div_d((double)sv, Rd, invR);
-    } else {   // fp64 sums (exact: every term < 2^31 under the |x - mu| < 2^25 bound checked here)
-      double svd = 0.0;
-      if constexpr (BATCH) load_lo(rs, after(vo, mu), rowb, xr);
-      const uint32_t mui = (uint32_t)(int32_t)mu;   // (an int32: the mean of int32 values)
+    } else {   // fp64 sums of the relative deviations (exact: terms < 2^43, R <= 256), narrow or wide forms
+      const uint32_t mui = (uint32_t)(int32_t)mu;
+      // (each loop takes its own opaque copy of the row mask: 64 shared per-row masks, or shared
+      // conversions, would stay live across the branch -- one wave per SIMD less)
+      bool wd = false;
+      {
+        uint64_t m0 = mm;
+        asm volatile("" : "+v"(m0));
 #pragma unroll
-      for (int i = 0; i < 64; ++i) {
-        if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
-        const uint32_t xw = BATCH ? xr[i] : bload(rs, vo, i * rowb);
-        const bool mk = bit_mask(mm, i) != 0u;
-        if (vc && mk && !near25(xw, mui)) bad = true;
-        svd += mk ? qdev_h(xv(xw) - mu) : 0.0;
+        for (int i = 0; i < 64; ++i) wd = wd || (vc && bit_mask(m0, i) != 0u && wide25(xr[i] - mui));
+      }
+      double svd = 0.0;
+      uint64_t m1 = mm;
+      asm volatile("" : "+v"(m1));
+      if (__ballot(wd) == 0) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
+          svd += bit_mask(m1, i) ? qdev_h((double)(int32_t)(xr[i] - mui)) : 0.0;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
+          svd += bit_mask(m1, i) ? qdev_wide((double)(int32_t)(xr[i] - mui)) : 0.0;
+        }
       }
       svd = group_sum<NSEG, P>(svd);
       var = floor_div_d(svd, Rd, invR);
-      if (vc && !(var < 2147483648.0)) bad = true;   // wsqrt_d's bound
+      if (vc && !(var < 8796093022208.0)) bad = true;   // wsqrt_wide's bound (2^43)
       if (bad) var = 0.0;
     }
     // var 0 (sqrt 0 -> wsad_div by zero) and var 1 (sqrt(1) divides by zero) revert the round
     double sd = 1.0;
-    const bool ok_sd = var >= 2.0 && wsqrt_d(var, sd);
+    bool ok_sd;
+    if (CONS || var < 2147483648.0) {
+      ok_sd = var >= 2.0 && wsqrt_d(var, sd);
+    } else {   // (unconstrained, wide columns)
+      int64_t sdi = 1;
+      ok_sd = wsqrt_wide((int64_t)var, sdi);
+      sd = (double)sdi;
+    }
     if (vc && !ok_sd) dz = true;   // sqrt(0) -> wsad_div by 0, sqrt(1) divides by 0: DIV_BY_ZERO
     // z = wsad_div(x - mu, sd) = I128Div((x - mu) 1e6 + floor(sd / 2), sd): A = x 1e6 + C0 (exact integers
     // below 2^51), then the half-offset forms of wsad_fast.hpp -- no remainder tests in the row loop
@@ -594,8 +711,14 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
       s3 += wmul_h(z2, z, z < 0.0);
       s4 += wmul_pos_h(z2, z2);
     };
-    if constexpr (BATCH || (WINH > 0 && BATCH1)) {
-      if constexpr (WINH == 0) load_lo(rs, after(vo, sd), rowb, xr);
+    if constexpr (BATCH || (WINH > 0 && BATCH1) || !CONS) {
+      if constexpr (WINH == 0 && CONS) load_lo(rs, after(vo, sd), rowb, xr);
+      if constexpr (!CONS) {   // (re-read: the column is not kept across the square root)
+        const uint32_t bl = base_of(vc ? col : 0, (int)sd)[0];
+        load_lo(rs, after(vo, sd), rowb, xr);
+#pragma unroll
+        for (int i = 0; i < 64; ++i) xr[i] -= bl;
+      }
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bound the fp64 temporaries in flight
@@ -615,9 +738,10 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
 #pragma nounroll
       for (int g = 0; g < 64; g += 8) {   // 8 rows per step: their loads in flight together
         uint32_t xg[8];
+        const uint32_t bl = CONS ? 0u : base_of(vc ? col : 0, g)[0];   // (unconstrained: the base)
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          xg[k] = bload(rs, vo, (g + k) * rowb);
+          xg[k] = bload(rs, vo, (g + k) * rowb) - bl;
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -669,8 +793,9 @@ __global__ __launch_bounds__(WAVES * 64) void consensus_wsad_kernel(ExactParams 
   // ------------------------------------------------------------ commit (a successful round)
   const int64_t ob = (int64_t)b * D;
   for (int c = tid; c < D; c += NT) {
-    if (MODE == 0 && p.c1) p.c1[ob + c] = stg[c];   // (mode 2: c1 is the input, unchanged)
-    p.consensus[ob + c] = stg[D + c];
+    const int64_t bs = stage_base(stg, c);   // (unconstrained: the column's base; else 0)
+    if (MODE == 0 && p.c1) p.c1[ob + c] = stg[c] + bs;   // (mode 2: c1 is the input, unchanged)
+    p.consensus[ob + c] = stg[D + c] + bs;
     p.skew[ob + c] = stg[2 * D + c];
     p.kurt[ob + c] = stg[3 * D + c];
   }

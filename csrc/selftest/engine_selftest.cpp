@@ -265,6 +265,7 @@ static void wsad_wide_paths() {
     const int64_t S = uni(-(1ll << 40), 1ll << 40);
     const int64_t want = (int64_t)idiv((i128)S + (i128)k * B, (i128)k, st) - B;
     if (tdiv_rel(S, B, k) != want) ++bad;
+    if (tdiv_rel_fix(S / k, S % k == 0, S < 0, B) != want) ++bad;
     if (it % 8 == 0) {
       const int64_t v = it % 16 == 0 ? uni(0, 1ll << 31) : uni(0, (1ll << 43) - 1);
       int st2 = ST_OK;
