@@ -274,7 +274,22 @@ void consensus_wsad_kernel(ExactParams p) {
         // staged at rows 4 .. 4 + 2 WINH of this instance's stage (true keys = the values)
         constexpr int WN = NSEG == 1 ? 2 * WINH : WINH;
         uint32_t w[WN];
-        window_group<NSEG, P, WINH>(r, seg, lane, w, lo, hi);
+        if constexpr (NSEG == 4 && WINH == 17) {
+          // pruned network (sortnet.hpp window_group_pruned: only every lane's middle 32 keys enter the cross-lane
+          // merges) with its exactness check; a wave with any failing column reruns the full network from the rows
+          bool ok;
+          window_group_pruned<P, WINH>(r, seg, lane, w, lo, hi, ok);
+          if (__ballot(!ok) != 0) {
+#pragma unroll
+            for (int i = 0; i < 64; ++i) {
+              const uint32_t x = bload(rs, after(vo, lo), i * rowb) - Bl;
+              r[i] = (i < nv ? x ^ kSign : (i < nl ? 0u : ~0u)) ^ pol;
+            }
+            window_group<NSEG, P, WINH>(r, seg, lane, w, lo, hi);
+          }
+        } else {
+          window_group<NSEG, P, WINH>(r, seg, lane, w, lo, hi);
+        }
         constexpr int SLO = NSEG == 4 ? 1 : 0;   // the lane holding the lower part (the upper: SLO + 1)
         if (vc) {
 #pragma unroll

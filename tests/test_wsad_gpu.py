@@ -506,3 +506,26 @@ def test_wsad_kernel_unconstrained_int64_extremes():
     comb = _run(vg, f, None, constrained=False, ms=ms)
     for k in OUTS:
         assert torch.equal(comb[k], cpu[k]), k
+
+
+@pytest.mark.parametrize("N", [256, 200])
+def test_wsad_pruned_window_fallback(N):
+    """N in (128, 256], f <= 32: pass 1 runs the pruned window network (only each lane's middle 32 keys enter
+    the cross-lane merges) and reruns the full network for a wave whose check fails.  Adversarial columns --
+    one lane group's 64 rows holding the column's lowest values, or its highest -- force the rerun; every
+    round stays bit-identical to the i128 kernel."""
+    B, D, f = 6, 160, 32
+    v = _wsad(B, N, D, f, seed=N + 1)
+    g = torch.Generator().manual_seed(9)
+    for b in range(B):
+        for c in range(0, D, 7):                      # every 7th column: sorted ascending down the rows
+            v[b, :, c] = torch.sort(v[b, :, c]).values
+        for c in range(3, D, 11):                     # every 11th: the first 64 rows at the top of the column
+            col = torch.sort(v[b, :, c], descending=True).values
+            v[b, :, c] = col[torch.randperm(N, generator=g)] if b % 2 else col
+    fast = _run(v.to(DEV, torch.int32), f, {"SVOC_EXACT_WSAD_ONLY": "1", "SVOC_EXACT_WSAD_MIN_D": "1"})
+    ref = _run(v.to(DEV), f, {"SVOC_EXACT_I128": "1"})
+    took = fast["status"] == 0
+    assert took.sum() >= B - 1, fast["status"]
+    for k in OUTS:
+        assert torch.equal(fast[k][took], ref[k][took]), k
