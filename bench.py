@@ -166,6 +166,8 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
         elem = 8 if mode == "exact" else eng.values.element_size()
         per_batch = B * U_per_inst * (D_local * elem + 16)
         pool = max(2, min(args.steps, int(96e9 // max(1, per_batch)))) if dev.type == "cuda" else 2
+        if args.stream_pool > 0:   # (A/B: a fixed pool, e.g. round 4's period-2 stream)
+            pool = args.stream_pool
         extra["stream_pool"] = pool
         stream = SyntheticUpdateStream(B, c["N"], D_local, U_per_inst, c["f"], pool=pool, device=dev,
                                        seed=(0 if dshard else rank),
@@ -359,6 +361,8 @@ def main():
                     help="strong scaling: every rank holds a column slice of ALL instances (D-sharding, one "
                          "[B, N] qr all-reduce per round) instead of its own instances (DP, default)")
     ap.add_argument("--backend", default=None, help="torch.distributed backend (default: nccl = RCCL on GPU)")
+    ap.add_argument("--stream-pool", type=int, default=0,
+                    help="streaming configs: distinct update batches cycled (0 = one per timed step, within 96 GB)")
     ap.add_argument("--log", default=None, help="append the result record to this JSON-lines file")
     ap.add_argument("--kernel-table", type=int, default=0, help="profile N extra steps (torch.profiler) "
                     "after the timed region and add the per-kernel table to the log record")
