@@ -129,7 +129,7 @@ struct ExactParams {
 // smallest of {5, 17} covering ranks R/2 - 1 .. R/2 + f of the full column, i.e. >= max(a + 1, f - a + 1)
 // with a = N/2 - R/2; 0 = no window (two median networks).
 inline int exact_win_h(int N, int f) {
-  if (N < 4 || f < 0 || f > N - 2) return 0;
+  if (N < 4 || N > 256 || f < 0 || f > N - 2) return 0;   // (N > 256: the wide lane groups, two networks)
   const int R = N - f, a = N / 2 - R / 2;
   const int need = a + 1 > f - a + 1 ? a + 1 : f - a + 1;
   // (N <= 64 with 17: the one-lane-group kernel goes past 256 VGPRs, one wave per SIMD -- two networks win)

@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
 #include <utility>
 
 #include "svoc/bufload.hpp"
@@ -139,6 +140,97 @@ SVOC_DEV void qtree64_all(const uint32_t (&q)[64], int lane, uint64_t* acc, std:
   ((acc[Is] += qtree64<__builtin_ctz(P), Is, P>(q, lane)), ...);
 }
 
+// Inclusive prefix sum of one value per thread over a 256-thread workgroup (wave scans + the wave totals);
+// `wsum` is 4 words of LDS.  Every thread returns its inclusive prefix; `total` gets the sum.
+SVOC_DEV uint32_t block_scan_256(uint32_t v, uint32_t* wsum, int tid, uint32_t& total) {
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = (uint32_t)__shfl_up((int)v, o);
+    if (lane >= o) v += u;
+  }
+  if (lane == 63) wsum[wave] = v;
+  __syncthreads();
+  uint32_t before = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) before += w < wave ? wsum[w] : 0u;
+  total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  __syncthreads();
+  return v + before;
+}
+
+// Rank mask for the wide lane groups (N up to 4096; sort.cairo:9-103 + contract.cairo:345-363): instead of
+// ranking every row against every other (N^2 / 256 LDS reads per thread), T = the (R-1)-th smallest qr is found
+// by an 8-pass radix select (one 256-bin LDS histogram per byte, thread = bin), rows below T are reliable and
+// the rows AT T by index descending (the merge sort's tie rule) until R rows are.  Thread tid owns the
+// contiguous rows [tid RPT, tid RPT + RPT).  256 threads.
+template <int NPAD>
+SVOC_DEV void rank_mask_select(const uint64_t* qr, int N, int R, uint64_t* relmask, uint32_t* hist, uint32_t* wsum,
+                               uint32_t* sel, int tid) {
+  constexpr int RPT = NPAD / 256;
+  static_assert(RPT >= 1 && 64 % RPT == 0, "rows per thread within one mask word");
+  for (int w = tid; w < NPAD / 64; w += 256) relmask[w] = 0ull;
+  uint64_t prefix = 0ull, pmask = 0ull;
+  uint32_t k = (uint32_t)(R - 1);   // target rank among the rows matching the prefix
+  for (int byte = 7; byte >= 0; --byte) {
+    hist[tid] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int t = tid * RPT + i;
+      if (t < N) {
+        const uint64_t q = qr[t];
+        if ((q & pmask) == prefix) atomicAdd(&hist[(uint32_t)(q >> (8 * byte)) & 255u], 1u);
+      }
+    }
+    __syncthreads();
+    const uint32_t c = hist[tid];
+    uint32_t tot;
+    const uint32_t incl = block_scan_256(c, wsum, tid, tot);
+    if (incl - c <= k && k < incl) {   // this bin holds the target
+      sel[0] = (uint32_t)tid;
+      sel[1] = k - (incl - c);
+    }
+    __syncthreads();
+    prefix |= (uint64_t)sel[0] << (8 * byte);
+    pmask |= 0xffull << (8 * byte);
+    k = sel[1];
+    __syncthreads();
+  }
+  const uint64_t T = prefix;
+  uint32_t lt = 0, ties = 0;
+#pragma unroll
+  for (int i = 0; i < RPT; ++i) {
+    const int t = tid * RPT + i;
+    if (t < N) {
+      const uint64_t q = qr[t];
+      lt += q < T ? 1u : 0u;
+      ties += q == T ? 1u : 0u;
+    }
+  }
+  uint32_t lt_tot, tie_tot;
+  (void)block_scan_256(lt, wsum, tid, lt_tot);
+  const uint32_t tie_incl = block_scan_256(ties, wsum, tid, tie_tot);
+  const uint32_t need = (uint32_t)R - lt_tot;              // tie rows taken, largest indices first
+  uint32_t above = tie_tot - tie_incl;                     // tie rows after this thread's block
+  uint64_t bits = 0ull;
+#pragma unroll
+  for (int i = RPT - 1; i >= 0; --i) {
+    const int t = tid * RPT + i;
+    if (t < N) {
+      const uint64_t q = qr[t];
+      bool rel = q < T;
+      if (q == T) {
+        rel = above < need;
+        ++above;
+      }
+      if (rel) bits |= 1ull << ((tid * RPT + i) & 63);
+    }
+  }
+  if (bits) atomicOr((unsigned long long*)&relmask[(tid * RPT) >> 6], (unsigned long long)bits);
+  __syncthreads();
+}
+
 // sum over the NSEG lanes of a column group (lanes lane ^ t*P)
 template <int NSEG, int P, class T>
 SVOC_DEV T group_sum(T v) {
@@ -178,15 +270,22 @@ void consensus_wsad_kernel(ExactParams p) {
   constexpr int W = WAVES * P;      // columns per tile
   constexpr int NT = WAVES * 64;
   constexpr int KEEP = 64 / P;      // qr rows a lane holds after the butterfly
+  // WIDE (NSEG 8 .. 64: N up to 512 .. 4096, whole constrained rounds): full cross-lane median networks
+  // (median_group_wide), the per-oracle qr summed by LDS atomics instead of the transposing butterfly (a lane
+  // holds 64 rows of one column: the butterfly would leave it 64 / P row sums -- 128 VGPRs at P = 1), and
+  // 64-bit / fp64 column sums (R values up to 1e6 pass 2^32)
+  constexpr bool WIDE = NSEG > 4;
+  static_assert(!WIDE || (CONS && MODE == 0 && WINH == 0), "wide groups: whole constrained rounds, two networks");
+  constexpr int MW = NSEG > 4 ? NSEG : 4;   // 64-bit row-mask words
   constexpr int ESZ = V32 ? 4 : 8;
   // re-reads issued as 64-load batches ordered after the value they need (load_lo / after): +37% at
   // 256 x 4096; the N <= 64 kernel batches the qr and mean re-reads only (+27% at 64 x 1024): batching
   // the fp64 variance / z-power re-reads too costs it a wave per SIMD (-18%)
   constexpr bool BATCH = NSEG >= 2;
   constexpr bool BATCH1 = BATCH || SVOC_WSAD_BATCH_QR;   // the qr and mean re-reads only (no fp64 temporaries)
-  __shared__ uint64_t qr_part[WAVES * NPAD];
+  __shared__ uint64_t qr_part[WIDE ? 1 : WAVES * NPAD];
   __shared__ uint64_t qr_lds[NPAD];
-  __shared__ uint64_t relmask[4], lowmask[4];
+  __shared__ uint64_t relmask[MW], lowmask[MW];
   __shared__ int64_t rels[2];
   __shared__ int flag;
   __shared__ int early_st;   // a revert decided before the moments (its final status)
@@ -226,9 +325,13 @@ void consensus_wsad_kernel(ExactParams p) {
   const uint32_t pol = group_polarity<NSEG>(seg);
   uint32_t badv = 0;                     // a value outside [0, 1e6]
 
-  uint64_t acc[KEEP];
+  uint64_t acc[WIDE ? 1 : KEEP];
 #pragma unroll
-  for (int k = 0; k < KEEP; ++k) acc[k] = 0;
+  for (int k = 0; k < (WIDE ? 1 : KEEP); ++k) acc[k] = 0;
+  if constexpr (WIDE) {
+    for (int t = tid; t < NPAD; t += NT) qr_lds[t] = 0;
+    __syncthreads();
+  }
   // unconstrained: the base B of column c = its row-0 value (low / high words; int32 storage: sign-extended)
   auto base_of = [&](int c, int ord) __attribute__((always_inline)) -> u32x2_t {
     if constexpr (V32) {
@@ -304,6 +407,8 @@ void consensus_wsad_kernel(ExactParams p) {
             }
           }
         }
+      } else if constexpr (WIDE) {
+        median_group_wide<NSEG, P>(r, seg, lane, lo, hi);
       } else {
         median_group<NSEG>(r, lo, hi);   // smooth median: ranks N/2 - 1, N/2 (math.cairo:113-126)
       }
@@ -376,7 +481,15 @@ void consensus_wsad_kernel(ExactParams p) {
         q[i] = (vc && i < nv) ? qdev_u(xv(x) - cd) : 0u;
       }
     }
-    if constexpr (CONS) qtree_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
+    if constexpr (WIDE) {
+      // each lane's 64 rows (one column) into the per-oracle sums: LDS atomics (rows of the same segment meet
+      // from the P columns of a wave and from the other waves)
+#pragma unroll
+      for (int i = 0; i < 64; ++i)
+        if (q[i]) atomicAdd((unsigned long long*)&qr_lds[seg * 64 + i], (unsigned long long)q[i]);
+    } else if constexpr (CONS) {
+      qtree_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
+    }
     if constexpr (!V32) {
       // int64 storage: the high words, 8 rows in flight -- 0 (constrained: [0, 1e6]); unconstrained: x - B
       // is the sign extension of its low word and within 2^30
@@ -401,7 +514,7 @@ void consensus_wsad_kernel(ExactParams p) {
       }
     }
   }
-  {
+  if constexpr (!WIDE) {
     int base = 0;
 #pragma unroll
     for (int h = 32, msk = P / 2; msk >= 1; h >>= 1, msk >>= 1) base += (lane & msk) ? h : 0;
@@ -409,7 +522,7 @@ void consensus_wsad_kernel(ExactParams p) {
     for (int k = 0; k < KEEP; ++k) qr_part[wave * NPAD + seg * 64 + base + k] = acc[k];
   }
   __syncthreads();
-  for (int t = tid; t < NPAD; t += NT) {
+  for (int t = tid; t < (WIDE ? 0 : NPAD); t += NT) {
     uint64_t v = 0;
     if (MODE == 2) {   // the all-reduced qr (int64; a negative total cannot come from this domain)
       const int64_t q = t < N ? p.qr[(int64_t)b * N + t] : 0;
@@ -440,7 +553,14 @@ void consensus_wsad_kernel(ExactParams p) {
   // ------------------------------------------------------------ rank mask (contract.cairo:345-363)
   const int f = p.n_failing;
   const int R = N - f;
-  for (int base = 0; base < NPAD; base += NT) {
+  if constexpr (WIDE) {
+    __shared__ uint32_t rk_hist[256], rk_wsum[4], rk_sel[2];
+    static_assert(NT == 256, "rank_mask_select: 256 threads");
+    if (R >= 1 && R <= N) rank_mask_select<NPAD>(qr_lds, N, R, relmask, rk_hist, rk_wsum, rk_sel, tid);
+    else
+      for (int w = tid; w < MW; w += NT) relmask[w] = 0ull;   // (no reliable row: the stage checks revert)
+  }
+  for (int base = 0; base < (WIDE ? 0 : NPAD); base += NT) {
     const int t = base + tid;
     bool rel = false;
     if (t < N) {
@@ -453,7 +573,7 @@ void consensus_wsad_kernel(ExactParams p) {
       rel = rank < R;
     }
     const uint64_t bal = __ballot(rel);
-    if (lane == 0 && (t >> 6) < 4) relmask[t >> 6] = bal;
+    if (lane == 0 && (t >> 6) < MW) relmask[t >> 6] = bal;
   }
   __syncthreads();
   if (tid == 0) {
@@ -494,7 +614,7 @@ void consensus_wsad_kernel(ExactParams p) {
     if (fb) flag = 1;
     // pass-2 sentinel split: the first (NPAD - R + 1) / 2 non-reliable rows (row order) become -inf
     int need = (NPAD - R + 1) >> 1;
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < MW; ++w) {
       uint64_t nr = w < NSEG ? ~relmask[w] : 0ull, lm = 0ull;
       while (need > 0 && nr) {
         const uint64_t bit = nr & (0ull - nr);
@@ -598,7 +718,8 @@ void consensus_wsad_kernel(ExactParams p) {
         }
       }
       uint32_t lo, hi;
-      median_group<NSEG>(r, lo, hi);
+      if constexpr (WIDE) median_group_wide<NSEG, P>(r, seg, lane, lo, hi);
+      else median_group<NSEG>(r, lo, hi);
       cons = (lo + hi) >> 1;
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -615,8 +736,9 @@ void consensus_wsad_kernel(ExactParams p) {
     // mean (math.cairo:240-254): idiv(sum, R) of non-negative values
     uint32_t xr[64];
     double mu;
+    using SumT = std::conditional_t<WIDE, uint64_t, uint32_t>;   // (R values of up to 1e6)
     if constexpr (CONS) {
-      uint32_t sx = 0;
+      SumT sx = 0;
       if constexpr (BATCH1) {
         // (window path: no network in this loop, so the column is loaded once and kept for the mean,
         // variance and z-power loops; otherwise re-read per statistic)
@@ -649,7 +771,7 @@ void consensus_wsad_kernel(ExactParams p) {
     // population variance (math.cairo:208-222): mean of qdev(x, mu) over the reliable rows
     double var;
     if constexpr (CONS) {
-      uint32_t sv = 0;
+      SumT sv = 0;
       if constexpr (BATCH || (WINH > 0 && BATCH1)) {
         if constexpr (WINH == 0) load_lo(rs, after(vo, mu), rowb, xr);
 #pragma unroll
@@ -779,6 +901,8 @@ void consensus_wsad_kernel(ExactParams p) {
     s3 = group_sum<NSEG, P>(s3);
     s4 = group_sum<NSEG, P>(s4);
     // skewness = idiv(s3 * n, (n-1)(n-2)); kurtosis = idiv(idiv(s4 n (n+1), n-1) - 3W(n-1)^2, (n-2)(n-3))
+    // (wide groups: the int64 / fp64 forms below hold while s3 R < 2^51 and s4 R (R + 1) < 2^63)
+    if (vc && !(fabs(s3) * Rd < 2251799813685248.0 && s4 * Rd * (Rd + 1.0) < 9.2e18)) bad = true;
     const double sk = trunc_div_d(s3 * Rd, k3, ik3);
     const int64_t t1 = ((int64_t)s4 * (int64_t)R * (int64_t)(R + 1)) / (int64_t)(R - 1);
     const int64_t t2 = 3ll * 1000000ll * (int64_t)(R - 1) * (int64_t)(R - 1);
@@ -844,6 +968,15 @@ static int launch_wsad_c(const ExactParams& p, hipStream_t stream) {
   hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   return (int)hipGetLastError();
 }
+// N > 256: whole constrained rounds on the wide lane groups (the binding sized the stage for win_h = 0)
+template <int NSEG>
+static int launch_wide(const ExactParams& p, hipStream_t stream) {
+  constexpr int WAVES = 4;
+  if (p.win_h != 0) return -3;
+  auto k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 0, true> : consensus_wsad_kernel<NSEG, WAVES, false, 0, true>;
+  hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
+  return (int)hipGetLastError();
+}
 template <int NSEG>
 static int launch_wsad(const ExactParams& p, hipStream_t stream) {
   return p.constrained ? launch_wsad_c<NSEG, true>(p, stream) : launch_wsad_c<NSEG, false>(p, stream);
@@ -859,11 +992,16 @@ extern "C" int svoc_exact_round_wsad(const ExactParams* p, hipStream_t stream) {
   // lane = column: with few columns most lanes idle, and for N <= 32 the i128 kernel packs 2-8
   // instances per wave instead (profiles/r2_exact_crossover.json: 7 x 6 140 M vs 10 M rounds/s,
   // 16 x 16 27 M vs 10 M; but 64 x 16 already 8.3 M vs 6.0 M for this kernel)
-  if (p->N < 4 || p->N > 256) return -2;
+  if (p->N < 4 || p->N > 4096) return -2;
+  if (p->N > 256 && !(p->constrained && p->mode == 0 && !p->legacy)) return -2;   // (wide: whole constrained rounds)
   if (p->N <= 32 && p->D < p->wsad_min_d) return -2;
   if (!p->stage || !p->fallback) return -2;
   if ((int64_t)p->N * p->D * (p->val32 ? 4 : 8) >= (1ll << 31)) return -2;   // 32-bit buffer offsets
   if (p->N <= 64) return launch_wsad<1>(*p, stream);
   if (p->N <= 128) return launch_wsad<2>(*p, stream);
-  return launch_wsad<4>(*p, stream);
+  if (p->N <= 256) return launch_wsad<4>(*p, stream);
+  if (p->N <= 512) return launch_wide<8>(*p, stream);
+  if (p->N <= 1024) return launch_wide<16>(*p, stream);
+  if (p->N <= 2048) return launch_wide<32>(*p, stream);
+  return launch_wide<64>(*p, stream);
 }

@@ -529,3 +529,20 @@ def test_wsad_pruned_window_fallback(N):
     assert took.sum() >= B - 1, fast["status"]
     for k in OUTS:
         assert torch.equal(fast[k][took], ref[k][took]), k
+
+
+@pytest.mark.parametrize("N,D,f", [(300, 70, 30), (512, 64, 64), (1000, 33, 100), (2048, 20, 256), (4096, 8, 512)])
+def test_wsad_kernel_wide_groups(N, D, f):
+    """N > 256: the column kernel's wide lane groups (8 .. 64 lanes per column, full cross-lane
+    median networks, qr by LDS atomics) take the constrained rounds and equal the i128 kernel and the CPU engine
+    bit for bit."""
+    B = 4
+    v = _wsad(B, N, D, f, seed=N + D)
+    fast = _run(v.to(DEV, torch.int32), f, {"SVOC_EXACT_WSAD_ONLY": "1", "SVOC_EXACT_WSAD_MIN_D": "1"})
+    ref = _run(v.to(DEV), f, {"SVOC_EXACT_I128": "1"})
+    cpu = _cpu(v, f, True, 0)
+    took = fast["status"] == 0
+    assert took.all(), fast["status"]
+    for k in OUTS:
+        assert torch.equal(fast[k], ref[k]), k
+        assert torch.equal(fast[k], cpu[k]), k
