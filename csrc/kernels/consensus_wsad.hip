@@ -284,6 +284,15 @@ void consensus_wsad_kernel(ExactParams p) {
   constexpr bool BATCH = NSEG >= 2;
   constexpr bool BATCH1 = BATCH || SVOC_WSAD_BATCH_QR;   // the qr and mean re-reads only (no fp64 temporaries)
   __shared__ uint64_t qr_part[WIDE ? 1 : WAVES * NPAD];
+  // WIDE: the slab's W columns of every row staged in LDS by 16-byte row loads (a lane owns 64 rows of ONE column,
+  // so a direct column load touches a cache line per element: 16x the bytes at D = 64), column-major with one
+  // word of padding per 64 rows (row r at r + r / 64: a lane's 64 rows sit in distinct banks across the wave)
+  // (TILE: 32 / 64 lanes per column, 1 / 2 columns per wave -- with 8 / 16 lanes per column a wave's direct load
+  // still reads 32 / 16 contiguous bytes per row, and the tile's per-slab barriers cost more than they save:
+  // 512 x 2048 ran 85 k rounds/s direct, 62 k through the tile)
+  constexpr bool TILE = WIDE && NSEG >= 32;
+  constexpr int TROW = NPAD + NPAD / 64;
+  __shared__ uint32_t tile[TILE ? W * TROW : 1];
   __shared__ uint64_t qr_lds[NPAD];
   __shared__ uint64_t relmask[MW], lowmask[MW];
   __shared__ int64_t rels[2];
@@ -325,6 +334,35 @@ void consensus_wsad_kernel(ExactParams p) {
   const uint32_t pol = group_polarity<NSEG>(seg);
   uint32_t badv = 0;                     // a value outside [0, 1e6]
 
+  // WIDE: stage slab s (columns s W .. s W + W - 1, rows < N) into the tile; int64 values' high words must be 0
+  auto load_tile = [&](int s) __attribute__((always_inline)) {
+    __syncthreads();   // (the previous slab's readers are done)
+    constexpr int VPR = W * ESZ / 16;   // 16-byte vectors per row
+    const int c0 = s * W;
+    for (int v = tid; v < N * VPR; v += NT) {
+      const int row = v / VPR, part = v - row * VPR;
+      const uint32_t off = (uint32_t)(row * rowb + c0 * ESZ + part * 16);
+      const uint4 w = (c0 * ESZ + part * 16 < D * ESZ) ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0))
+                                                        : make_uint4(0u, 0u, 0u, 0u);
+      const int pr = row + (row >> 6);
+      if constexpr (V32) {
+        tile[(part * 4 + 0) * TROW + pr] = w.x;
+        tile[(part * 4 + 1) * TROW + pr] = w.y;
+        tile[(part * 4 + 2) * TROW + pr] = w.z;
+        tile[(part * 4 + 3) * TROW + pr] = w.w;
+      } else {
+        tile[(part * 2 + 0) * TROW + pr] = w.x;
+        tile[(part * 2 + 1) * TROW + pr] = w.z;
+        const int c = c0 + part * 2;
+        badv |= ((c < D && w.y != 0u) || (c + 1 < D && w.w != 0u)) ? 1u : 0u;   // constrained: [0, 1e6]
+      }
+    }
+    __syncthreads();
+  };
+  // WIDE: row i of this lane's column from the tile
+  auto tl = [&](int i) __attribute__((always_inline)) -> uint32_t {
+    return tile[(wave * P + cw) * TROW + seg * 65 + i];
+  };
   uint64_t acc[WIDE ? 1 : KEEP];
 #pragma unroll
   for (int k = 0; k < (WIDE ? 1 : KEEP); ++k) acc[k] = 0;
@@ -352,6 +390,7 @@ void consensus_wsad_kernel(ExactParams p) {
     const bool vc = col < D;
     const int vo = seg_off + (vc ? col : 0) * ESZ;
     uint32_t c1;
+    if constexpr (TILE) load_tile(s);
     // unconstrained: the column's base B = its row-0 value (every lane of the group loads it)
     uint32_t Bl = 0u, Bh = 0u;
     if constexpr (!CONS) Bl = base_of(vc ? col : 0, s)[0];   // (the high word: after the network)
@@ -361,7 +400,7 @@ void consensus_wsad_kernel(ExactParams p) {
       for (int i = 0; i < 64; ++i) {
         // (the low word only: int64 rows get their high words checked below, 8 rows at a time -- loaded
         // here they held 64 more VGPRs and cost the int64 kernels their second wave per SIMD)
-        const uint32_t x = bload(rs, vo, i * rowb) - Bl;   // (unconstrained: relative to B)
+        const uint32_t x = (TILE ? tl(i) : bload(rs, vo, i * rowb)) - Bl;   // (unconstrained: relative to B)
         const bool real = i < nv;
         if constexpr (CONS) badv |= (vc && real && x > kWsadMax) ? 1u : 0u;   // outside [0, 1e6]
         if constexpr (!CONS && V32) {   // int32 storage: x - B without int32 overflow and within 2^30
@@ -467,6 +506,12 @@ void consensus_wsad_kernel(ExactParams p) {
         }
         qtree_hi_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
       }
+    } else if constexpr (TILE) {
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
+        q[i] = (vc && i < nv) ? qdev_u((double)tl(i) - cd) : 0u;
+      }
     } else if constexpr (BATCH1) {
       load_lo(rs, after(vo, c1), rowb, q);
 #pragma unroll
@@ -490,7 +535,7 @@ void consensus_wsad_kernel(ExactParams p) {
     } else if constexpr (CONS) {
       qtree_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
     }
-    if constexpr (!V32) {
+    if constexpr (!V32 && !TILE) {
       // int64 storage: the high words, 8 rows in flight -- 0 (constrained: [0, 1e6]); unconstrained: x - B
       // is the sign extension of its low word and within 2^30
 #pragma nounroll
@@ -695,12 +740,18 @@ void consensus_wsad_kernel(ExactParams p) {
     uint64_t mm = mymask, ml = mylow;
     asm volatile("" : "+v"(mm), "+v"(ml));   // keep the 64 row masks out of the slab loop's live set
     uint32_t cons = 0;
+    if constexpr (TILE) load_tile(s);
     if constexpr (CONS && WINH > 0) {
       cons = (uint32_t)stg[D + (vc ? col : 0)];   // (the window phase above)
     } else if constexpr (CONS) {
       uint32_t r[64];
       if constexpr (BATCH && (MODE != 2 || V32)) {   // values validated in pass 1 (or 32-bit): one batch
-        load_lo(rs, vo, rowb, r);
+        if constexpr (TILE) {
+#pragma unroll
+          for (int i = 0; i < 64; ++i) r[i] = tl(i);
+        } else {
+          load_lo(rs, vo, rowb, r);
+        }
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
           if (MODE == 2) badv |= (vc && i < nv && r[i] > kWsadMax) ? 1u : 0u;   // no pass 1 here
@@ -742,7 +793,12 @@ void consensus_wsad_kernel(ExactParams p) {
       if constexpr (BATCH1) {
         // (window path: no network in this loop, so the column is loaded once and kept for the mean,
         // variance and z-power loops; otherwise re-read per statistic)
-        load_lo(rs, WINH > 0 ? vo : after(vo, cons), rowb, xr);
+        if constexpr (TILE) {
+#pragma unroll
+          for (int i = 0; i < 64; ++i) xr[i] = tl(i);
+        } else {
+          load_lo(rs, WINH > 0 ? vo : after(vo, cons), rowb, xr);
+        }
 #pragma unroll
         for (int i = 0; i < 64; ++i) sx += xr[i] & bit_mask(mm, i);
       } else {
@@ -773,7 +829,12 @@ void consensus_wsad_kernel(ExactParams p) {
     if constexpr (CONS) {
       SumT sv = 0;
       if constexpr (BATCH || (WINH > 0 && BATCH1)) {
-        if constexpr (WINH == 0) load_lo(rs, after(vo, mu), rowb, xr);
+        if constexpr (TILE) {
+#pragma unroll
+          for (int i = 0; i < 64; ++i) xr[i] = tl(i);
+        } else if constexpr (WINH == 0) {
+          load_lo(rs, after(vo, mu), rowb, xr);
+        }
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
           if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
@@ -849,7 +910,12 @@ void consensus_wsad_kernel(ExactParams p) {
       s4 += wmul_pos_h(z2, z2);
     };
     if constexpr (BATCH || (WINH > 0 && BATCH1) || !CONS) {
-      if constexpr (WINH == 0 && CONS) load_lo(rs, after(vo, sd), rowb, xr);
+      if constexpr (TILE) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) xr[i] = tl(i);
+      } else if constexpr (WINH == 0 && CONS) {
+        load_lo(rs, after(vo, sd), rowb, xr);
+      }
       if constexpr (!CONS) {   // (re-read: the column is not kept across the square root)
         const uint32_t bl = base_of(vc ? col : 0, (int)sd)[0];
         load_lo(rs, after(vo, sd), rowb, xr);
@@ -878,7 +944,7 @@ void consensus_wsad_kernel(ExactParams p) {
         const uint32_t bl = CONS ? 0u : base_of(vc ? col : 0, g)[0];   // (unconstrained: the base)
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-          xg[k] = bload(rs, vo, (g + k) * rowb) - bl;
+          xg[k] = (TILE ? tl(g + k) : bload(rs, vo, (g + k) * rowb)) - bl;
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
