@@ -30,6 +30,7 @@ run c2_exact_int64 300 --config c2 --mode exact --storage int64 --steps 10 --war
 run c5_exact 300 --config-file configs/c5_exact_rounds.yaml --steps 20 --warmup 2 &&
 run c3_exact 300 --config-file configs/c3_exact_rounds.yaml --steps 10 --warmup 2 &&
 run c2_exact_uncons 300 --config-file configs/c2_exact_unconstrained.yaml --steps 10 --warmup 2 &&
+run c2_exact_uncons_prices 300 --config-file configs/c2_exact_unconstrained_prices.yaml --steps 10 --warmup 2 &&
 run c5_exact_stream 300 --config-file configs/c5_exact_stream.yaml --steps 20 --warmup 2 &&
 true || exit 1
 fi
@@ -37,6 +38,7 @@ run wide512 300 --config-file configs/wide512.yaml --steps 10 --warmup 2 &&
 run wide512_fp32 300 --config-file configs/wide512.yaml --storage fp32 --steps 10 --warmup 2 &&
 run wide2048 300 --config-file configs/wide2048.yaml --steps 5 --warmup 1 &&
 run wide2048_fp32 300 --config-file configs/wide2048.yaml --storage fp32 --steps 5 --warmup 1 &&
+run wide512_exact 300 --config-file configs/wide512_exact.yaml --steps 3 --warmup 1 &&
 run wide4096_exact 300 --config-file configs/wide4096_exact.yaml --steps 3 --warmup 1 &&
 run c1 300 --config c1 --steps 50 --warmup 3 || exit 1
 for spec in "c3:--storage fp32" "c2:--storage bf16" "c4:"; do   # one storage per trace (no alt run)

@@ -35,6 +35,8 @@ ROWS = [
     ("c3_exact", "c3 shape (256 × 4096), exact wsad, int32 storage", "≈6/s numpy fp64 (non-exact)"),
     ("c2_exact_uncons", "c2 shape, exact wsad, UNCONSTRAINED rounds (reliable-mean essence), int64 storage",
      "0.61/s exact Python emulator (constrained)"),
+    ("c2_exact_uncons_prices", "c2 shape, exact UNCONSTRAINED rounds over price-like columns (60,000 ± 200 units, "
+     "int64 wsad ~6e10)", "0.61/s exact Python emulator (constrained)"),
     ("c5_exact", "c5 shape (7 × 6), exact wsad, 1M instances", "939/s exact Python emulator"),
     ("c5_exact_stream", "c5 shape, exact transactional update stream (store + round + revert per update)",
      "939/s exact Python emulator"),
@@ -46,6 +48,7 @@ ROWS = [
     ("wide512_fp32", "512 × 2048, fast mode over fp32 storage", "—"),
     ("wide2048", "2048 oracles × 512 dims (N > 1024)", "—"),
     ("wide2048_fp32", "2048 × 512, fast mode over fp32 storage", "—"),
+    ("wide512_exact", "512 × 2048, exact wsad rounds (column kernel, 8 lanes per column), 1024 instances", "—"),
     ("wide4096_exact", "4096 oracles × 64 dims, exact wsad rounds (N > 1024), 1024 instances", "—"),
 ]
 
