@@ -87,7 +87,10 @@ SVOC_HD double wmul_pos_h(double a, double b) { return floor(fma(a, b, 500000.5)
 // I128Div(A, b) = trunc(A / b) for integral |A| < 2^51, integral b >= 1, given ib = 1.0 / b (IEEE) and
 // hb = 0.5 * ib: trunc((A + sign(A) / 2) / b).  wsad_div(a, b) is this with A = a * 1e6 + floor(b / 2)
 // (signed_decimal.cairo:114-116).
-SVOC_HD double tdiv_h(double A, double ib, double hb) { return trunc(fma(A, ib, copysign(hb, A))); }
+// (Written on |A|: round-to-nearest is symmetric, so trunc(fma(-|A|, ib, -hb)) = -trunc(fma(|A|, ib, hb)) -- the
+// absolute value is a free source modifier of v_fma_f64 and the sign goes back with one in-place v_bfi_b32,
+// where copysign(hb, A) as the addend needed a v_bfi_b32 plus a v_mov_b32 for the pair's low word.)
+SVOC_HD double tdiv_h(double A, double ib, double hb) { return copysign(trunc(fma(fabs(A), ib, hb)), A); }
 SVOC_HD double wdiv_h(double a, double b) {
   const double ib = 1.0 / b;
   return tdiv_h(fma(a, kW, floor(b * 0.5)), ib, 0.5 * ib);

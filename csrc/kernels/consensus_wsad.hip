@@ -231,6 +231,15 @@ SVOC_DEV void rank_mask_select(const uint64_t* qr, int N, int R, uint64_t* relma
   __syncthreads();
 }
 
+// bit i of m as an all-ones / zero word the compiler cannot see through: (x & mk) | (y & ~mk) stays one
+// v_bfi_b32 and x & mk one v_and (a known sign-extended bit is canonicalised into a shift, a compare and a
+// select per row: 5 VALU where 2 do)
+SVOC_DEV uint32_t bit_mask_o(uint64_t m, int i) {
+  uint32_t k = bit_mask(m, i);
+  asm volatile("" : "+v"(k));
+  return k;
+}
+
 // sum over the NSEG lanes of a column group (lanes lane ^ t*P)
 template <int NSEG, int P, class T>
 SVOC_DEV T group_sum(T v) {
@@ -262,7 +271,7 @@ SVOC_DEV T group_sum(T v) {
 // a = N/2 - R/2.  The second network over the reliable rows (~30 % of the kernel's VALU) goes away.
 template <int NSEG, int WAVES, bool V32, int MODE, bool CONS, int WINH = 0>
 // (unconstrained int64, 4-lane groups: the wide pass-1 branch lands 2 VGPRs past 256 without the hint)
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu((!CONS && !V32 && NSEG == 4) ? 2 : 1)))
+__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(NSEG <= 4 ? 2 : 1)))
 void consensus_wsad_kernel(ExactParams p) {
   static_assert(WINH == 0 || (MODE == 0 && CONS), "the window path is for whole constrained rounds");
   constexpr int P = 64 / NSEG;      // columns per wave
@@ -384,11 +393,17 @@ void consensus_wsad_kernel(ExactParams p) {
   constexpr uint32_t kSign = CONS ? 0u : 0x80000000u;   // order-preserving key of an int32
 
   // ------------------------------------------------------------ pass 1 (contract.cairo:455-463)
-#pragma nounroll
-  for (int s = 0; s < (MODE == 2 ? 0 : nslab); ++s) {
+  // One slab.  FULL: N = NPAD and every column of the slab < D -- no per-row masks (the general form's 64
+  // per-lane row compares were hoisted out of the loop as SGPR masks and, with the 64 row offsets, spilled
+  // to VGPR lanes: ~480 v_readlane per slab).  The row offsets are recomputed per slab (opaque stride).
+  auto pass1 = [&](auto full_c, int s) __attribute__((always_inline)) {
+    constexpr bool FULL = decltype(full_c)::value;
     const int col = s * W + wave * P + cw;
-    const bool vc = col < D;
+    const bool vc = FULL || col < D;
     const int vo = seg_off + (vc ? col : 0) * ESZ;
+    const int nvf = FULL ? 64 : nv, nlf = FULL ? 64 : nl;
+    int rowb1 = rowb;
+    asm volatile("" : "+s"(rowb1));
     uint32_t c1;
     if constexpr (TILE) load_tile(s);
     // unconstrained: the column's base B = its row-0 value (every lane of the group loads it)
@@ -400,15 +415,15 @@ void consensus_wsad_kernel(ExactParams p) {
       for (int i = 0; i < 64; ++i) {
         // (the low word only: int64 rows get their high words checked below, 8 rows at a time -- loaded
         // here they held 64 more VGPRs and cost the int64 kernels their second wave per SIMD)
-        const uint32_t x = (TILE ? tl(i) : bload(rs, vo, i * rowb)) - Bl;   // (unconstrained: relative to B)
-        const bool real = i < nv;
+        const uint32_t x = (TILE ? tl(i) : bload(rs, vo, i * rowb1)) - Bl;   // (unconstrained: relative to B)
+        const bool real = i < nvf;
         if constexpr (CONS) badv |= (vc && real && x > kWsadMax) ? 1u : 0u;   // outside [0, 1e6]
         if constexpr (!CONS && V32) {   // int32 storage: x - B without int32 overflow and within 2^30
           const uint32_t xw = x + Bl;   // (the stored word)
           const bool ovf = (((xw ^ Bl) & (xw ^ x)) >> 31) != 0u;
           badv |= (vc && real && (ovf || x + (1u << 30) >= (1u << 31))) ? 1u : 0u;
         }
-        r[i] = (real ? x ^ kSign : (i < nl ? 0u : ~0u)) ^ pol;
+        r[i] = (real ? x ^ kSign : (i < nlf ? 0u : ~0u)) ^ pol;
       }
       uint32_t lo, hi;
       if constexpr (WINH > 0) {
@@ -424,8 +439,8 @@ void consensus_wsad_kernel(ExactParams p) {
           if (__ballot(!ok) != 0) {
 #pragma unroll
             for (int i = 0; i < 64; ++i) {
-              const uint32_t x = bload(rs, after(vo, lo), i * rowb) - Bl;
-              r[i] = (i < nv ? x ^ kSign : (i < nl ? 0u : ~0u)) ^ pol;
+              const uint32_t x = bload(rs, after(vo, lo), i * rowb1) - Bl;
+              r[i] = (i < nvf ? x ^ kSign : (i < nlf ? 0u : ~0u)) ^ pol;
             }
             window_group<NSEG, P, WINH>(r, seg, lane, w, lo, hi);
           }
@@ -479,13 +494,13 @@ void consensus_wsad_kernel(ExactParams p) {
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         q[i] = q[i] - Bl - c1;
-        wd = wd || (vc && i < nv && wide25(q[i]));
+        wd = wd || (vc && i < nvf && wide25(q[i]));
       }
       if (__ballot(wd) == 0) {
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
           if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
-          q[i] = (vc && i < nv) ? qdev_u((double)(int32_t)q[i]) : 0u;
+          q[i] = (vc && i < nvf) ? qdev_u((double)(int32_t)q[i]) : 0u;
         }
         qtree64_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
       } else {
@@ -494,7 +509,7 @@ void consensus_wsad_kernel(ExactParams p) {
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
           if ((i & 3) == 0) __builtin_amdgcn_sched_barrier(0);   // (4 rows of double-double temporaries)
-          q[i] = (vc && i < nv) ? q_lo(qdev_wide((double)(int32_t)q[i])) : 0u;
+          q[i] = (vc && i < nvf) ? q_lo(qdev_wide((double)(int32_t)q[i])) : 0u;
         }
         qtree64_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
         __builtin_amdgcn_sched_barrier(0);   // (the re-read after the whole butterfly, not beside it)
@@ -502,7 +517,7 @@ void consensus_wsad_kernel(ExactParams p) {
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
           if ((i & 3) == 0) __builtin_amdgcn_sched_barrier(0);
-          q[i] = (vc && i < nv) ? q_hi(qdev_wide((double)(int32_t)(q[i] - Bl - c1))) : 0u;
+          q[i] = (vc && i < nvf) ? q_hi(qdev_wide((double)(int32_t)(q[i] - Bl - c1))) : 0u;
         }
         qtree_hi_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
       }
@@ -510,20 +525,20 @@ void consensus_wsad_kernel(ExactParams p) {
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
-        q[i] = (vc && i < nv) ? qdev_u((double)tl(i) - cd) : 0u;
+        q[i] = (vc && i < nvf) ? qdev_u((double)tl(i) - cd) : 0u;
       }
     } else if constexpr (BATCH1) {
       load_lo(rs, after(vo, c1), rowb, q);
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bound the fp64 temporaries in flight
-        q[i] = (vc && i < nv) ? qdev_u(xv(q[i]) - cd) : 0u;
+        q[i] = (vc && i < nvf) ? qdev_u(xv(q[i]) - cd) : 0u;
       }
     } else {
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
-        const uint32_t x = bload(rs, vo, i * rowb);   // (low word; int64 high words are checked below)
-        q[i] = (vc && i < nv) ? qdev_u(xv(x) - cd) : 0u;
+        const uint32_t x = bload(rs, vo, i * rowb1);   // (low word; int64 high words are checked below)
+        q[i] = (vc && i < nvf) ? qdev_u(xv(x) - cd) : 0u;
       }
     }
     if constexpr (WIDE) {
@@ -549,15 +564,22 @@ void consensus_wsad_kernel(ExactParams p) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           if constexpr (CONS) {
-            badv |= (vc && g + k < nv && hw[k] != 0u) ? 1u : 0u;
+            badv |= (vc && g + k < nvf && hw[k] != 0u) ? 1u : 0u;
           } else {
             const uint32_t rl = lw[k] - Bl, rh = hw[k] - Bh - (lw[k] < Bl ? 1u : 0u);
             const bool ok = rh == (uint32_t)((int32_t)rl >> 31) && rl + (1u << 30) < (1u << 31);
-            badv |= (vc && g + k < nv && !ok) ? 1u : 0u;
+            badv |= (vc && g + k < nvf && !ok) ? 1u : 0u;
           }
         }
       }
     }
+  };
+  if constexpr (MODE != 2) {
+    const int nfull = N == NPAD ? min(D / W, nslab) : 0;
+#pragma nounroll
+    for (int s = 0; s < nfull; ++s) pass1(std::true_type{}, s);
+#pragma nounroll
+    for (int s = nfull; s < nslab; ++s) pass1(std::false_type{}, s);
   }
   if constexpr (!WIDE) {
     int base = 0;
@@ -800,7 +822,7 @@ void consensus_wsad_kernel(ExactParams p) {
           load_lo(rs, WINH > 0 ? vo : after(vo, cons), rowb, xr);
         }
 #pragma unroll
-        for (int i = 0; i < 64; ++i) sx += xr[i] & bit_mask(mm, i);
+        for (int i = 0; i < 64; ++i) sx += xr[i] & bit_mask_o(mm, i);
       } else {
 #pragma unroll 16
         for (int i = 0; i < 64; ++i) sx += bload(rs, vo, i * rowb) & bit_mask(mm, i);
@@ -838,7 +860,7 @@ void consensus_wsad_kernel(ExactParams p) {
 #pragma unroll
         for (int i = 0; i < 64; ++i) {
           if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
-          sv += bit_mask(mm, i) & qdev_u((double)xr[i] - mu);
+          sv += bit_mask_o(mm, i) & qdev_u((double)xr[i] - mu);
         }
       } else {
 #pragma unroll 16
@@ -901,9 +923,12 @@ void consensus_wsad_kernel(ExactParams p) {
     double s3 = 0.0, s4 = 0.0;
     bool outl = false;   // a row with z^2 >= 2^25 (|z| >= 5.79): this column's sums are redone below
     // z-score powers of one row (a masked row reads as mu: z = 0, all powers 0)
+    // (1e6 as an opaque SGPR pair: with the literal the fma became v_fmac_f64 on a v_mov_b64 copy of C0)
+    double kWs = kW;
+    asm volatile("" : "+s"(kWs));
     auto zpow = [&](uint32_t x, uint32_t mk) {
       const uint32_t xm = (x & mk) | (mu_u & ~mk);
-      const double z = tdiv_h(fma(xv(xm), kW, C0), isd, hisd);
+      const double z = tdiv_h(fma(xv(xm), kWs, C0), isd, hisd);
       const double z2 = wmul_pos_h(z, z);
       outl = outl || !(z2 < 33554432.0);   // 2^25: keeps z^2 z and z^2 z^2 below the forms' 2.25e9 quotients
       s3 += wmul_h(z2, z, z < 0.0);
@@ -925,7 +950,7 @@ void consensus_wsad_kernel(ExactParams p) {
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);   // bound the fp64 temporaries in flight
-        zpow(xr[i], bit_mask(mm, i));
+        zpow(xr[i], bit_mask_o(mm, i));
       }
     } else {
 #pragma unroll 8
