@@ -270,8 +270,11 @@ SVOC_DEV T group_sum(T v) {
 // need g at positions R/2 - 1 .. R/2 + f, inside the window when WINH >= max(a + 1, f - a + 1),
 // a = N/2 - R/2.  The second network over the reliable rows (~30 % of the kernel's VALU) goes away.
 template <int NSEG, int WAVES, bool V32, int MODE, bool CONS, int WINH = 0>
-// (unconstrained int64, 4-lane groups: the wide pass-1 branch lands 2 VGPRs past 256 without the hint)
-__global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(NSEG <= 4 ? 2 : 1)))
+// (2 waves per SIMD where the kernel fits 256 VGPRs without scratch in its loops: the whole / first-half constrained
+// rounds and the unconstrained int64 ones; the unconstrained int32 and D-sharded second-half instantiations spill
+// a few hundred bytes at that cap and keep one wave with AGPR spill slots)
+__global__ __launch_bounds__(WAVES * 64)
+__attribute__((amdgpu_waves_per_eu(NSEG <= 4 && !(CONS && MODE == 2) ? 2 : 1)))
 void consensus_wsad_kernel(ExactParams p) {
   static_assert(WINH == 0 || (MODE == 0 && CONS), "the window path is for whole constrained rounds");
   constexpr int P = 64 / NSEG;      // columns per wave
@@ -411,19 +414,31 @@ void consensus_wsad_kernel(ExactParams p) {
     if constexpr (!CONS) Bl = base_of(vc ? col : 0, s)[0];   // (the high word: after the network)
     {
       uint32_t r[64];
+      // domain checks as running extremes of the stored words (one v_max3 / v_min3 per two rows; per-row compares
+      // became 64 SGPR masks, and the int32 overflow test held the stored words: one wave per SIMD less).  Rows
+      // past N read as 0 from the buffer (constrained: inside [0, 1e6]) or are replaced by the base
+      uint32_t wmax = 0u;                   // constrained: largest stored word (unsigned: negative -> huge)
+      int32_t smax = (int32_t)Bl, smin = (int32_t)Bl;   // unconstrained int32: extremes of the real rows
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
         // (the low word only: int64 rows get their high words checked below, 8 rows at a time -- loaded
         // here they held 64 more VGPRs and cost the int64 kernels their second wave per SIMD)
-        const uint32_t x = (TILE ? tl(i) : bload(rs, vo, i * rowb1)) - Bl;   // (unconstrained: relative to B)
+        const uint32_t w = TILE ? tl(i) : bload(rs, vo, i * rowb1);
+        const uint32_t x = w - Bl;   // (unconstrained: relative to B)
         const bool real = i < nvf;
-        if constexpr (CONS) badv |= (vc && real && x > kWsadMax) ? 1u : 0u;   // outside [0, 1e6]
-        if constexpr (!CONS && V32) {   // int32 storage: x - B without int32 overflow and within 2^30
-          const uint32_t xw = x + Bl;   // (the stored word)
-          const bool ovf = (((xw ^ Bl) & (xw ^ x)) >> 31) != 0u;
-          badv |= (vc && real && (ovf || x + (1u << 30) >= (1u << 31))) ? 1u : 0u;
+        if constexpr (CONS) wmax = __builtin_elementwise_max(wmax, w);
+        if constexpr (!CONS && V32) {
+          const int32_t ws = FULL ? (int32_t)w : (int32_t)((w & lt_mask(i, nvf)) | (Bl & ~lt_mask(i, nvf)));
+          smax = __builtin_elementwise_max(smax, ws);
+          smin = __builtin_elementwise_min(smin, ws);
         }
         r[i] = (real ? x ^ kSign : (i < nlf ? 0u : ~0u)) ^ pol;
+      }
+      if constexpr (CONS) badv |= (vc && wmax > kWsadMax) ? 1u : 0u;   // outside [0, 1e6]
+      if constexpr (!CONS && V32) {
+        // int32 storage: every x - B within [-2^30, 2^30) as an exact integer (no int32 overflow)
+        const int64_t up = (int64_t)smax - (int32_t)Bl, dn = (int64_t)(int32_t)Bl - smin;
+        badv |= (vc && (up >= (1ll << 30) || dn > (1ll << 30))) ? 1u : 0u;
       }
       uint32_t lo, hi;
       if constexpr (WINH > 0) {
