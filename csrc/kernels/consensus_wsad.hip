@@ -287,7 +287,7 @@ void consensus_wsad_kernel(ExactParams p) {
   // holds 64 rows of one column: the butterfly would leave it 64 / P row sums -- 128 VGPRs at P = 1), and
   // 64-bit / fp64 column sums (R values up to 1e6 pass 2^32)
   constexpr bool WIDE = NSEG > 4;
-  static_assert(!WIDE || (CONS && MODE == 0 && WINH == 0), "wide groups: whole constrained rounds, two networks");
+  static_assert(!WIDE || (MODE == 0 && WINH == 0), "wide groups: whole rounds, two networks");
   constexpr int MW = NSEG > 4 ? NSEG : 4;   // 64-bit row-mask words
   constexpr int ESZ = V32 ? 4 : 8;
   // re-reads issued as 64-load batches ordered after the value they need (load_lo / after): +37% at
@@ -303,6 +303,7 @@ void consensus_wsad_kernel(ExactParams p) {
   // still reads 32 / 16 contiguous bytes per row, and the tile's per-slab barriers cost more than they save:
   // 512 x 2048 ran 85 k rounds/s direct, 62 k through the tile)
   constexpr bool TILE = WIDE && NSEG >= 32;
+  static_assert(!TILE || CONS || V32, "the tile keeps low words only: unconstrained int64 rounds need their high words");
   constexpr int TROW = NPAD + NPAD / 64;
   __shared__ uint32_t tile[TILE ? W * TROW : 1];
   __shared__ uint64_t qr_lds[NPAD];
@@ -504,7 +505,12 @@ void consensus_wsad_kernel(ExactParams p) {
     const double cd = xv(c1);
     if constexpr (!CONS) {
       // d = x - c1 relative (|d| < 2^30 in the domain); the narrow form unless some |d| >= 2^25 in the wave
-      load_lo(rs, after(vo, c1), rowb, q);
+      if constexpr (TILE) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) q[i] = tl(i);
+      } else {
+        load_lo(rs, after(vo, c1), rowb, q);
+      }
       bool wd = false;
 #pragma unroll
       for (int i = 0; i < 64; ++i) {
@@ -517,7 +523,17 @@ void consensus_wsad_kernel(ExactParams p) {
           if ((i & 7) == 0) __builtin_amdgcn_sched_barrier(0);
           q[i] = (vc && i < nvf) ? qdev_u((double)(int32_t)q[i]) : 0u;
         }
-        qtree64_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
+        if constexpr (!WIDE) qtree64_all<P>(q, lane, acc, std::make_integer_sequence<int, KEEP>{});
+      } else if constexpr (WIDE) {
+        // 43-bit quotients straight into the per-oracle sums (64-bit LDS atomics); q is cleared for the
+        // narrow-path atomics below
+#pragma unroll
+        for (int i = 0; i < 64; ++i) {
+          if ((i & 3) == 0) __builtin_amdgcn_sched_barrier(0);
+          const uint64_t qq = (vc && i < nvf) ? (uint64_t)qdev_wide((double)(int32_t)q[i]) : 0ull;
+          if (qq) atomicAdd((unsigned long long*)&qr_lds[seg * 64 + i], (unsigned long long)qq);
+          q[i] = 0u;
+        }
       } else {
         // 43-bit quotients: the low words through the 64-bit butterfly, then (recomputed from a second read)
         // the high words through the 32-bit one, shifted
@@ -848,7 +864,12 @@ void consensus_wsad_kernel(ExactParams p) {
                // zero shifted back (tdiv_rel); the mean is the consensus.  The column is loaded once (no network
                // in this loop) and kept for the variance and z-power loops.
       const u32x2_t bv = base_of(vc ? col : 0, (int)mm);
-      load_lo(rs, after(vo, mm), rowb, xr);
+      if constexpr (TILE) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) xr[i] = tl(i);
+      } else {
+        load_lo(rs, after(vo, mm), rowb, xr);
+      }
 #pragma unroll
       for (int i = 0; i < 64; ++i) xr[i] -= bv[0];
       double sxd = 0.0;
@@ -958,7 +979,7 @@ void consensus_wsad_kernel(ExactParams p) {
       }
       if constexpr (!CONS) {   // (re-read: the column is not kept across the square root)
         const uint32_t bl = base_of(vc ? col : 0, (int)sd)[0];
-        load_lo(rs, after(vo, sd), rowb, xr);
+        if constexpr (!TILE) load_lo(rs, after(vo, sd), rowb, xr);
 #pragma unroll
         for (int i = 0; i < 64; ++i) xr[i] -= bl;
       }
@@ -1074,12 +1095,21 @@ static int launch_wsad_c(const ExactParams& p, hipStream_t stream) {
   hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   return (int)hipGetLastError();
 }
-// N > 256: whole constrained rounds on the wide lane groups (the binding sized the stage for win_h = 0)
+// N > 256: whole rounds on the wide lane groups (the binding sized the stage for win_h = 0); unconstrained
+// int64 rounds at 32 / 64 lanes per column (the tiled groups) go to the i128 kernel
 template <int NSEG>
 static int launch_wide(const ExactParams& p, hipStream_t stream) {
   constexpr int WAVES = 4;
   if (p.win_h != 0) return -3;
   auto k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 0, true> : consensus_wsad_kernel<NSEG, WAVES, false, 0, true>;
+  if (!p.constrained) {
+    if constexpr (NSEG >= 32) {
+      if (!p.val32) return -2;
+      k = consensus_wsad_kernel<NSEG, WAVES, true, 0, false>;
+    } else {
+      k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 0, false> : consensus_wsad_kernel<NSEG, WAVES, false, 0, false>;
+    }
+  }
   hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   return (int)hipGetLastError();
 }
@@ -1099,7 +1129,7 @@ extern "C" int svoc_exact_round_wsad(const ExactParams* p, hipStream_t stream) {
   // instances per wave instead (profiles/r2_exact_crossover.json: 7 x 6 140 M vs 10 M rounds/s,
   // 16 x 16 27 M vs 10 M; but 64 x 16 already 8.3 M vs 6.0 M for this kernel)
   if (p->N < 4 || p->N > 4096) return -2;
-  if (p->N > 256 && !(p->constrained && p->mode == 0 && !p->legacy)) return -2;   // (wide: whole constrained rounds)
+  if (p->N > 256 && p->mode != 0) return -2;   // (wide groups: whole rounds)
   if (p->N <= 32 && p->D < p->wsad_min_d) return -2;
   if (!p->stage || !p->fallback) return -2;
   if ((int64_t)p->N * p->D * (p->val32 ? 4 : 8) >= (1ll << 31)) return -2;   // 32-bit buffer offsets
