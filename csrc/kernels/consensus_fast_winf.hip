@@ -177,11 +177,6 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
   // (-1: the state row), and the slots whose row failed the interval check
   __shared__ int smap[FUSED ? NPAD : 1];
   __shared__ uint32_t badu[8];
-  // fused, pass 2: the removed rows' byte offsets in their source (batch slot or state row) and which of them
-  // come from the batch (bit k), resolved once per instance -- per column and slot the two dependent LDS
-  // lookups (urow, smap) serialised the loads and their descriptors' live ranges spilled SGPRs
-  __shared__ int uoff[FUSED ? 32 : 1];
-  __shared__ uint32_t ubat[FUSED ? 1 : 1];
 
   const int b = blockIdx.x;
   static_assert(!FUSED || (MODE == 0 && CONS), "fused streaming: whole constrained rounds");
@@ -620,16 +615,6 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     }
   }
 
-  if constexpr (FUSED) {
-    if (tid < 32) {
-      const int row = urow[tid];
-      const int u = smap[row];
-      uoff[tid] = u >= 0 ? u * D * 4 : row * rowb;
-      const uint64_t bb = __ballot(u >= 0);
-      if (tid == 0) ubat[0] = (uint32_t)bb;
-    }
-    __syncthreads();
-  }
   // ------------------------------------------------------------ phase B: pass 2 (contract.cairo:476-500)
   // one lane per column: the removed keys are sorted once and ranked against the window.
   // Constrained rounds with D <= 4096 (LDSO): the outputs are staged in the idle slab region and the
@@ -658,22 +643,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     const int s0 = CONS ? shl : 0;
     const uint64_t realm = ((fl >= 64 ? ~0ull : (1ull << fl) - 1)) << s0;
     q.c1c = p.c1[ob + pc];
-    uint32_t ub = 0u;
-    if constexpr (FUSED) ub = __builtin_amdgcn_readfirstlane(ubat[0]);
 #pragma unroll
     for (int t = 0; t < NS; ++t) {
       const int row = t - s0;
       const bool real = (realm >> t) & 1;
       q.uw[t] = 0u;
-      if (CONS || real) {
-        const int k = real ? row : 0;
-        if constexpr (FUSED) {
-          const int off = __builtin_amdgcn_readfirstlane(uoff[k]);
-          q.uw[t] = ((ub >> k) & 1u) ? bload(rb, vo, off) : bload(rs, vo, off);
-        } else {
-          q.uw[t] = bload(rs, vo, __builtin_amdgcn_readfirstlane(urow[k]) * rowb);
-        }
-      }
+      if (CONS || real) q.uw[t] = row_load(__builtin_amdgcn_readfirstlane(urow[real ? row : 0]), vo);
     }
     if constexpr (CONS) {
 #pragma unroll
