@@ -41,7 +41,7 @@ CONFIGS = {
                batch=1024, update_frac=0.25, pipeline=2, storage="fp32", alt_storage="bf16"),
     "c2": dict(model="svoc-consensus N=64 D=1024 batched (f=8, constrained)", N=64, D=1024, f=8,
                batch=10000, update_frac=0.0, storage="bf16", alt_storage="fp32"),
-    "c4": dict(model="sentiment oracles: BERT-base (12x768, bf16) on 30-comment windows -> 7 oracles x 6 dims",
+    "c4": dict(model="sentiment oracles: RoBERTa-base (BERT-base sized 12x768, erf GELU, bf16) on 30-comment windows -> 7 oracles x 6 dims",
                N=7, D=6, f=2, batch=64, update_frac=1.0, seq_len=128, alt_precision="fp32"),
     "c5": dict(model="deployed config 7 oracles x 6 dims, governance + reliability stream (1% instances vote/step)",
                N=7, D=6, f=2, batch=1 << 20, update_frac=1 / 7, gov_frac=0.01),

@@ -81,7 +81,7 @@ SVOC_DEV bool moments_from_sums_d(double n, double t1, double t2, double t3, dou
   return true;
 }
 
-// qr partials: every lane accumulates (x - c1)^2 of its 64 rows (rows m, m + 32 as one packed pair)
+// qr partials: every lane accumulates (x - c1)^2 of its 64 rows (rows 2m, 2m + 1 as one packed pair)
 // over all the columns it visits in phase A, with the column's power sums of d = x - c1 on the way
 // (v_pk_add / v_pk_fma); the rows' sums across the wave's P column lanes are formed once, after phase
 // A, by the transposing butterfly qr_halve (stage MSK exchanges with lane ^ MSK and halves the row set:
@@ -105,14 +105,17 @@ SVOC_DEV void qr_halve(float (&part)[64], int lane) {
 template <bool MASKW, bool MASKROWS>
 SVOC_DEV void qr_moments_regs(const RawRows& xs, int nvl, float c, uint32_t mw, f32x2 (&acc)[32],
                               f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
+  // (rows 2m, 2m + 1 as one packed pair: the slab copy's ds_read2st64 lands them in adjacent registers, so
+  // the pair is a v_pk operand without the v_mov that pairing rows m, m + 32 needed)
 #pragma unroll
   for (int m = 0; m < 32; ++m) {
-    const uint32_t w0 = MASKW ? xs.lo[m] & mw : xs.lo[m], w1 = MASKW ? xs.hi[m] & mw : xs.hi[m];
+    const uint32_t r0 = xs.at(2 * m), r1 = xs.at(2 * m + 1);
+    const uint32_t w0 = MASKW ? r0 & mw : r0, w1 = MASKW ? r1 & mw : r1;
     f32x2 y = f32x2{u2f(w0), u2f(w1)} - f32x2{c, c};
     f32x2 q = y * y;
     acc[m] += q;
     if (MASKROWS) {
-      const uint32_t m0 = lt_mask(m, nvl), m1 = lt_mask(m + 32, nvl);
+      const uint32_t m0 = lt_mask(2 * m, nvl), m1 = lt_mask(2 * m + 1, nvl);
       const float y0 = y.x, y1 = y.y, q0 = q.x, q1 = q.y;
       y = f32x2{fand(y0, m0), fand(y1, m1)};
       q = f32x2{fand(q0, m0), fand(q1, m1)};
@@ -130,8 +133,8 @@ SVOC_DEV void qr_keep(const f32x2 (&a)[32], int lane, float (&keep)[64 / P], boo
   float part[64];
 #pragma unroll
   for (int m = 0; m < 32; ++m) {
-    part[m] = a[m].x;
-    part[m + 32] = a[m].y;
+    part[2 * m] = a[m].x;
+    part[2 * m + 1] = a[m].y;
   }
   qr_halve<P / 2, 32>(part, lane);
 #pragma unroll
@@ -303,9 +306,12 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       uint32_t pfrom = 0u;
 #pragma unroll
       for (int k = 0; k < 16; ++k) pfrom |= (((pm[k / 4] >> (8 * (k % 4))) & 0xffu) ? 1u : 0u) << k;
+      // (24-bit multiplies: a 32-bit integer product is a quarter-rate v_mad_u64_u32 here, 32 per slab; the
+      // dispatcher keeps rows and D * 4 below 2^24 bytes on this path.  A state piece's batch offset -- slot
+      // byte 0 -- wraps below zero and is never used: exec-masked)
       dma.issue_mapped(
-          rsd, rbd, reg_o, [&](int k) { return dma.row_of(k) * rowb_o + cb; },
-          [&](int k) { return ((int)((pm[k / 4] >> (8 * (k % 4))) & 0xffu) - 1) * d4 + cb; }, pfrom);
+          rsd, rbd, reg_o, [&](int k) { return (int)__umul24((unsigned)dma.row_of(k), (unsigned)rowb_o) + cb; },
+          [&](int k) { return (int)__umul24((pm[k / 4] >> (8 * (k % 4))) & 0xffu, (unsigned)d4) - d4 + cb; }, pfrom);
     } else {
       dma.issue(rsd, region, rowb, s * W + wave * P);
     }
@@ -944,7 +950,7 @@ extern "C" int svoc_fast_round_f32_win(const FastParams* p, hipStream_t stream) 
   if ((int64_t)p->N * p->ld * 4 >= (1ll << 31)) return -2;
   if (p->mode == 2 && p->work_fresh) return -2;   // pass 1 ran elsewhere: no windows to read
   if (p->upd_rows && (p->mode != 0 || !p->constrained || p->upd_per_inst <= 0 || p->upd_per_inst > 256 ||
-                      (int64_t)p->upd_per_inst * p->D * 4 >= (1ll << 31)))
+                      (int64_t)p->upd_per_inst * p->D * 4 >= (1ll << 31) || (int64_t)p->ld * 4 >= (1ll << 24)))
     return -3;
   if (p->n_failing < 0 || p->n_failing > 32 || p->n_failing > p->N - 2) return -2;
   const int H = fast_win_h(p->N, p->n_failing);

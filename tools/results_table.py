@@ -26,7 +26,7 @@ ROWS = [
     ("c3_notxn", "c3, coalesced without transactions (a reverted batch's rows stay; the round-3 headline form)",
      "≈6/s numpy fp64"),
     ("c3_bf16", "c3 shape, fast mode over bf16 storage, transactional", "≈6/s numpy fp64"),
-    ("c4", "c4: BERT-base sentiment oracles → consensus", "—"),
+    ("c4", "c4: RoBERTa-base (BERT-base sized) sentiment oracles → consensus", "—"),
     ("c5", "c5: governance + reliability stream, 1M instances (7 × 6)", "≈127,900/s numpy fp64 (7×6)"),
     ("c2_fp32", "c2 shape, fast mode over fp32 storage (reference resolution)", "≈93/s numpy fp64"),
     ("c3_fp32", "c3 shape, fast mode over fp32 storage (reference resolution)", "≈6/s numpy fp64"),
