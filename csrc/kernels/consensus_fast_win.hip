@@ -48,22 +48,30 @@ SVOC_DEV u16x2 win_cand(u16x2 wt, u16x2 zt) {  // wt < zt ? wt : 0xFFFF, per 16-
 }
 
 // Skewness / sample-adjusted excess kurtosis (math.cairo:320-363) of n values from power sums of
-// d = x - shift; returns false for zero variance (the contract's sqrt(0) -> div-by-zero revert).
-SVOC_DEV bool moments_from_sums(float n, float t1, float t2, float t3, float t4, float& dl, float& sk, float& ku) {
+// d = x - shift; returns false for zero variance (the contract's sqrt(0) -> div-by-zero revert).  The
+// n-only factors are formed once per instance (MomK); per column one IEEE division (1 / mu2) and one
+// v_rsq_f32 remain of the ~10 divisions (each a div_scale / rcp / fma / div_fmas / div_fixup sequence) the
+// direct formulas cost -- a third of the c2 pass-2 loop.  (Within a few ulp of the direct form.)
+struct MomK {
+  float n, in, k3, k4a, k4b, ik4c;
+};
+SVOC_DEV MomK mom_k(float n) {
+  return MomK{n, 1.f / n, n / ((n - 1.f) * (n - 2.f)), n * (n + 1.f) / (n - 1.f), 3.f * (n - 1.f) * (n - 1.f),
+              1.f / ((n - 2.f) * (n - 3.f))};
+}
+SVOC_DEV bool moments_from_sums(const MomK& K, float t1, float t2, float t3, float t4, float& dl, float& sk, float& ku) {
 #pragma clang fp contract(off)
-  dl = t1 / n;
-  const float e2 = t2 / n, e3 = t3 / n, e4 = t4 / n;
+  dl = t1 * K.in;
+  const float e2 = t2 * K.in, e3 = t3 * K.in, e4 = t4 * K.in;
   const float mu2 = e2 - dl * dl;
   const float mu3 = e3 - 3.f * dl * e2 + 2.f * dl * dl * dl;
   const float mu4 = e4 - 4.f * dl * e3 + 6.f * dl * dl * e2 - 3.f * dl * dl * dl * dl;
   sk = 0.f;
   ku = 0.f;
   if (!(mu2 > 0.f)) return false;
-  const float k3 = n / ((n - 1.f) * (n - 2.f));
-  const float k4a = n * (n + 1.f) / (n - 1.f), k4b = 3.f * (n - 1.f) * (n - 1.f), k4c = (n - 2.f) * (n - 3.f);
-  const float sd = sqrtf(mu2);
-  sk = n * mu3 / (mu2 * sd) * k3;
-  ku = (n * mu4 / (mu2 * mu2) * k4a - k4b) / k4c;
+  const float r = 1.f / mu2;
+  sk = K.n * mu3 * r * __builtin_amdgcn_rsqf(mu2) * K.k3;
+  ku = (K.n * mu4 * (r * r) * K.k4a - K.k4b) * K.ik4c;
   return true;
 }
 
@@ -580,6 +588,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   // one lane per column pair: the removed keys are sorted once (true key order) and ranked against
   // both window halves; packed power sums for the two columns
   const float n = (float)R;
+  const MomK mk = mom_k(n);
   const int sh = H - 1 - (N / 2 - R / 2);   // -inf sentinels in front of the removed keys
   const int64_t ob = (int64_t)b * D;
   bool zv = false;
@@ -673,7 +682,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
       const float r2 = h ? t2.y : t2.x, r4 = h ? t4.y : t4.x;
       // trusted: no deep cancellation in the all-minus-removed difference, and the reliable mean
       // within 2 sigma of the shift c1 (moments about a far shift cancel like (dl^2 / mu2)^2)
-      const float rdl = (h ? t1.y : t1.x) / n, rmu2 = r2 / n - rdl * rdl;
+      const float rdl = (h ? t1.y : t1.x) * mk.in, rmu2 = r2 * mk.in - rdl * rdl;
       const bool good = r2 > 0.f && a2 <= p.win_cancel * r2 && a4 <= p.win_cancel * r4 && rdl * rdl <= 4.f * rmu2;
       if (CONS) {
         p.consensus[ob + col] = h ? 0.5f * (bf16_hi(medw) + bf16_hi(mhw)) : 0.5f * (bf16_lo(medw) + bf16_lo(mhw));
@@ -681,7 +690,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
       }
       if (good) {
         float dl, sk, ku;
-        const bool nz = moments_from_sums(n, h ? t1.y : t1.x, r2, h ? t3.y : t3.x, r4, dl, sk, ku);
+        const bool nz = moments_from_sums(mk, h ? t1.y : t1.x, r2, h ? t3.y : t3.x, r4, dl, sk, ku);
         if (CONS) {
           p.skew[ob + col] = p.legacy ? 0.f : sk;
           p.kurt[ob + col] = p.legacy ? 0.f : ku;
@@ -741,7 +750,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
       c1s += xor_lane<32>(c1s); t2 += xor_lane<32>(t2); t3 += xor_lane<32>(t3); t4 += xor_lane<32>(t4);
       if (lane == 0) {
         float dl, sk, ku;
-        const bool nz = moments_from_sums(n, c1s, t2, t3, t4, dl, sk, ku);
+        const bool nz = moments_from_sums(mk, c1s, t2, t3, t4, dl, sk, ku);
         if (CONS) {
           p.skew[ob + col] = p.legacy ? 0.f : sk;
           p.kurt[ob + col] = p.legacy ? 0.f : ku;

@@ -62,22 +62,29 @@ SVOC_DEV uint32_t winf_cand(uint32_t wt, uint32_t zt) {
 }
 
 // Skewness / sample-adjusted excess kurtosis (math.cairo:320-363) of n values from power sums of
-// d = x - shift, combined in fp64; false for zero variance (the contract's sqrt(0) -> div-by-zero).
-SVOC_DEV bool moments_from_sums_d(double n, double t1, double t2, double t3, double t4, double& dl, float& sk,
+// d = x - shift, combined in fp64; false for zero variance (the contract's sqrt(0) -> div-by-zero).  The
+// n-only factors are formed once per instance (MomKd): per column two fp64 divisions and a square root remain
+// of the nine divisions of the direct formulas.
+struct MomKd {
+  double n, in, k3, k4a, k4b, ik4c;
+};
+SVOC_DEV MomKd mom_kd(double n) {
+  return MomKd{n, 1.0 / n, n / ((n - 1.0) * (n - 2.0)), n * (n + 1.0) / (n - 1.0), 3.0 * (n - 1.0) * (n - 1.0),
+               1.0 / ((n - 2.0) * (n - 3.0))};
+}
+SVOC_DEV bool moments_from_sums_d(const MomKd& K, double t1, double t2, double t3, double t4, double& dl, float& sk,
                                   float& ku) {
-  dl = t1 / n;
-  const double e2 = t2 / n, e3 = t3 / n, e4 = t4 / n;
+  dl = t1 * K.in;
+  const double e2 = t2 * K.in, e3 = t3 * K.in, e4 = t4 * K.in;
   const double mu2 = e2 - dl * dl;
   const double mu3 = e3 - 3.0 * dl * e2 + 2.0 * dl * dl * dl;
   const double mu4 = e4 - 4.0 * dl * e3 + 6.0 * dl * dl * e2 - 3.0 * dl * dl * dl * dl;
   sk = 0.f;
   ku = 0.f;
   if (!(mu2 > 0.0)) return false;
-  const double k3 = n / ((n - 1.0) * (n - 2.0));
-  const double k4a = n * (n + 1.0) / (n - 1.0), k4b = 3.0 * (n - 1.0) * (n - 1.0), k4c = (n - 2.0) * (n - 3.0);
-  const double sd = sqrt(mu2);
-  sk = (float)(n * mu3 / (mu2 * sd) * k3);
-  ku = (float)((n * mu4 / (mu2 * mu2) * k4a - k4b) / k4c);
+  const double r = 1.0 / mu2;
+  sk = (float)(K.n * mu3 * r / sqrt(mu2) * K.k3);
+  ku = (float)((K.n * mu4 * (r * r) * K.k4a - K.k4b) * K.ik4c);
   return true;
 }
 
@@ -628,6 +635,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
   // flight, the next column's words (removed rows, window, power sums, c1) are loaded while this one is
   // computed (in-order vmcnt waits).  Otherwise one column per iteration, outputs stored directly.
   const double n = (double)R;
+  const MomKd mk = mom_kd(n);
   const int sh = H - 1 - (N / 2 - R / 2);   // -inf sentinels in front of the removed keys
   const int64_t ob = (int64_t)b * D;
   bool zv = false;
@@ -725,7 +733,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     if (col < D) {
       // trusted: no deep cancellation in the all-minus-removed difference, and the reliable mean within
       // 2 sigma of the shift c1 (moments about a far shift cancel like (dl^2 / mu2)^2)
-      const double rdl = r1 / n, rmu2 = r2 / n - rdl * rdl;
+      const double rdl = r1 * mk.in, rmu2 = r2 * mk.in - rdl * rdl;
       const double wc = (double)p.win_cancel;
       const bool good = r2 > 0.0 && a2 <= wc * r2 && a4 <= wc * r4 && rdl * rdl <= 4.0 * rmu2;
       if constexpr (LDSO) {
@@ -738,7 +746,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       if (good) {
         double dl;
         float sk, ku;
-        const bool nz = moments_from_sums_d(n, r1, r2, r3, r4, dl, sk, ku);
+        const bool nz = moments_from_sums_d(mk, r1, r2, r3, r4, dl, sk, ku);
         if constexpr (LDSO) {
           o_lds[D + col] = p.legacy ? 0.f : sk;
           o_lds[2 * D + col] = p.legacy ? 0.f : ku;
@@ -829,7 +837,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
       if (lane == 0) {
         double dl;
         float sk, ku;
-        const bool nz = moments_from_sums_d(n, c1s, t2, t3, t4, dl, sk, ku);
+        const bool nz = moments_from_sums_d(mk, c1s, t2, t3, t4, dl, sk, ku);
         if (CONS && ldso) {
           o_lds[D + col] = p.legacy ? 0.f : sk;
           o_lds[2 * D + col] = p.legacy ? 0.f : ku;
