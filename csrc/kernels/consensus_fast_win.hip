@@ -41,10 +41,16 @@ namespace svoc {
 // all-row sums' own relative error (~1e-6 worst case, ~1e-7 typical).
 
 SVOC_DEV u16x2 win_cand(u16x2 wt, u16x2 zt) {  // wt < zt ? wt : 0xFFFF, per 16-bit half
-  const u16x2 d = __builtin_elementwise_sub_sat(zt, wt);
-  const u16x2 one = {1, 1};
-  const u16x2 m = __builtin_elementwise_min(d, one) - one;  // 0 where wt < zt, 0xFFFF otherwise
-  return wt | m;
+  // four packed instructions (written with the elementwise builtins, LLVM split the halves into compares and
+  // selects: ~7 VALU per candidate, 20 candidates per column pair in pass 2)
+  const uint32_t one = 0x00010001u;
+  uint32_t d;
+  asm("v_pk_sub_u16 %0, %1, %2 clamp\n\t"
+      "v_pk_min_u16 %0, %0, %3\n\t"
+      "v_pk_sub_u16 %0, %0, %3"
+      : "=&v"(d)
+      : "v"(as_u32(zt)), "v"(as_u32(wt)), "v"(one));
+  return as_k(as_u32(wt) | d);   // d: 0 where wt < zt, 0xFFFF otherwise
 }
 
 // Skewness / sample-adjusted excess kurtosis (math.cairo:320-363) of n values from power sums of
