@@ -332,6 +332,11 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
                 rank_ok=[float(o) for o in per_rank[:, 1]], ok=dp.global_ok_fraction())
 
 
+def _enc_fp32_gemm() -> str:
+    from svoc.models import encoder
+    return encoder.FP32_GEMM
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -470,7 +475,11 @@ def main():
         out["config"]["alt_precision"] = {
             "encoder_dtype": "fp32", "value": rp["B"] * scale * args.steps / rp["elapsed"],
             "ms_per_step": 1e3 * rp["elapsed"] / args.steps, "ok_fraction": rp["ok"],
-            "path": "packed tokens, fp32 GEMMs (hipBLASLt), fp32 MFMA attention + fp32 LayerNorm kernels"}
+            "path": "packed tokens, fp32 MFMA attention + fp32 LayerNorm kernels, "
+                    + ("fp32 GEMMs as six bf16 products of three-way bf16 splits (fp32 accumulate; "
+                       "SVOC_FP32_GEMM=native: hipBLASLt fp32)" if _enc_fp32_gemm() == "bf16x6"
+                       else "fp32 GEMMs (hipBLASLt)"),
+            "fp32_gemm": _enc_fp32_gemm()}
         log_eng, log_step = rp["eng"], rp["step"]
     if rank == 0:
         print(json.dumps(out))

@@ -20,6 +20,7 @@ extern "C" int svoc_embed_layernorm_f32(const int64_t* ids, const int64_t* pos_i
                                         const float* typ, const float* w, const float* b, float* out, int64_t rows, int H,
                                         float eps, hipStream_t stream);
 extern "C" int svoc_segment_mean_f32(const float* x, const int* cu, float* out, int64_t B, int H, hipStream_t stream);
+extern "C" int svoc_split3_bf16(const float* x, void* out, int64_t rows, int K, int gelu, hipStream_t stream);
 extern "C" int svoc_attention_short_f32(const float* qkv, const void* kmask, const int* cu_seqlens, int64_t rows_total,
                                         float* out, int64_t B, int S, int H, int DH, hipStream_t stream);
 
@@ -145,6 +146,33 @@ at::Tensor segment_mean_hip(const at::Tensor& x, const at::Tensor& cu) {
   return out;
 }
 
+// [rows, K] fp32 -> [rows, 3K] bf16 planes [x0 | x1 | x2] of the three-way split (encoder_ops.hip
+// split3_bf16_kernel); gelu: RoBERTa's erf GELU first.  The CPU form is the reference of the same arithmetic.
+at::Tensor split3_ref(const at::Tensor& x, bool gelu) {
+  auto f = x.to(at::kFloat);
+  if (gelu) f = at::gelu(f);
+  auto x0 = f.to(at::kBFloat16);
+  auto r1 = f - x0.to(at::kFloat);
+  auto x1 = r1.to(at::kBFloat16);
+  auto x2 = (r1 - x1.to(at::kFloat)).to(at::kBFloat16);
+  return at::cat({x0, x1, x2}, -1);
+}
+
+at::Tensor split3_cpu(const at::Tensor& x, bool gelu) { return split3_ref(x, gelu); }
+
+at::Tensor split3_hip(const at::Tensor& x, bool gelu) {
+  TORCH_CHECK(x.dim() == 2, "split3: x must be [rows, K]");
+  TORCH_CHECK(x.scalar_type() == at::kFloat, "split3: fp32 input");
+  const int64_t rows = x.size(0), K = x.size(1);
+  if (K % 4 != 0) return split3_ref(x, gelu);
+  auto xc = x.contiguous();
+  auto out = at::empty({rows, 3 * K}, xc.options().dtype(at::kBFloat16));
+  const int rc = svoc_split3_bf16(xc.data_ptr<float>(), out.data_ptr(), rows, (int)K, gelu ? 1 : 0,
+                                  c10::hip::getCurrentHIPStream(x.device().index()).stream());
+  TORCH_CHECK(rc == 0, "svoc_split3_bf16 failed: ", rc);
+  return out;
+}
+
 }  // namespace
 
 void register_attention_defs(torch::Library& m);
@@ -156,18 +184,21 @@ void register_encoder_defs(torch::Library& m) {
   m.def("embed_layernorm(Tensor ids, Tensor pos_ids, Tensor tok, Tensor pos, Tensor typ, Tensor weight, Tensor bias, "
         "float eps) -> Tensor");
   m.def("segment_mean(Tensor x, Tensor cu_seqlens) -> Tensor");
+  m.def("split3(Tensor x, bool gelu) -> Tensor");
   register_attention_defs(m);
 }
 void register_encoder_cpu(torch::Library& m) {
   m.impl("add_layernorm", &add_layernorm_cpu);
   m.impl("embed_layernorm", &embed_layernorm_cpu);
   m.impl("segment_mean", &segment_mean_cpu);
+  m.impl("split3", &split3_cpu);
   register_attention_cpu(m);
 }
 void register_encoder_hip(torch::Library& m) {
   m.impl("add_layernorm", &add_layernorm_hip);
   m.impl("embed_layernorm", &embed_layernorm_hip);
   m.impl("segment_mean", &segment_mean_hip);
+  m.impl("split3", &split3_hip);
   register_attention_hip(m);
 }
 

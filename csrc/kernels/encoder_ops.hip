@@ -754,3 +754,57 @@ extern "C" int svoc_attention_short_f32(const float* qkv, const void* kmask, con
   }
   return (int)hipGetLastError();
 }
+
+// ---- fp32 GEMMs on the bf16 matrix cores: three-way split ------------------------------------------------
+// x = x0 + x1 + x2 with x0 = bf16(x), x1 = bf16(x - x0), x2 = bf16(x - x0 - x1) (each difference is exact in
+// fp32): 24 significant bits, the fp32 mantissa.  Row r of the output holds [x0 | x1 | x2] (3K bf16), so the
+// encoder's emulated fp32 linear (encoder.py _emul_linear) runs X W^T as three bf16 GEMMs with fp32 outputs,
+// [x0|x1|x2] [w0|w0|w0]^T + [x0|x1] [w1|w1]^T + x0 w2^T: the six products above 2^-24 (the dropped x1 w2,
+// x2 w1, x2 w2 are below it) at the bf16 MFMA rate, 16x the fp32 one on gfx950.  GELU = 1 applies RoBERTa's
+// erf GELU to x first (the FC1 output -> the FC2 input).  4 elements per thread: one 16-byte load, three
+// 8-byte stores.
+namespace svoc {
+
+template <bool GELU>
+__global__ __launch_bounds__(256) void split3_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ out,
+                                                          int64_t rows, int K) {
+  const int kq = K / 4;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= rows * kq) return;
+  const int64_t r = t / kq;
+  const int c = (int)(t - r * kq) * 4;
+  float4 v = *(const float4*)(x + r * K + c);
+  float a[4] = {v.x, v.y, v.z, v.w};
+  uint16_t h0[4], h1[4], h2[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float f = a[i];
+    if (GELU) f = 0.5f * f * (1.f + erff(f * 0.70710678118654752440f));
+    h0[i] = f2bf(f);
+    const float r1 = f - bf2f(h0[i]);
+    h1[i] = f2bf(r1);
+    h2[i] = f2bf(r1 - bf2f(h1[i]));
+  }
+  uint16_t* o = out + r * 3 * (int64_t)K + c;
+  auto pack = [](const uint16_t (&h)[4]) {
+    return make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16), (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+  };
+  *(uint2*)o = pack(h0);
+  *(uint2*)(o + K) = pack(h1);
+  *(uint2*)(o + 2 * K) = pack(h2);
+}
+
+}  // namespace svoc
+
+extern "C" int svoc_split3_bf16(const float* x, void* out, int64_t rows, int K, int gelu, hipStream_t stream) {
+  using namespace svoc;
+  if (rows <= 0) return 0;
+  if (K % 4 != 0 || K <= 0) return -1;
+  const int64_t n = rows * (K / 4);
+  const int64_t blocks = (n + 255) / 256;
+  if (blocks > 0x7fffffffll) return -1;
+  if (gelu) hipLaunchKernelGGL(split3_bf16_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, x, (uint16_t*)out, rows, K);
+  else hipLaunchKernelGGL(split3_bf16_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, x, (uint16_t*)out, rows, K);
+  return (int)hipGetLastError();
+}
+

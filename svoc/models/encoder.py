@@ -82,7 +82,13 @@ class Layer(nn.Module):
     def forward_packed(self, x: torch.Tensor, plan: "PackPlan") -> torch.Tensor:
         """x: [T, H] real tokens only (sequence b = rows [cu[b], cu[b+1]))."""
         from .. import ops as svops
-        a = svops.ops().attention_varlen(self.qkv(x), plan.cu, plan.max_len, self.heads)
+        o = svops.ops()
+        if _use_emul(x, self.qkv):   # fp32: every GEMM on the bf16 matrix cores (_emul_linear)
+            a = o.attention_varlen(_emul_linear(o.split3(x, False), self.qkv), plan.cu, plan.max_len, self.heads)
+            x = _add_ln(x, _emul_linear(o.split3(a, False), self.out), self.ln1)
+            h = _emul_linear(o.split3(x, False), self.fc1)
+            return _add_ln(x, _emul_linear(o.split3(h, True), self.fc2), self.ln2)   # (split3 applies the GELU)
+        a = o.attention_varlen(self.qkv(x), plan.cu, plan.max_len, self.heads)
         x = _add_ln(x, self.out(a), self.ln1)
         return _add_ln(x, self.fc2(_linear_gelu(x, self.fc1)), self.ln2)
 
@@ -118,6 +124,50 @@ def _linear_gelu(x: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
             y = torch.ops.aten.gelu_(torch.addmm(fc.bias, x2, fc.weight.t()))
         return y.view(*x.shape[:-1], -1)
     return F.gelu(fc(x))
+
+
+# fp32 weights on the GPU: SVOC_FP32_GEMM=bf16x6 runs the four per-layer linears as fp32 GEMMs emulated on
+# the bf16 matrix cores.  Both operands are split three ways into bf16 (encoder_ops.hip split3: x = x0 + x1 +
+# x2, 24 significant bits) and the six partial products above 2^-24 run as three bf16 GEMMs with fp32
+# accumulation and output: [x0|x1|x2] [w0|w0|w0]^T + [x0|x1] [w1|w1]^T + x0 w2^T -- the error of an fp32 GEMM
+# (tests/test_encoder_ops_gpu.py pins it against an fp64 reference next to the native fp32 GEMM's).  Not the
+# default: hipBLASLt runs these shapes at ~88 % of the fp32 matrix peak but the bf16 ones at 30-47 % of the
+# bf16 peak, so six bf16 products plus the splits measured slower (c4 fp32 262 vs 297 windows/s,
+# tools/probe_emul_gemm.py, docs/PERF.md).  "native" (default) = hipBLASLt fp32 GEMMs.
+FP32_GEMM = os.environ.get("SVOC_FP32_GEMM", "native")
+
+
+def _weight_planes(fc: nn.Linear):
+    """[w0|w0|w0], [w1|w1], w2 (bf16, [N, 3K] / [N, 2K] / [N, K]) of an fp32 Linear, cached on the module."""
+    w = fc.weight
+    key = (w.data_ptr(), w._version, w.device)
+    cached = getattr(fc, "_emul_planes", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    from .. import ops as svops
+    K = w.shape[1]
+    p = svops.ops().split3(w.detach(), False)
+    w0, w1, w2 = p[:, :K], p[:, K:2 * K], p[:, 2 * K:]
+    planes = (torch.cat([w0, w0, w0], 1).contiguous(), torch.cat([w1, w1], 1).contiguous(), w2.contiguous())
+    fc._emul_planes = (key, planes)
+    return planes
+
+
+def _emul_linear(xp: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
+    """fc(x) in fp32 from x's split planes xp = split3(x) ([M, 3K] bf16): three bf16 GEMMs, fp32 accumulate."""
+    b1, b2, b3 = _weight_planes(fc)
+    K = fc.weight.shape[1]
+    y = torch.mm(xp[:, :K], b3.t(), out_dtype=torch.float32)              # x0 w2
+    y = torch.addmm(y, xp[:, :2 * K], b2.t(), out_dtype=torch.float32)    # + x0 w1 + x1 w1
+    y = torch.addmm(y, xp, b1.t(), out_dtype=torch.float32)               # + x0 w0 + x1 w0 + x2 w0
+    if fc.bias is not None:
+        y.add_(fc.bias)
+    return y
+
+
+def _use_emul(x: torch.Tensor, fc: nn.Linear) -> bool:
+    return (FP32_GEMM == "bf16x6" and x.is_cuda and x.dtype == torch.float32 and fc.weight.dtype == torch.float32
+            and x.dim() == 2 and x.shape[1] % 4 == 0)
 
 
 def _add_ln(x: torch.Tensor, y: torch.Tensor, ln: nn.LayerNorm) -> torch.Tensor:

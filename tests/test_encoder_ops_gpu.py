@@ -264,3 +264,67 @@ def test_attention_varlen_f32_mfma():
     out = svops.ops().attention_varlen(qkv, cu, max(lens), heads)
     ref = svops.ops().attention_varlen(qkv.cpu().double(), cu.cpu(), max(lens), heads)
     torch.testing.assert_close(out.double().cpu(), ref, rtol=0, atol=2e-5)
+
+
+# ---------------------------------------------------------------- fp32 GEMMs on the bf16 matrix cores
+@pytest.mark.parametrize("gelu", [False, True])
+def test_split3_matches_cpu(gelu):
+    """The three-way bf16 split kernel vs its CPU reference: x0 + x1 + x2 reproduces x (or GELU(x)) to 2^-24."""
+    g = torch.Generator(device="cuda").manual_seed(3 + gelu)
+    x = 3 * torch.randn(1000, 768, device="cuda", generator=g)
+    p = svops.ops().split3(x, gelu)
+    assert p.shape == (1000, 3 * 768) and p.dtype == torch.bfloat16
+    pc = svops.ops().split3(x.cpu(), gelu)
+    rec = p[:, :768].double() + p[:, 768:1536].double() + p[:, 1536:].double()
+    if gelu:   # (the kernel's fp32 erf GELU vs aten's fp32 one; 1 + erf cancels for negative x: absolute bound)
+        torch.testing.assert_close(rec, F.gelu(x).double(), rtol=1e-6, atol=2e-7)
+    else:
+        assert ((rec - x.double()).abs() <= 2 ** -22 * x.double().abs()).all()
+    if not gelu:
+        assert torch.equal(p.cpu(), pc)
+    else:   # (device erff vs the CPU's: the leading plane may differ by one bf16 ulp on ties)
+        recc = pc[:, :768].double() + pc[:, 768:1536].double() + pc[:, 1536:].double()
+        torch.testing.assert_close(rec.cpu(), recc, rtol=1e-5, atol=2e-6)
+
+
+@pytest.mark.parametrize("M,K,N", [(2000, 768, 2304), (1500, 3072, 768), (333, 768, 3072)])
+def test_emul_linear_error_is_fp32_like(M, K, N):
+    """encoder._emul_linear (fp32 GEMM as six bf16 products, three bf16 GEMMs with fp32 accumulation) against an
+    fp64 reference, next to hipBLASLt's native fp32 GEMM: the same error scale."""
+    from svoc.models.encoder import _emul_linear
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    fc = torch.nn.Linear(K, N).cuda()
+    with torch.no_grad():
+        fc.weight.copy_(0.05 * torch.randn(N, K, device="cuda", generator=g))
+        fc.bias.copy_(0.1 * torch.randn(N, device="cuda", generator=g))
+    x = torch.randn(M, K, device="cuda", generator=g)
+    with torch.no_grad():
+        ref = torch.addmm(fc.bias.double(), x.double(), fc.weight.double().t())
+        native = torch.addmm(fc.bias, x, fc.weight.t())
+        emul = _emul_linear(svops.ops().split3(x, False), fc)
+    en = (native.double() - ref).abs().max().item()
+    ee = (emul.double() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    assert ee <= 2.0 * en + 1e-6 * scale, (ee, en, scale)
+    assert ee <= 1e-5 * scale, (ee, scale)
+
+
+def test_encoder_fp32_emul_matches_native():
+    """The fp32 encoder with every layer GEMM emulated on the bf16 matrix cores equals the native fp32 GEMM
+    encoder to fp32 rounding (oracle 6-vectors)."""
+    import svoc.models.encoder as enc_mod
+    from svoc.models.encoder import build, scores_to_oracle_vectors
+    enc = build("cuda", torch.float32, seed=21)
+    g = torch.Generator().manual_seed(9)
+    ids = torch.randint(3, enc.cfg.vocab_size, (6, 128), generator=g).cuda()
+    mask = (torch.arange(128)[None] < torch.tensor([128, 64, 7, 90, 33, 128])[:, None]).to(torch.int64).cuda()
+    old = enc_mod.FP32_GEMM
+    try:
+        with torch.no_grad():
+            enc_mod.FP32_GEMM = "native"
+            vn = scores_to_oracle_vectors(enc(ids, mask).cpu())
+            enc_mod.FP32_GEMM = "bf16x6"
+            ve = scores_to_oracle_vectors(enc(ids, mask).cpu())
+    finally:
+        enc_mod.FP32_GEMM = old
+    assert (vn - ve).abs().max().item() <= 2e-4
