@@ -313,8 +313,9 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(NSEG
       s3B += __shfl_xor(s3B, t * P); s4B += __shfl_xor(s4B, t * P);
     }
     if (seg == 0) {
-      const float k3 = n / ((n - 1.f) * (n - 2.f));
-      const float k4a = n * (n + 1.f) / (n - 1.f), k4b = 3.f * (n - 1.f) * (n - 1.f), k4c = (n - 2.f) * (n - 3.f);
+      // (the n-only factors once per slab, one division and one v_rsq per column: as consensus_fast_win.hip)
+      const float in = 1.f / n, k3 = n / ((n - 1.f) * (n - 2.f));
+      const float k4a = n * (n + 1.f) / (n - 1.f), k4b = 3.f * (n - 1.f) * (n - 1.f), ik4c = 1.f / ((n - 2.f) * (n - 3.f));
       bool zv = false;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -322,16 +323,16 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(NSEG
         if (!v) continue;
         const float s1 = h ? s1B : s1A, s2 = h ? s2B : s2A, s3 = h ? s3B : s3A, s4 = h ? s4B : s4A;
         const float sh = h ? shB : shA, med = h ? cB : cA;
-        const float dl = s1 / n, e2 = s2 / n, e3 = s3 / n, e4 = s4 / n;
+        const float dl = s1 * in, e2 = s2 * in, e3 = s3 * in, e4 = s4 * in;
         const float mu2 = e2 - dl * dl;
         const float mu3 = e3 - 3.f * dl * e2 + 2.f * dl * dl * dl;
         const float mu4 = e4 - 4.f * dl * e3 + 6.f * dl * dl * e2 - 3.f * dl * dl * dl * dl;
         float sk = 0.f, ku = 0.f;
         if (mu2 > 0.f) {
-          const float sd = sqrtf(mu2);
-          const float z3 = n * mu3 / (mu2 * sd), z4 = n * mu4 / (mu2 * mu2);
+          const float r = 1.f / mu2;
+          const float z3 = n * mu3 * r * __builtin_amdgcn_rsqf(mu2), z4 = n * mu4 * (r * r);
           sk = z3 * k3;
-          ku = (z4 * k4a - k4b) / k4c;
+          ku = (z4 * k4a - k4b) * ik4c;
         } else {
           zv = true;
         }
