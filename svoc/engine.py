@@ -333,7 +333,9 @@ class ConsensusEngine:
                 and self.cfg.constrained and 2 <= self.N <= 256 and 0 <= self.cfg.n_failing_oracles <= 32
                 and self.cfg.n_failing_oracles <= self.N - 2 and svops.fast_win_h(self.N, self.cfg.n_failing_oracles)
                 and 0 < U <= 256 and vals.dtype == self.vdtype and vals.dim() == 2 and vals.shape[1] == self.D
-                and oracle.dtype == torch.int64 and not self.cfg.legacy):
+                and oracle.dtype == torch.int64 and not self.cfg.legacy
+                # (the kernel's 32-bit batch offsets and 24-bit row-offset multiplies: svoc_fast_round_f32_win)
+                and U * self.D * 4 < (1 << 31) and self.ld * 4 < (1 << 24)):
             return False
         if not getattr(self, "_all_active", False):
             if torch.cuda.is_current_stream_capturing():
