@@ -183,6 +183,7 @@ RestoreParams make_restore_params(at::Tensor& values, at::Tensor& enabled, at::T
                        {&upd_status, "upd_status"}, {&saved, "saved"}, {&saved_en, "saved_en"}, {&status, "status"},
                        {&active, "active"}});
   RestoreParams p{};
+  p.inactive_status = -1;
   p.values = values.data_ptr();
   p.enabled = enabled.data_ptr<uint8_t>();
   p.n_active = n_active.data_ptr<int32_t>();
@@ -201,14 +202,20 @@ RestoreParams make_restore_params(at::Tensor& values, at::Tensor& enabled, at::T
 
 void restore_updates_cpu(at::Tensor values, at::Tensor enabled, at::Tensor n_active, const at::Tensor& inst,
                          const at::Tensor& oracle, at::Tensor upd_status, const at::Tensor& saved,
-                         const at::Tensor& saved_en, const at::Tensor& status, const at::Tensor& active) {
+                         const at::Tensor& saved_en, const at::Tensor& status, const at::Tensor& active,
+                         int64_t inactive_status) {
   RestoreParams p = make_restore_params(values, enabled, n_active, inst, oracle, upd_status, saved, saved_en, status,
                                         active);
   const int64_t row_bytes = (int64_t)p.D * p.elem_bytes;
   for (int64_t u = p.U - 1; u >= 0; --u) {   // reverse batch order (a slot updated twice: see apply)
     if (p.upd_status[u] != ST_OK) continue;
     const int64_t b = p.inst[u], o = p.oracle[u];
-    if (b < 0 || b >= p.B || o < 0 || o >= p.N || !p.active[b] || p.status[b] == ST_OK) continue;
+    if (b < 0 || b >= p.B || o < 0 || o >= p.N) continue;
+    if (!p.active[b]) {
+      if (inactive_status >= 0) p.upd_status[u] = (int32_t)inactive_status;
+      continue;
+    }
+    if (p.status[b] == ST_OK) continue;
     const uint8_t was = p.saved_en[u];
     if (was != kNotSaved) {
       std::memcpy((unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes,
@@ -224,9 +231,11 @@ void restore_updates_cpu(at::Tensor values, at::Tensor enabled, at::Tensor n_act
 
 void restore_updates_hip(at::Tensor values, at::Tensor enabled, at::Tensor n_active, const at::Tensor& inst,
                          const at::Tensor& oracle, at::Tensor upd_status, const at::Tensor& saved,
-                         const at::Tensor& saved_en, const at::Tensor& status, const at::Tensor& active) {
+                         const at::Tensor& saved_en, const at::Tensor& status, const at::Tensor& active,
+                         int64_t inactive_status) {
   RestoreParams p = make_restore_params(values, enabled, n_active, inst, oracle, upd_status, saved, saved_en, status,
                                         active);
+  p.inactive_status = (int)inactive_status;
   auto stream = c10::hip::getCurrentHIPStream(values.device().index()).stream();
   const int rc = svoc_restore_updates(&p, stream);
   TORCH_CHECK(rc == 0, "svoc_restore_updates failed: ", rc);
@@ -270,7 +279,7 @@ void register_extra_defs(torch::Library& m) {
       "Tensor(g!)? saved=None, Tensor(h!)? saved_en=None) -> ()");
   m.def(
       "restore_updates(Tensor(a!) values, Tensor(b!) enabled, Tensor(c!) n_active, Tensor inst, Tensor oracle, "
-      "Tensor(d!) upd_status, Tensor saved, Tensor saved_en, Tensor status, Tensor active) -> ()");
+      "Tensor(d!) upd_status, Tensor saved, Tensor saved_en, Tensor status, Tensor active, int inactive_status=-1) -> ()");
   m.def("commit_updates(Tensor rows, Tensor oracle, Tensor upd_status, Tensor(a!) values, int upd_per_inst) -> ()");
   register_governance_defs(m);
   register_generator_defs(m);

@@ -273,6 +273,7 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
       // instance-grouped batch: update u belongs to instance u / U
       at::Tensor inst = at::arange(n, upd_oracle->options()).div(upd_per_inst, "floor");
       RestoreParams r{};
+      r.inactive_status = -1;
       r.values = values.data_ptr();
       r.enabled = rst_enabled->data_ptr<uint8_t>();
       r.n_active = rst_n_active->data_ptr<int32_t>();

@@ -191,6 +191,9 @@ struct RestoreParams {
   const uint8_t* active;    // [B] the round ran
   int64_t inst_stride;
   int B, N, D, ld, U, elem_bytes;
+  // >= 0: an applied update whose instance did not run its round (not fully active) gets this status (the exact
+  // engine's per-update transactions report NOT_ACTIVE, the update stays stored); -1: it keeps OK
+  int inactive_status;
 };
 
 }  // namespace svoc

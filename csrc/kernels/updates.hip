@@ -328,7 +328,11 @@ __global__ __launch_bounds__(256) void upd_restore_kernel(RestoreParams p) {
     const int64_t b = p.inst[u], o = p.oracle[u];
     if (b < 0 || b >= p.B || o < 0 || o >= p.N) continue;
     const int rst = p.status[b];
-    if (!p.active[b] || rst == ST_OK) continue;
+    if (!p.active[b]) {
+      if (p.inactive_status >= 0) p.upd_status[u] = p.inactive_status;
+      continue;
+    }
+    if (rst == ST_OK) continue;
     const uint8_t was = p.saved_en[u];
     if (was != kNotSaved) {
       unsigned char* dst = (unsigned char*)p.values + (b * p.inst_stride + o * p.ld) * p.elem_bytes;

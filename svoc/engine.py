@@ -590,6 +590,8 @@ class ConsensusEngine:
                 lay = inst == torch.arange(U, device=self.device) // K
                 if not bool((lay | ~okl).all()):
                     K = 0
+            if K and self.device.type == "cuda":
+                return self._exact_transactions_k(inst, oracle, vals, K, out)
             waves = [torch.arange(k, U, K, device=self.device) for k in range(K)]
         else:
             order, bounds = self._transaction_waves(inst, oracle)
@@ -627,6 +629,29 @@ class ConsensusEngine:
             self.enabled[bi_c, oi_c] = torch.where(revert, old_en, self.enabled[bi_c, oi_c])
             self.n_active[bi_c] = torch.where(revert, old_na, self.n_active[bi_c])
             out[sel] = tx
+        return out
+
+    def _exact_transactions_k(self, inst, oracle, vals, K: int, out: torch.Tensor) -> torch.Tensor:
+        """_exact_transactions for the b * K + k layout on the GPU, with the transaction bookkeeping in the update
+        and restore kernels: per wave the update kernel validates, saves the overwritten row / ``enabled`` flag
+        and stores (one launch), the round runs, and the restore kernel rolls back the transactions whose round
+        reverted and gives every applied update its transaction status -- the round's code, NOT_ACTIVE where the
+        instance is not fully active (the update stays stored), OK otherwise.  The per-wave gathers, compares,
+        ``where`` selects and scatters of the general path (~20 small kernels, ~10 % of a c3 wave) go away; the
+        batch is reordered wave-major once."""
+        n = inst.numel() // K
+        iw = inst.view(n, K).t().contiguous()                 # [K, n]: wave k = the k-th update of every instance
+        ow = oracle.view(n, K).t().contiguous()
+        vw = vals.reshape(n, K, -1).transpose(0, 1).contiguous()
+        sw = torch.empty(K, n, dtype=torch.int32, device=self.device)
+        sv, sen, _ = self._save_buffer(("exact_tx",), n)
+        for k in range(K):
+            self.touched.zero_()
+            self.apply_updates(iw[k], ow[k], vw[k], unique=True, save=(sv, sen, sw[k]))
+            self.run_round(only_touched=True)                 # outputs are only written when a round succeeds
+            self._ops.restore_updates(self.values, self.enabled, self.n_active, iw[k], ow[k], sw[k], sv, sen,
+                                      self.status, self._active, int(Status.NOT_ACTIVE))
+        out.copy_(sw.t().reshape(-1))
         return out
 
     # ------------------------------------------------------------------ synthetic data
