@@ -91,6 +91,10 @@ SVOC_HD double wmul_pos_h(double a, double b) { return floor(fma(a, b, 500000.5)
 // absolute value is a free source modifier of v_fma_f64 and the sign goes back with one in-place v_bfi_b32,
 // where copysign(hb, A) as the addend needed a v_bfi_b32 plus a v_mov_b32 for the pair's low word.)
 SVOC_HD double tdiv_h(double A, double ib, double hb) { return copysign(trunc(fma(fabs(A), ib, hb)), A); }
+// wsad_mul(a, b) of either sign without the caller's sign test: I128Div(t, 1e6) of the exact t = a b + 500000 by
+// tdiv_h (the half offset follows t's sign, which is what truncation toward zero needs) -- for |a b| < 2^51 - 2^19.
+// One fma more, but no compare / select / register copy per product (wmul_h's offset pair).
+SVOC_HD double wmul_t(double a, double b) { return tdiv_h(fma(a, b, 500000.0), kInv6, 0.5 * kInv6); }
 SVOC_HD double wdiv_h(double a, double b) {
   const double ib = 1.0 / b;
   return tdiv_h(fma(a, kW, floor(b * 0.5)), ib, 0.5 * ib);

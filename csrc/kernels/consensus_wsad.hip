@@ -748,11 +748,17 @@ void consensus_wsad_kernel(ExactParams p) {
     __syncthreads();
     const int a = N / 2 - R / 2;
     const int wb = WINH - a - 1;   // window index of position R/2 - 1 (>= 0: launch_wsad_c checked)
+    // f <= 2 WINH - 2 (launch_wsad_c: f - a + 1 <= WINH with a >= f / 2): only the first 2 WINH - 2 slots can
+    // hold removed keys, the rest are +inf -- sorted as a 32- (8-) key network instead of the 64-key one with
+    // 34 (10) runtime slots
+    constexpr int NR = 2 * WINH - 2;
+    constexpr int SN = NR <= 8 ? 8 : 32;
+    static_assert(WINH == 0 || NR <= SN, "removed-key slots");
     for (int col = tid; col < D; col += NT) {
-      uint32_t z[64];
+      uint32_t z[SN];
 #pragma unroll
-      for (int t = 0; t < 64; ++t) {
-        if (t < 2 * WINH) {
+      for (int t = 0; t < SN; ++t) {
+        if (t < NR) {
           const int ur = __builtin_amdgcn_readfirstlane(urow[t < f ? t : 0]);
           const uint32_t x = bload(rs, col * ESZ, ur * rowb);
           z[t] = t < f ? x : ~0u;   // u_f.. = +inf
@@ -760,7 +766,7 @@ void consensus_wsad_kernel(ExactParams p) {
           z[t] = ~0u;
         }
       }
-      sort_oem<64>(z);
+      sort_oem<SN>(z);
       uint32_t gw[2 * WINH];
 #pragma unroll
       for (int t = 0; t < 2 * WINH; ++t) {
@@ -770,9 +776,10 @@ void consensus_wsad_kernel(ExactParams p) {
       uint32_t lo = ~0u, hi = ~0u;
 #pragma unroll
       for (int j = 0; j + 1 < 2 * WINH; ++j) {
+        const uint32_t zj = j < SN ? z[j < SN ? j : 0] : ~0u;   // (slot NR = 2 WINH - 2: +inf)
         if (j <= f) {   // (uniform)
-          lo = kmin(lo, gw[j] < z[j] ? gw[j] : ~0u);
-          hi = kmin(hi, gw[j + 1] < z[j] ? gw[j + 1] : ~0u);
+          lo = kmin(lo, gw[j] < zj ? gw[j] : ~0u);
+          hi = kmin(hi, gw[j + 1] < zj ? gw[j + 1] : ~0u);
         }
       }
       stg[D + col] = (int32_t)((lo + hi) >> 1);
@@ -967,7 +974,7 @@ void consensus_wsad_kernel(ExactParams p) {
       const double z = tdiv_h(fma(xv(xm), kWs, C0), isd, hisd);
       const double z2 = wmul_pos_h(z, z);
       outl = outl || !(z2 < 33554432.0);   // 2^25: keeps z^2 z and z^2 z^2 below the forms' 2.25e9 quotients
-      s3 += wmul_h(z2, z, z < 0.0);
+      s3 += wmul_t(z2, z);
       s4 += wmul_pos_h(z2, z2);
     };
     if constexpr (BATCH || (WINH > 0 && BATCH1) || !CONS) {
@@ -1014,7 +1021,7 @@ void consensus_wsad_kernel(ExactParams p) {
           const double z = tdiv_h(fma(xv(xm), kW, C0), isd, hisd);
           const double z2 = wmul_pos_h(z, z);
           if (z2 < 33554432.0) {
-            s3 += wmul_h(z2, z, z < 0.0);
+            s3 += wmul_t(z2, z);
             s4 += wmul_pos_h(z2, z2);
           } else {
             const int64_t zi = (int64_t)z, z2i = (int64_t)z2;

@@ -215,10 +215,12 @@ static void wsad_half_paths() {
     const int64_t z = uni(-5800000, 5800000), z2 = uni(0, (1 << 25) - 1);
     if ((int64_t)wmul_pos_h((double)z, (double)z) != (int64_t)wmul(z, z, st)) ++bad;
     if ((int64_t)wmul_h((double)z2, (double)z, z < 0) != (int64_t)wmul(z2, z, st)) ++bad;
+    if ((int64_t)wmul_t((double)z2, (double)z) != (int64_t)wmul(z2, z, st)) ++bad;
     if ((int64_t)wmul_pos_h((double)z2, (double)z2) != (int64_t)wmul(z2, z2, st)) ++bad;
     // small products of either sign (a b + 500000 changes sign)
     const int64_t a = uni(-2000, 2000), b = uni(-2000, 2000);
     if ((int64_t)wmul_h((double)a, (double)b, a * b < 0) != (int64_t)wmul(a, b, st)) ++bad;
+    if ((int64_t)wmul_t((double)a, (double)b) != (int64_t)wmul(a, b, st)) ++bad;
     // wsad_div by a standard deviation, |a| < 2^26, b up to 2^31
     const int64_t num = it & 2 ? uni(-1000000, 1000000) : uni(-(1 << 26), 1 << 26);
     const int64_t sd = it & 4 ? uni(1, 2000000) : uni(1, (1ll << 31) - 1);
@@ -247,6 +249,8 @@ static void wsad_half_paths() {
       int st = ST_OK;
       CHECK((int64_t)wmul_pos_h((double)t, 1.0) == (int64_t)wmul(t, 1, st));
       CHECK((int64_t)wmul_h((double)-t, 1.0, true) == (int64_t)wmul(-t, 1, st));
+      CHECK((int64_t)wmul_t((double)-t, 1.0) == (int64_t)wmul(-t, 1, st));
+      CHECK((int64_t)wmul_t((double)t, 1.0) == (int64_t)wmul(t, 1, st));
     }
   }
 }
