@@ -265,3 +265,28 @@ def test_kernels_reject_host_index_tensors():
     with pytest.raises(RuntimeError, match="must be on|device"):
         o.apply_updates(e.values, e.enabled, e.n_active, e.touched, e._winner, torch.tensor([0, 1]),
                         torch.tensor([0, 1], device="cuda"), rows, True, st, True, None, None)
+
+
+def test_restore_kernel_inactive_status_cpu_twin():
+    """restore_updates (the CPU twin of updates.hip upd_restore_kernel): reverted instances get their rows, enabled
+    flag and n_active back and the round's code; with inactive_status >= 0 the updates of an instance whose round
+    did not run keep their row and report that status (the exact engine's NOT_ACTIVE); -1 keeps OK."""
+    from svoc import ops as svops
+    B, N, D = 3, 4, 2
+    vals = torch.arange(B * N * D, dtype=torch.int32).reshape(B, N, D).clone()
+    enabled = torch.ones(B, N, dtype=torch.uint8)
+    enabled[2, 1] = 0
+    n_active = enabled.sum(1).to(torch.int32)
+    inst = torch.tensor([0, 1, 2], dtype=torch.int64)
+    oracle = torch.tensor([1, 2, 3], dtype=torch.int64)
+    saved = torch.full((3, D), -7, dtype=torch.int32)
+    saved_en = torch.tensor([1, 0, 1], dtype=torch.uint8)
+    status = torch.tensor([int(Status.OK), int(Status.DIV_BY_ZERO), int(Status.OK)], dtype=torch.int32)
+    active = torch.tensor([1, 1, 0], dtype=torch.uint8)   # instance 2: not fully active, no round
+    for inactive, want2 in ((-1, int(Status.OK)), (int(Status.NOT_ACTIVE), int(Status.NOT_ACTIVE))):
+        v, en, na = vals.clone(), enabled.clone(), n_active.clone()
+        st = torch.zeros(3, dtype=torch.int32)
+        svops.ops().restore_updates(v, en, na, inst, oracle, st, saved, saved_en, status, active, inactive)
+        assert st.tolist() == [int(Status.OK), int(Status.DIV_BY_ZERO), want2]
+        assert v[1, 2].tolist() == [-7, -7] and int(en[1, 2]) == 0 and int(na[1]) == n_active[1] - 1
+        assert torch.equal(v[0], vals[0]) and torch.equal(v[2], vals[2])
