@@ -303,7 +303,6 @@ void consensus_wsad_kernel(ExactParams p) {
   // still reads 32 / 16 contiguous bytes per row, and the tile's per-slab barriers cost more than they save:
   // 512 x 2048 ran 85 k rounds/s direct, 62 k through the tile)
   constexpr bool TILE = WIDE && NSEG >= 32;
-  static_assert(!TILE || CONS || V32, "the tile keeps low words only: unconstrained int64 rounds need their high words");
   constexpr int TROW = NPAD + NPAD / 64;
   __shared__ uint32_t tile[TILE ? W * TROW : 1];
   __shared__ uint64_t qr_lds[NPAD];
@@ -367,7 +366,21 @@ void consensus_wsad_kernel(ExactParams p) {
         tile[(part * 2 + 0) * TROW + pr] = w.x;
         tile[(part * 2 + 1) * TROW + pr] = w.z;
         const int c = c0 + part * 2;
-        badv |= ((c < D && w.y != 0u) || (c + 1 < D && w.w != 0u)) ? 1u : 0u;   // constrained: [0, 1e6]
+        if constexpr (CONS) {
+          badv |= ((c < D && w.y != 0u) || (c + 1 < D && w.w != 0u)) ? 1u : 0u;   // constrained: [0, 1e6]
+        } else {
+          // unconstrained: the high words are checked here, against the columns' row-0 values (the base B;
+          // the same vector of row 0, an L1 hit): x - B must be the sign extension of its low word and
+          // within [-2^30, 2^30) -- the tile then holds everything the round reads
+          const uint4 b0 = (c0 * ESZ + part * 16 < D * ESZ)
+                               ? __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, c0 * ESZ + part * 16, 0, 0))
+                               : make_uint4(0u, 0u, 0u, 0u);
+          auto bad64 = [](uint32_t l, uint32_t h, uint32_t bl, uint32_t bh) __attribute__((always_inline)) {
+            const uint32_t rl = l - bl, rh = h - bh - (l < bl ? 1u : 0u);
+            return !(rh == (uint32_t)((int32_t)rl >> 31) && rl + (1u << 30) < (1u << 31));
+          };
+          badv |= ((c < D && bad64(w.x, w.y, b0.x, b0.y)) || (c + 1 < D && bad64(w.z, w.w, b0.z, b0.w))) ? 1u : 0u;
+        }
       }
     }
     __syncthreads();
@@ -1102,21 +1115,14 @@ static int launch_wsad_c(const ExactParams& p, hipStream_t stream) {
   hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   return (int)hipGetLastError();
 }
-// N > 256: whole rounds on the wide lane groups (the binding sized the stage for win_h = 0); unconstrained
-// int64 rounds at 32 / 64 lanes per column (the tiled groups) go to the i128 kernel
+// N > 256: whole rounds on the wide lane groups (the binding sized the stage for win_h = 0)
 template <int NSEG>
 static int launch_wide(const ExactParams& p, hipStream_t stream) {
   constexpr int WAVES = 4;
   if (p.win_h != 0) return -3;
   auto k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 0, true> : consensus_wsad_kernel<NSEG, WAVES, false, 0, true>;
-  if (!p.constrained) {
-    if constexpr (NSEG >= 32) {
-      if (!p.val32) return -2;
-      k = consensus_wsad_kernel<NSEG, WAVES, true, 0, false>;
-    } else {
-      k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 0, false> : consensus_wsad_kernel<NSEG, WAVES, false, 0, false>;
-    }
-  }
+  if (!p.constrained)
+    k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 0, false> : consensus_wsad_kernel<NSEG, WAVES, false, 0, false>;
   hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   return (int)hipGetLastError();
 }
