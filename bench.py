@@ -225,9 +225,11 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
             else:
                 eng.apply_updates(inst, orc, vals, unique=True)
                 run_round()
-        else:
+        elif dshard:
             eng.touched.fill_(1)
             run_round()
+        else:   # every active instance runs a round (the prologue ignores `touched`: no fill per step)
+            eng.run_round(only_touched=False)
         if gov is not None:
             gov.submit_tensors(*gov_batches[i % len(gov_batches)])
 
@@ -259,8 +261,12 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
         # (pipelined: a graph of at least 4 steps, so 3 of 4 step boundaries overlap; a pool of >= 4 steps
         # already overlaps all but one)
         sp = stream.pool if stream is not None else 1
+        # (whole-batch rounds without a stream -- c2, the wide configs: every step is the same round of every
+        # instance, so one graph holds up to 20 of them, as the streamed configs' graph holds its pool: the
+        # metrics reduce runs once per replay either way)
+        same = max(1, min(args.steps, 20)) if (stream is None and pipe is None and gov is None) else 1
         for k in (sp, len(gov_batches) if gov is not None else 1,
-                  2 if pipe is not None else 1, 4 if (pipeline > 1 and sp < 4) else 1):
+                  2 if pipe is not None else 1, 4 if (pipeline > 1 and sp < 4) else 1, same):
             period = period * k // math.gcd(period, k)
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream(dev))
@@ -280,6 +286,7 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
                     step(i)
                 join()   # every forked stream rejoins the capture stream
             graph_period = period
+            extra["graph_steps"] = period
         except Exception as e:  # graph capture is an optimisation; eager stays correct
             if rank == 0:
                 print(f"[bench] graph capture failed ({e}); running eager", file=sys.stderr)

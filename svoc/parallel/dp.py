@@ -29,6 +29,9 @@ class DataParallelConsensus:
         # [rel2 sum over committed rounds, committed rounds, processed rounds, reverted rounds]
         self._fx = torch.zeros(4, dtype=torch.int64, device=dev)
         self._global = torch.zeros(4, dtype=torch.float64, device=dev)
+        # fixed-point scale of the rel2 sum (fast: 2^-32, exact: 1e-6); the other counters are integers
+        fx_scale = (2.0 ** -32) if getattr(engine, "mode", "fast") == "fast" else 1e-6
+        self._scale = torch.tensor([fx_scale, 1.0, 1.0, 1.0], dtype=torch.float64, device=dev)
 
     # -- sharding ---------------------------------------------------------------------------------
     def global_ids(self) -> torch.Tensor:
@@ -48,11 +51,13 @@ class DataParallelConsensus:
         [sum rel2 of committed rounds, committed, processed, reverted]."""
         e = self.engine
         e.pipeline_join()
-        self._fx.copy_(e.metrics_fx)
+        src = e.metrics_fx
         if self.world > 1:
+            self._fx.copy_(src)
             dist.all_reduce(self._fx, op=dist.ReduceOp.SUM, group=self.group)
-        self._global.copy_(self._fx)
-        self._global[0] *= (2.0 ** -32) if e.mode == "fast" else 1e-6
+            src = self._fx
+        # one elementwise kernel: int64 counters -> float64, rel2 sum scaled (the 4-element tail of a step)
+        torch.mul(src, self._scale, out=self._global)
         return self._global
 
     def step_metrics(self) -> None:
