@@ -7,8 +7,9 @@ Configs (BASELINE.json):
   c3 (default): 256 oracles x 4096 dims, streaming updates with failing-oracle masking, DP over
       independent instances.  One step on every rank = a batch of fresh predictions from 1/4 of the
       oracles of every local instance (synthetic stream, pre-generated in HBM, cycled) scattered into
-      the state + one full two-pass consensus round per instance (fused HIP kernel) + an RCCL
-      all-reduce of the step's health metrics (reliability sum, OK count).  Storage: fp32 -- the
+      the state + one full two-pass consensus round per instance (fused HIP kernel).  The step's
+      health metrics (reliability sum, OK count) are folded on the device every step and all-reduced
+      over RCCL once per graph replay (``graph_steps`` steps, reported on the line).  Storage: fp32 -- the
       reference computes on the 1e-6 wsad grid (contract/src/signed_decimal.cairo:82-83) and fp32 holds
       every grid value of [0, 1] exactly; the bf16-storage step is measured too and reported as the
       extra field ``config.alt_storage``.
@@ -97,7 +98,7 @@ def _dtype_name(mode: str, storage: str, c: dict) -> str:
     return {"fp32": "fp32", "bf16": "bf16"}.get(storage, c.get("dtype", "bf16"))
 
 
-def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
+def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None, enc_pool=None):
     """Build the engine + update source for one storage dtype, warm up, time exactly args.steps steps
     (barrier + device sync on both sides) and gather every rank's time and round outcomes."""
     from svoc.config import ConsensusConfig
@@ -139,11 +140,13 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
         from svoc.models import corpus
         from svoc.models.sentiment_oracle import SentimentOraclePipeline
         enc = None
-        if enc_dtype is not None:
+        if enc_dtype is not None or enc_pool is not None:
             # the reference's precision (HF pipeline, fp32 weights: oracle_scheduler.py:23-25): fp32 GEMMs over the
-            # packed tokens, the fp32 encoder kernels (mfma_f32_32x32x2_f32 attention, fp32 LayerNorms)
+            # packed tokens, the fp32 encoder kernels (mfma_f32_32x32x2_f32 attention, fp32 LayerNorms); or the
+            # reference's classifier head (RobertaClassificationHead on the <s> state: pool="cls")
+            from svoc.models.encoder import EncoderConfig
             from svoc.models.encoder import build as build_encoder
-            enc = build_encoder(dev, enc_dtype, 0)
+            enc = build_encoder(dev, enc_dtype or torch.bfloat16, 0, EncoderConfig(pool=enc_pool or "mean"))
         pipe = SentimentOraclePipeline(eng, encoder=enc, seed=0)
         from svoc.models import encoder as _encm
         extra["encoder_pool"] = pipe.encoder.cfg.pool
@@ -237,7 +240,7 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None):
         if dshard:
             flush_sharded(eng, world=world)
 
-    def step_metrics():   # DP: one all-reduce of the round counters per step (D-shard: every rank
+    def step_metrics():   # DP: one all-reduce of the round counters per call -- per graph replay (D-shard: every rank
         if not dshard:    # commits the same rounds, so the counters are reduced once, after the loop)
             dp.reduce()
 
@@ -488,6 +491,17 @@ def main():
                        else "fp32 GEMMs (hipBLASLt)"),
             "fp32_gemm": _enc_fp32_gemm()}
         log_eng, log_step = rp["eng"], rp["step"]
+    if args.config == "c4" and dev.type == "cuda":
+        # the reference's head (client/oracle_scheduler.py:23-40: the <s> state through the classification
+        # head, SamLowe/roberta-base-go_emotions) -- same encoder, <s> pooling instead of the masked mean
+        r = eng = None
+        log_eng = log_step = None
+        torch.cuda.empty_cache()
+        rc = measure(args, c, storage, dev, rank, world, dshard, enc_pool="cls")
+        out["config"]["cls_pool"] = {
+            "encoder_pool": "cls", "value": rc["B"] * scale * args.steps / rc["elapsed"],
+            "ms_per_step": 1e3 * rc["elapsed"] / args.steps, "ok_fraction": rc["ok"]}
+        log_eng, log_step = rc["eng"], rc["step"]
     if rank == 0:
         print(json.dumps(out))
         if args.log:

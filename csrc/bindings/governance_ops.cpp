@@ -67,6 +67,32 @@ void governance_hip(const at::Tensor& admins, at::Tensor oracle_addr, at::Tensor
   TORCH_CHECK(rc == 0, "svoc_governance failed: ", rc);
 }
 
+// Ordered batches: any number of actions per instance, applied in submission order per instance.  `order`:
+// the action indices sorted stably by instance (Governance.submit_batch sorts on the device).
+void governance_seq_cpu(const at::Tensor& admins, at::Tensor oracle_addr, at::Tensor votes, at::Tensor prop_tag,
+                        at::Tensor prop_idx, at::Tensor prop_addr, const at::Tensor& inst, const at::Tensor& caller,
+                        const at::Tensor& kind, const at::Tensor& arg0, const at::Tensor& arg1, const at::Tensor& addr,
+                        bool enable, int64_t majority, const at::Tensor& order, at::Tensor status, at::Tensor applied) {
+  (void)order;   // the CPU applies the whole list in order (instances are independent)
+  governance_cpu(admins, oracle_addr, votes, prop_tag, prop_idx, prop_addr, inst, caller, kind, arg0, arg1, addr,
+                 enable, majority, status, applied);
+}
+
+void governance_seq_hip(const at::Tensor& admins, at::Tensor oracle_addr, at::Tensor votes, at::Tensor prop_tag,
+                        at::Tensor prop_idx, at::Tensor prop_addr, const at::Tensor& inst, const at::Tensor& caller,
+                        const at::Tensor& kind, const at::Tensor& arg0, const at::Tensor& arg1, const at::Tensor& addr,
+                        bool enable, int64_t majority, const at::Tensor& order, at::Tensor status, at::Tensor applied) {
+  GovState g{}; GovAction a{};
+  prep(admins, oracle_addr, votes, prop_tag, prop_idx, prop_addr, inst, caller, kind, arg0, arg1, addr, status,
+       applied, enable, majority, g, a);
+  TORCH_CHECK(order.scalar_type() == at::kLong && order.is_contiguous() && order.numel() == inst.numel(),
+              "order: contiguous int64 [K]");
+  a.order = order.data_ptr<int64_t>();
+  auto stream = c10::hip::getCurrentHIPStream(admins.device().index()).stream();
+  const int rc = svoc_governance(&g, &a, stream);
+  TORCH_CHECK(rc == 0, "svoc_governance failed: ", rc);
+}
+
 }  // namespace
 
 void register_governance_defs(torch::Library& m) {
@@ -74,8 +100,19 @@ void register_governance_defs(torch::Library& m) {
       "governance(Tensor admins, Tensor(a!) oracle_addr, Tensor(b!) votes, Tensor(c!) prop_tag, "
       "Tensor(d!) prop_idx, Tensor(e!) prop_addr, Tensor inst, Tensor caller, Tensor kind, Tensor arg0, "
       "Tensor arg1, Tensor addr, bool enable, int majority, Tensor(f!) status, Tensor(g!) applied) -> ()");
+  m.def(
+      "governance_seq(Tensor admins, Tensor(a!) oracle_addr, Tensor(b!) votes, Tensor(c!) prop_tag, "
+      "Tensor(d!) prop_idx, Tensor(e!) prop_addr, Tensor inst, Tensor caller, Tensor kind, Tensor arg0, "
+      "Tensor arg1, Tensor addr, bool enable, int majority, Tensor order, Tensor(f!) status, "
+      "Tensor(g!) applied) -> ()");
 }
-void register_governance_cpu(torch::Library& m) { m.impl("governance", &governance_cpu); }
-void register_governance_hip(torch::Library& m) { m.impl("governance", &governance_hip); }
+void register_governance_cpu(torch::Library& m) {
+  m.impl("governance", &governance_cpu);
+  m.impl("governance_seq", &governance_seq_cpu);
+}
+void register_governance_hip(torch::Library& m) {
+  m.impl("governance", &governance_hip);
+  m.impl("governance_seq", &governance_seq_hip);
+}
 
 }  // namespace svoc

@@ -233,6 +233,8 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
     TORCH_CHECK(mode == 0 && upd_per_inst > 0 && upd_oracle.has_value() && upd_status.has_value() &&
                     rst_saved_en.has_value() && rst_enabled.has_value() && rst_n_active.has_value(),
                 "rst_saved: mode 0, with upd_oracle, upd_status, upd_per_inst, rst_saved_en, rst_enabled, rst_n_active");
+    // (checked before any launch: the rc == -3 fallback below needs it after the plain round has run)
+    TORCH_CHECK(active.has_value() && active->defined(), "rst_saved: needs the round's active mask");
     const int64_t n = B * upd_per_inst;
     TORCH_CHECK(rst_saved->scalar_type() == values.scalar_type() && rst_saved->is_contiguous() &&
                     rst_saved->dim() == 2 && rst_saved->size(0) == n && rst_saved->size(1) == D,
@@ -269,7 +271,6 @@ void fast_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& a
       p.rst_U = 0;
       const int rc2 = f32 ? svoc_fast_round_f32(&p, stream) : svoc_fast_round_bf16(&p, stream);
       TORCH_CHECK(rc2 == 0, f32 ? "svoc_fast_round_f32" : "svoc_fast_round_bf16", " launch failed: ", rc2);
-      TORCH_CHECK(active.has_value() && active->defined(), "rollback fallback: needs the round's active mask");
       // instance-grouped batch: update u belongs to instance u / U
       at::Tensor inst = at::arange(n, upd_oracle->options()).div(upd_per_inst, "floor");
       RestoreParams r{};

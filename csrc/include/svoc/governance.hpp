@@ -37,6 +37,9 @@ struct GovAction {         // batched actions, one per instance in a launch
   int32_t* status;         // [K]
   uint8_t* applied;        // [K] replacement applied by this vote
   int K;
+  // ordered batches (any number of actions per instance): the action indices sorted stably by instance, so
+  // each instance's actions form one run in submission order (nullptr: one action per instance)
+  const int64_t* order;
 };
 
 SVOC_HD bool addr_eq(const int64_t* a, const int64_t* b) {

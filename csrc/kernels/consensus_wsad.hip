@@ -440,7 +440,9 @@ void consensus_wsad_kernel(ExactParams p) {
         const uint32_t w = TILE ? tl(i) : bload(rs, vo, i * rowb1);
         const uint32_t x = w - Bl;   // (unconstrained: relative to B)
         const bool real = i < nvf;
-        if constexpr (CONS) wmax = __builtin_elementwise_max(wmax, w);
+        // (rows past N: the non-tiled load reads 0 out of bounds, but the LDS tile's padding rows hold
+        // leftover words -- masked, or they would send the instance to the i128 kernel at random)
+        if constexpr (CONS) wmax = __builtin_elementwise_max(wmax, (FULL || !TILE) ? w : (w & lt_mask(i, nvf)));
         if constexpr (!CONS && V32) {
           const int32_t ws = FULL ? (int32_t)w : (int32_t)((w & lt_mask(i, nvf)) | (Bl & ~lt_mask(i, nvf)));
           smax = __builtin_elementwise_max(smax, ws);

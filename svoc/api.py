@@ -62,8 +62,20 @@ class ConsensusService:
         return out
 
     def governance(self, actions) -> Tuple[List[Status], List[bool]]:
+        """update_proposition / vote_for_a_proposition transactions (contract.cairo:661-738).  ``actions``: a list
+        of ("propose", inst, caller, (oracle_idx, new_address) | None) / ("vote", inst, caller, which_admin,
+        support) tuples -> (statuses, applied) lists; or a mapping of action tensors (``inst``, ``caller``,
+        ``kind``, ``arg0``, ``arg1``, ``addr``: see :meth:`Governance.submit_batch`) -> (status [K], applied [K])
+        device tensors, with no host work (one device sort + one launch)."""
+        if isinstance(actions, dict):
+            return self.governance_batch(**actions)
         st, ap = self.gov.submit(actions)
         return [Status(s) for s in st.cpu().tolist()], [bool(a) for a in ap.cpu().tolist()]
+
+    def governance_batch(self, inst, caller, kind, arg0, arg1, addr) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Tensor form of :meth:`governance` (any number of actions per instance, submission order per
+        instance): status [K] int32 (svoc.status.Status codes) and applied [K] uint8, on the device."""
+        return self.gov.submit_batch(inst, caller, kind, arg0, arg1, addr)
 
     def handle(self, b: int) -> "OracleConsensus":
         return OracleConsensus._from_service(self, b)

@@ -54,8 +54,10 @@ class _PendingBatches:
     them for the instances it reverts (latest batch first) and gives those updates the round's status.  Many
     batches before one round are folded into one dense pre-image of the state -- ``values``, ``enabled`` and
     ``n_active`` as they were before the first pending batch -- so the memory held stays bounded by one state
-    copy (the folded batches keep only their [U] instance ids and status tensors).  A checkpoint written while
-    batches are pending stores that pre-image (svoc.state), so a round after a reload reverts to the same rows.
+    copy (the folded batches keep only their [U] instance / oracle ids and status tensors).  A revert restores
+    only the rows (and ``enabled`` flags) the pending batches touched, folded or not, so both forms leave the same
+    state: a direct write to other rows of the instance stands.  A checkpoint written while batches are pending
+    stores that pre-image (svoc.state), so a round after a reload reverts to the same rows.
     """
 
     FOLD_AT = 8   # pending batches kept as saved rows before they are folded into the dense pre-image
@@ -65,6 +67,7 @@ class _PendingBatches:
         self.entries = []      # (inst, oracle, st, saved, saved_en), batch order
         self.dense = None      # (values, enabled, n_active) before the first folded batch
         self.folded_st = []    # (inst, st) of the folded batches
+        self.rows = None       # [B, N] bool: the rows the folded batches touched (restored on a revert)
 
     def __bool__(self) -> bool:
         return bool(self.entries) or self.dense is not None
@@ -88,8 +91,18 @@ class _PendingBatches:
             for inst, oracle, st, saved, saved_en in reversed(self.entries):
                 e._ops.restore_updates(pv, pe, pn, inst, oracle, st.clone(), saved, saved_en, revert_all, every)
             self.dense = (pv, pe, pn)
+        self._mark(self.entries)
         self.folded_st += [(inst, st) for inst, _, st, _, _ in self.entries]
         self.entries = []
+
+    def _mark(self, entries) -> None:
+        e = self.e
+        if self.rows is None:
+            self.rows = torch.zeros(e.B, e.N, dtype=torch.bool, device=e.device)
+        for inst, oracle, *_ in entries:
+            ok = (inst >= 0) & (inst < e.B) & (oracle >= 0) & (oracle < e.N)
+            ic, oc = inst.clamp(0, e.B - 1), oracle.clamp(0, e.N - 1)
+            self.rows[ic, oc] = self.rows[ic, oc] | ok
 
     def restore(self, status: torch.Tensor, active: torch.Tensor) -> None:
         """Roll back the pending batches of the instances whose round ran (``active``) and reverted."""
@@ -102,14 +115,17 @@ class _PendingBatches:
         else:
             rev = (active != 0) & (status != int(Status.OK))
             pv, pe, pn = self.dense
-            e.values.copy_(torch.where(rev[:, None, None], pv, e.values))
-            e.enabled.copy_(torch.where(rev[:, None], pe, e.enabled))
+            self._mark(self.entries)
+            # only the rows the pending batches touched go back to the pre-image (the unfolded path's rows)
+            m = rev[:, None] & self.rows
+            e.values.copy_(torch.where(m[:, :, None], pv, e.values))
+            e.enabled.copy_(torch.where(m, pe, e.enabled))
             e.n_active.copy_(torch.where(rev, pn, e.n_active))
             for inst, st in self.folded_st + [(x[0], x[2]) for x in self.entries]:
                 ok = (inst >= 0) & (inst < e.B)
                 ic = inst.clamp(0, e.B - 1)
                 st.copy_(torch.where((st == int(Status.OK)) & ok & rev[ic], status[ic].to(st.dtype), st))
-        self.entries, self.dense, self.folded_st = [], None, []
+        self.entries, self.dense, self.folded_st, self.rows = [], None, [], None
 
 
 class ConsensusEngine:

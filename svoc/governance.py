@@ -2,9 +2,10 @@
 
 Device state (see csrc/include/svoc/governance.hpp): admin / oracle addresses as 4 x int64 limbs,
 the A x A vote matrix column-packed into one uint64 per receiving admin, and one optional
-proposition per admin.  ``submit`` runs a list of actions with per-instance sequential semantics: it
-splits them into waves holding at most one action per instance and launches the batched kernel
-once per wave (the CPU engine processes the list in order).
+proposition per admin.  ``submit`` (a list of action tuples) and ``submit_batch`` (action tensors) run
+actions with per-instance sequential semantics: the batch is sorted stably by instance on the device
+and one launch applies each instance's run of actions in order (the CPU engine processes the list in
+order).
 
 Reference quirks kept: ``update_proposition(None)`` does not clear votes (§2.8-7); a proposal needs
 a vote call to be applied even with required_majority = 1 (§2.8-9); a majority on a None
@@ -102,33 +103,39 @@ class Governance:
                 a1[k] = 1 if act[4] else 0
             else:
                 raise ValueError(act[0])
-        status = torch.empty(K, dtype=torch.int32, device=self.device)
-        applied = torch.zeros(K, dtype=torch.uint8, device=self.device)
-        # waves: at most one action per instance per launch (GPU); CPU handles order itself
-        if self.device.type == "cpu":
-            waves = [np.arange(K)]
-        else:
-            occ = np.zeros(K, np.int64)
-            seen: Dict[int, int] = {}
-            for k in range(K):
-                occ[k] = seen.get(int(inst[k]), 0)
-                seen[int(inst[k])] = occ[k] + 1
-            waves = [np.nonzero(occ == w)[0] for w in range(int(occ.max()) + 1)] if K else []
         d = self.device
-        for sel in waves:
-            t = lambda x, dt: torch.as_tensor(x[sel], dtype=dt).to(d).contiguous()  # noqa: E731
-            st = torch.empty(len(sel), dtype=torch.int32, device=d)
-            ap = torch.zeros(len(sel), dtype=torch.uint8, device=d)
-            self._ops.governance(self.admins, self.oracle_addr, self.votes, self.prop_tag, self.prop_idx,
-                                 self.prop_addr, t(inst, torch.int64), t(caller, torch.int64),
-                                 t(kind, torch.int32), t(a0, torch.int32), t(a1, torch.int64),
-                                 t(addr, torch.int64), self.enable, self.majority, st, ap)
-            idx = torch.as_tensor(sel, device=d)
-            status[idx] = st
-            applied[idx] = ap
+        t = lambda x, dt: torch.as_tensor(x, dtype=dt).to(d)  # noqa: E731
+        status, applied = self.submit_batch(t(inst, torch.int64), t(caller, torch.int64), t(kind, torch.int32),
+                                            t(a0, torch.int32), t(a1, torch.int64), t(addr, torch.int64))
         if K and bool(applied.any()):
-            self._oracle_cache = None
             self.replacements += int(applied.sum())
+        return status, applied
+
+    def submit_batch(self, inst: torch.Tensor, caller: torch.Tensor, kind: torch.Tensor, arg0: torch.Tensor,
+                     arg1: torch.Tensor, addr: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Device path for an ordered batch of K actions (tensors, submission order; any number per instance):
+        inst [K] int64, caller [K, 4] int64 limbs, kind [K] int32 (PROPOSE / VOTE), arg0 [K] int32 (propose:
+        1 = Some / 0 = None; vote: which_admin), arg1 [K] int64 (propose: oracle index; vote: support 0/1),
+        addr [K, 4] int64 limbs (propose: new address).  Each instance's actions apply in submission order
+        (contract.cairo:661-738 transactions, serialised per contract): on the GPU the batch is sorted stably by
+        instance on the device and ONE launch applies every instance's run (no host wave split, no sync);
+        the CPU applies the list in order.  Returns (status [K] int32, applied [K] uint8), submission order."""
+        d = self.device
+        K = int(inst.numel())
+        c = lambda x, dt: x.to(d, dt).contiguous()  # noqa: E731
+        inst, caller, kind, arg0, arg1, addr = (c(inst, torch.int64), c(caller, torch.int64).reshape(K, 4),
+                                                c(kind, torch.int32), c(arg0, torch.int32), c(arg1, torch.int64),
+                                                c(addr, torch.int64).reshape(K, 4))
+        status = torch.empty(K, dtype=torch.int32, device=d)
+        applied = torch.zeros(K, dtype=torch.uint8, device=d)
+        if K == 0:
+            return status, applied
+        order = (torch.sort(inst, stable=True).indices if d.type != "cpu"
+                 else torch.arange(K, dtype=torch.int64))
+        self._ops.governance_seq(self.admins, self.oracle_addr, self.votes, self.prop_tag, self.prop_idx,
+                                 self.prop_addr, inst, caller, kind, arg0, arg1, addr, self.enable, self.majority,
+                                 order, status, applied)
+        self._oracle_cache = None
         return status, applied
 
     def submit_tensors(self, inst, caller, kind, arg0, arg1, addr):

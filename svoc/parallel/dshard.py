@@ -104,6 +104,12 @@ def run_round_sharded(engine, d_global: int, group=None, world: int = 1, defer: 
     if sh is None:
         sh = e._dshard_shadow = _Shadow(e)
     rank = dist.get_rank(group) if world > 1 else 0
+    if getattr(e, "_dshard_pending", None) is not None and getattr(e, "_dshard_pending_rows", None):
+        # a deferred transactional round still holds saved rows: its verdict and restore come before this
+        # round's pass 1 reads the rows (an instance selected again -- e.g. by touched.fill_(1) -- would
+        # otherwise compute from rows that are rolled back right after).  Without saved rows
+        # the verdict keeps riding in this round's packed buffer.
+        flush_sharded(e, group, world)
     pend = getattr(e, "_dshard_pending", None)
     e._ops.round_prologue(e.n_active, e.touched, e.N, True, e._active)
     lg = e.cfg.legacy
@@ -137,11 +143,7 @@ def run_round_sharded(engine, d_global: int, group=None, world: int = 1, defer: 
         if pend is not None:     # the previous (deferred) round: every rank's pass-2 verdict, then commit
             pst = buf[:, N:N + world].amax(1).to(e.status.dtype)
             _commit(e, sh, pend[0], pst, pend[2], pend[3])
-            rows = getattr(e, "_dshard_pending_rows", None)
-            if rows:
-                # (only reached with no batch applied since that round: apply_updates flushes a transactional
-                # engine first, so this round's pass 1 read exactly the rows the restore puts back -- none)
-                rows.restore(pst, pend[0])
+            # (no saved rows can be pending here: they were flushed before pass 1)
             e._dshard_pending_rows = None
             e._dshard_pending = pend = None
         e.status.copy_(buf[:, N + world:].amax(1).to(e.status.dtype))

@@ -57,7 +57,7 @@ def save(svc, path: str) -> None:
         e._pending.fold()
         pv, pe, pn = e._pending.dense
         secs += [("pending_pre_values", pv[:, :, :D].contiguous(), ""), ("pending_pre_enabled", pe, ""),
-                 ("pending_pre_n_active", pn, "")]
+                 ("pending_pre_n_active", pn, ""), ("pending_rows", e._pending.rows.to(torch.uint8), "")]
     svops.ops().save_state(path, json.dumps(meta), [s[0] for s in secs],
                            [s[1].detach().cpu().contiguous() for s in secs], [s[2] for s in secs])
 
@@ -118,4 +118,7 @@ def load(path: str, device="cpu"):
         pv = e.values.clone()
         pv[:, :, : e.D].copy_(t["pending_pre_values"].to(dev, e.vdtype))
         e._pending.dense = (pv, t["pending_pre_enabled"].to(dev).clone(), t["pending_pre_n_active"].to(dev).clone())
+        # (checkpoints from before the row mask: every row of a reverted instance)
+        e._pending.rows = (t["pending_rows"].to(dev).bool() if "pending_rows" in t
+                           else torch.ones(e.B, e.N, dtype=torch.bool, device=dev))
     return svc

@@ -555,11 +555,13 @@ def test_wsad_pruned_window_fallback(N):
         assert torch.equal(fast[k][took], ref[k][took]), k
 
 
-@pytest.mark.parametrize("N,D,f", [(300, 70, 30), (512, 64, 64), (1000, 33, 100), (2048, 20, 256), (4096, 8, 512)])
+@pytest.mark.parametrize("N,D,f", [(300, 70, 30), (512, 64, 64), (1000, 33, 100), (2048, 20, 256), (4096, 8, 512),
+                                   (1500, 24, 150), (3000, 12, 300)])
 def test_wsad_kernel_wide_groups(N, D, f):
     """N > 256: the column kernel's wide lane groups (8 .. 64 lanes per column, full cross-lane
     median networks, qr by LDS atomics) take the constrained rounds and equal the i128 kernel and the CPU engine
-    bit for bit."""
+    bit for bit.  N = 1500 / 3000 run the LDS-tiled groups with padding rows (N != 64 * NSEG): the domain check
+    must ignore the tile's leftover words there, or instances would leave for the i128 kernel."""
     B = 4
     v = _wsad(B, N, D, f, seed=N + D)
     fast = _run(v.to(DEV, torch.int32), f, {"SVOC_EXACT_WSAD_ONLY": "1", "SVOC_EXACT_WSAD_MIN_D": "1"})

@@ -85,6 +85,9 @@ def notes(r: dict) -> str:
         out.append(f"{c['governance_actions_per_step']} governance actions/step")
     if c.get("comments_per_step"):
         out.append(f"{c['comments_per_step']} comments/step")
+    if c.get("graph_steps"):
+        # steps per captured graph: the metrics all-reduce runs once per replay
+        out.append(f"{c['graph_steps']} steps/graph replay")
     return ", ".join(x for x in out if x)
 
 
