@@ -98,6 +98,9 @@ def _dtype_name(mode: str, storage: str, c: dict) -> str:
     return {"fp32": "fp32", "bf16": "bf16"}.get(storage, c.get("dtype", "bf16"))
 
 
+_MARK_SEQ = 0   # timed regions bracketed by marker kernels so far (--markers)
+
+
 def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None, enc_pool=None):
     """Build the engine + update source for one storage dtype, warm up, time exactly args.steps steps
     (barrier + device sync on both sides) and gather every rank's time and round outcomes."""
@@ -301,6 +304,15 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None, enc_pool
     fx0 = eng.metrics_fx.clone()   # this rank's round outcome counters before the timed steps
     if world > 1:
         dist.barrier()
+    mark = None
+    if getattr(args, "markers", False) and dev.type == "cuda":
+        # (profiling only) a one-lane marker kernel on each side of the timed steps: tools/replay_kernels.py
+        # keeps the trace's kernels between them -- the timed replay without setup, RNG or capture kernels
+        global _MARK_SEQ
+        _MARK_SEQ += 1
+        mark = torch.zeros(1, dtype=torch.int32, device=dev)
+        import svoc.ops as _svops
+        _svops.ops().bench_marker(mark, 2 * _MARK_SEQ - 1)
     sync()
     t0 = time.perf_counter()
     if graph is not None:
@@ -317,6 +329,8 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None, enc_pool
             step_metrics()
     flush()                        # (D-shard) the last round's commit: inside the timed region
     eng.pipeline_join()
+    if mark is not None:
+        _svops.ops().bench_marker(mark, 2 * _MARK_SEQ)
     sync()
     if world > 1:
         dist.barrier()
@@ -379,6 +393,8 @@ def main():
     ap.add_argument("--stream-pool", type=int, default=0,
                     help="streaming configs: distinct update batches cycled (0 = one per timed step, within 96 GB)")
     ap.add_argument("--log", default=None, help="append the result record to this JSON-lines file")
+    ap.add_argument("--markers", action="store_true",
+                    help="profiling: bracket each timed region with marker kernels (tools/replay_kernels.py)")
     ap.add_argument("--kernel-table", type=int, default=0, help="profile N extra steps (torch.profiler) "
                     "after the timed region and add the per-kernel table to the log record")
     args = ap.parse_args()

@@ -8,6 +8,7 @@
 
 extern "C" int svoc_round_prologue(const svoc::RoundBook* r, hipStream_t stream);
 extern "C" int svoc_round_epilogue(const svoc::RoundBook* r, hipStream_t stream);
+extern "C" int svoc_bench_marker(int* flag, int code, hipStream_t stream);
 
 namespace svoc {
 namespace {
@@ -94,9 +95,18 @@ void epilogue_hip(at::Tensor active, const at::Tensor& status, const at::Tensor&
   TORCH_CHECK(rc == 0, "svoc_round_epilogue failed: ", rc);
 }
 
+void bench_marker_hip(at::Tensor flag, int64_t code) {
+  TORCH_CHECK(flag.scalar_type() == at::kInt && flag.numel() >= 1, "flag: int32 [>= 1]");
+  const int rc = svoc_bench_marker(flag.data_ptr<int32_t>(), (int)code,
+                                   c10::hip::getCurrentHIPStream(flag.device().index()).stream());
+  TORCH_CHECK(rc == 0, "svoc_bench_marker failed: ", rc);
+}
+void bench_marker_cpu(at::Tensor flag, int64_t code) { flag.fill_(code); }
+
 }  // namespace
 
 void register_bookkeeping_defs(torch::Library& m) {
+  m.def("bench_marker(Tensor(a!) flag, int code) -> ()");
   m.def("round_prologue(Tensor n_active, Tensor(a!) touched, int N, bool only_touched, Tensor(b!) active) -> ()");
   m.def("round_epilogue(Tensor(a!) active, Tensor status, Tensor rel, Tensor(b!) consensus_active, "
         "Tensor(c!) touched, Tensor(d!)? acc) -> ()");
@@ -104,10 +114,12 @@ void register_bookkeeping_defs(torch::Library& m) {
 void register_bookkeeping_cpu(torch::Library& m) {
   m.impl("round_prologue", &prologue_cpu);
   m.impl("round_epilogue", &epilogue_cpu);
+  m.impl("bench_marker", &bench_marker_cpu);
 }
 void register_bookkeeping_hip(torch::Library& m) {
   m.impl("round_prologue", &prologue_hip);
   m.impl("round_epilogue", &epilogue_hip);
+  m.impl("bench_marker", &bench_marker_hip);
 }
 
 }  // namespace svoc

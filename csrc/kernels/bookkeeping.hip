@@ -111,3 +111,14 @@ extern "C" int svoc_round_epilogue(const RoundBook* r, hipStream_t stream) {
                      stream, *r);
   return (int)hipGetLastError();
 }
+
+// Timed-region marker for the profilers (bench.py --markers): a one-lane kernel whose name brackets the
+// timed steps in a rocprofv3 kernel trace (tools/replay_kernels.py keeps the kernels between the two).
+__global__ void svoc_bench_marker_kernel(int* flag, int code) {
+  if (threadIdx.x == 0) flag[0] = code;
+}
+
+extern "C" int svoc_bench_marker(int* flag, int code, hipStream_t stream) {
+  hipLaunchKernelGGL(svoc_bench_marker_kernel, dim3(1), dim3(64), 0, stream, flag, code);
+  return (int)hipGetLastError();
+}
