@@ -341,6 +341,14 @@ def measure(args, c, storage, dev, rank, world, dshard, enc_dtype=None, enc_pool
         # pruned window network (fp32, N = 256): share of slab networks whose exact check failed and reran
         # the full network (whole run, warm-up included)
         extra["pruned_net_fallback_rate"] = ns["fallbacks"] / ns["slab_networks"]
+    if mode == "exact" and dev.type == "cuda":
+        # exact rounds by kernel (whole run, warm-up included): the share handed to the i128 kernel and the share
+        # the int64 wide-column kernel took (unconstrained columns spread past 2^30 wsad); the rest ran on the
+        # column kernel
+        xr = eng.exact_routing()
+        if xr["processed"]:
+            extra["exact_i128_share"] = xr["i128"] / xr["processed"]
+            extra["exact_wide_column_share"] = xr["wide_column"] / xr["processed"]
     ok_local = float(fx[1] / fx[2]) if float(fx[2]) > 0 else 0.0
     mine = torch.tensor([t1 - t0, ok_local], dtype=torch.float64, device=dev)
     if world > 1:

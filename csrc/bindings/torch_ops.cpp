@@ -319,12 +319,13 @@ void exact_checks(const at::Tensor& values, const at::Tensor& c1, const at::Tens
 void exact_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t n_failing,
                      bool constrained, int64_t max_spread, at::Tensor c1, at::Tensor cons, at::Tensor skew,
                      at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable, at::Tensor status,
-                     bool legacy, int64_t mode, int64_t rel_dim) {
+                     bool legacy, int64_t mode, int64_t rel_dim, const c10::optional<at::Tensor>& stats) {
+  (void)stats;   // (GPU kernel routing counters; the CPU engine is one path)
   exact_checks(values, c1, cons, skew, kurt, rel, qr, reliable, status);
   TORCH_CHECK(mode >= 0 && mode <= 2, "mode: 0 (whole round), 1 / 2 (D-sharded halves)");
   if (values.scalar_type() == at::kInt) {   // int32 wsad storage: the CPU engine works on int64
     exact_round_cpu(values.to(at::kLong), active, n_failing, constrained, max_spread, c1, cons, skew, kurt, rel, qr,
-                    reliable, status, legacy, mode, rel_dim);
+                    reliable, status, legacy, mode, rel_dim, stats);
     return;
   }
   ExactBatch eb{};
@@ -351,7 +352,7 @@ void exact_round_cpu(const at::Tensor& values, const c10::optional<at::Tensor>& 
 void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& active, int64_t n_failing,
                      bool constrained, int64_t max_spread, at::Tensor c1, at::Tensor cons, at::Tensor skew,
                      at::Tensor kurt, at::Tensor rel, at::Tensor qr, at::Tensor reliable, at::Tensor status,
-                     bool legacy, int64_t mode, int64_t rel_dim) {
+                     bool legacy, int64_t mode, int64_t rel_dim, const c10::optional<at::Tensor>& stats) {
   exact_checks(values, c1, cons, skew, kurt, rel, qr, reliable, status);
   TORCH_CHECK(mode >= 0 && mode <= 2, "mode: 0 (whole round), 1 / 2 (D-sharded halves)");
   ExactParams p{};
@@ -376,6 +377,12 @@ void exact_round_hip(const at::Tensor& values, const c10::optional<at::Tensor>& 
   p.qr = qr.data_ptr<int64_t>();
   p.reliable = reliable.data_ptr<uint8_t>();
   p.status = status.data_ptr<int32_t>();
+  if (stats.has_value() && stats->defined()) {
+    // [0] += rounds the wide-column unconstrained kernel committed, [1] += rounds left to the i128 kernel
+    TORCH_CHECK(stats->scalar_type() == at::kInt && stats->numel() >= 2 && stats->device() == values.device(),
+                "stats: int32 [>= 2] on the values' device");
+    p.xstats = (unsigned int*)stats->data_ptr();
+  }
   at::Tensor work;
   if ((int64_t)p.D * kExactWsCols * 8 > 64 * 1024) {  // wide instances: per-column intermediates in HBM
     work = at::empty({(int64_t)p.B, kExactWsCols, (int64_t)p.D}, values.options().dtype(at::kLong));
@@ -421,7 +428,8 @@ TORCH_LIBRARY(svoc, m) {
   m.def(
       "exact_round(Tensor values, Tensor? active, int n_failing, bool constrained, int max_spread, "
       "Tensor(a!) c1, Tensor(b!) consensus, Tensor(c!) skew, Tensor(d!) kurt, Tensor(e!) rel, Tensor(f!) qr, "
-      "Tensor(g!) reliable, Tensor(h!) status, bool legacy=False, int mode=0, int rel_dim=0) -> ()");
+      "Tensor(g!) reliable, Tensor(h!) status, bool legacy=False, int mode=0, int rel_dim=0, "
+      "Tensor(i!)? stats=None) -> ()");
   svoc::register_extra_defs(m);
 }
 

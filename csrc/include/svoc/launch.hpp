@@ -123,6 +123,9 @@ struct ExactParams {
   int mode;
   int rel_dim;
   int win_h;                // the column kernel's window half-width (exact_win_h; the stage holds 4 + 2 win_h rows)
+  // [2] or null: += rounds committed by the wide-column unconstrained kernel (consensus_wsadx.hip), += rounds
+  // left to the i128 kernel
+  unsigned int* xstats;
 };
 
 // Window half-width of the column-parallel exact kernel's one-network path (consensus_wsad.hip): the

@@ -420,6 +420,7 @@ static int launch_exact(const ExactParams& p, hipStream_t stream) {
 using namespace svoc;
 
 extern "C" int svoc_exact_round_wsad(const ExactParams* p, hipStream_t stream);
+extern "C" int svoc_exact_round_wsadx(const ExactParams* p, hipStream_t stream);
 
 // i128 kernel over every active instance (the reference-order path; any status).  Lane group per
 // instance: the smallest of 8 / 16 / 32 lanes holding one row each (several instances per wave, e.g.
@@ -451,6 +452,10 @@ extern "C" int svoc_exact_round(const ExactParams* p, hipStream_t stream) {
     const int rc = svoc_exact_round_wsad(p, stream);
     if (rc != -2) {
       if (rc != 0 || p->skip_fallback) return rc;
+      // flagged unconstrained rounds over wide columns: the int64 column kernel first (it clears the flags of
+      // the rounds it commits; consensus_wsadx.hip), the i128 kernel for the rest
+      const int rx = svoc_exact_round_wsadx(p, stream);
+      if (rx != 0 && rx != -2) return rx;
       ExactParams q = *p;
       q.active = p->fallback;
       return exact_round_i128(&q, stream);

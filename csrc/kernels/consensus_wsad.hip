@@ -282,12 +282,12 @@ void consensus_wsad_kernel(ExactParams p) {
   constexpr int W = WAVES * P;      // columns per tile
   constexpr int NT = WAVES * 64;
   constexpr int KEEP = 64 / P;      // qr rows a lane holds after the butterfly
-  // WIDE (NSEG 8 .. 64: N up to 512 .. 4096, whole constrained rounds): full cross-lane median networks
+  // WIDE (NSEG 8 .. 64: N up to 512 .. 4096; whole rounds and the constrained D-sharded halves): full cross-lane median networks
   // (median_group_wide), the per-oracle qr summed by LDS atomics instead of the transposing butterfly (a lane
   // holds 64 rows of one column: the butterfly would leave it 64 / P row sums -- 128 VGPRs at P = 1), and
   // 64-bit / fp64 column sums (R values up to 1e6 pass 2^32)
   constexpr bool WIDE = NSEG > 4;
-  static_assert(!WIDE || (MODE == 0 && WINH == 0), "wide groups: whole rounds, two networks");
+  static_assert(!WIDE || (WINH == 0 && (MODE == 0 || CONS)), "wide groups: two networks; D-sharded halves constrained");
   constexpr int MW = NSEG > 4 ? NSEG : 4;   // 64-bit row-mask words
   constexpr int ESZ = V32 ? 4 : 8;
   // re-reads issued as 64-load batches ordered after the value they need (load_lo / after): +37% at
@@ -622,10 +622,18 @@ void consensus_wsad_kernel(ExactParams p) {
   };
   if constexpr (MODE != 2) {
     const int nfull = N == NPAD ? min(D / W, nslab) : 0;
+    // (a wave that meets a value outside the domain stops: the instance goes to the wide-column / i128 kernels
+    // anyway.  Not with the LDS tile, whose loads every wave's barriers share.)
 #pragma nounroll
-    for (int s = 0; s < nfull; ++s) pass1(std::true_type{}, s);
+    for (int s = 0; s < nfull; ++s) {
+      if (!TILE && __ballot(badv != 0u) != 0) break;
+      pass1(std::true_type{}, s);
+    }
 #pragma nounroll
-    for (int s = nfull; s < nslab; ++s) pass1(std::false_type{}, s);
+    for (int s = nfull; s < nslab; ++s) {
+      if (!TILE && __ballot(badv != 0u) != 0) break;
+      pass1(std::false_type{}, s);
+    }
   }
   if constexpr (!WIDE) {
     int base = 0;
@@ -635,9 +643,10 @@ void consensus_wsad_kernel(ExactParams p) {
     for (int k = 0; k < KEEP; ++k) qr_part[wave * NPAD + seg * 64 + base + k] = acc[k];
   }
   __syncthreads();
-  for (int t = tid; t < (WIDE ? 0 : NPAD); t += NT) {
+  // (WIDE: pass 1 summed the qr into qr_lds by LDS atomics; mode 2 reads the all-reduced qr for every width)
+  for (int t = tid; t < ((WIDE && MODE != 2) ? 0 : NPAD); t += NT) {
     uint64_t v = 0;
-    if (MODE == 2) {   // the all-reduced qr (int64; a negative total cannot come from this domain)
+    if constexpr (MODE == 2) {   // the all-reduced qr (int64; a negative total cannot come from this domain)
       const int64_t q = t < N ? p.qr[(int64_t)b * N + t] : 0;
       if (q < 0) flag = 1;
       v = (uint64_t)q;
@@ -647,8 +656,12 @@ void consensus_wsad_kernel(ExactParams p) {
     }
     qr_lds[t] = v;
   }
-  if (MODE == 1 && badv) flag = 1;
+  if (MODE != 2 && badv) flag = 1;
   __syncthreads();
+  if (MODE == 0 && flag) {   // a value outside the domain: the wide-column / i128 kernels take the round (pass 1
+    if (tid == 0) p.fallback[b] = 1;   // stopped at the wave's first such slab; no rank mask / reliabilities here)
+    return;
+  }
   if (MODE == 1) {   // first half done: c1 and the qr partials out (partials < 2^58: D <= 2^38 columns)
     if (flag) {
       if (tid == 0) p.fallback[b] = 1;
@@ -1117,7 +1130,9 @@ static int launch_wsad_c(const ExactParams& p, hipStream_t stream) {
   hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   return (int)hipGetLastError();
 }
-// N > 256: whole rounds on the wide lane groups (the binding sized the stage for win_h = 0)
+// N > 256: whole rounds on the wide lane groups (the binding sized the stage for win_h = 0), and the D-sharded
+// halves of constrained rounds (mode 1: c1 + the per-oracle qr partials of this column slice, summed by the LDS
+// atomics of pass 1; mode 2: the rank mask from the all-reduced qr, then pass 2 -- svoc.parallel.dshard)
 template <int NSEG>
 static int launch_wide(const ExactParams& p, hipStream_t stream) {
   constexpr int WAVES = 4;
@@ -1125,6 +1140,10 @@ static int launch_wide(const ExactParams& p, hipStream_t stream) {
   auto k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 0, true> : consensus_wsad_kernel<NSEG, WAVES, false, 0, true>;
   if (!p.constrained)
     k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 0, false> : consensus_wsad_kernel<NSEG, WAVES, false, 0, false>;
+  else if (p.mode == 1)
+    k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 1, true> : consensus_wsad_kernel<NSEG, WAVES, false, 1, true>;
+  else if (p.mode == 2)
+    k = p.val32 ? consensus_wsad_kernel<NSEG, WAVES, true, 2, true> : consensus_wsad_kernel<NSEG, WAVES, false, 2, true>;
   hipLaunchKernelGGL(k, dim3(p.B), dim3(WAVES * 64), 0, stream, p);
   return (int)hipGetLastError();
 }
@@ -1144,7 +1163,7 @@ extern "C" int svoc_exact_round_wsad(const ExactParams* p, hipStream_t stream) {
   // instances per wave instead (profiles/r2_exact_crossover.json: 7 x 6 140 M vs 10 M rounds/s,
   // 16 x 16 27 M vs 10 M; but 64 x 16 already 8.3 M vs 6.0 M for this kernel)
   if (p->N < 4 || p->N > 4096) return -2;
-  if (p->N > 256 && p->mode != 0) return -2;   // (wide groups: whole rounds)
+  if (p->N > 256 && p->mode != 0 && !p->constrained) return -2;   // (wide groups: D-sharded halves constrained)
   if (p->N <= 32 && p->D < p->wsad_min_d) return -2;
   if (!p->stage || !p->fallback) return -2;
   if ((int64_t)p->N * p->D * (p->val32 ? 4 : 8) >= (1ll << 31)) return -2;   // 32-bit buffer offsets

@@ -183,6 +183,9 @@ class ConsensusEngine:
         # pruned window network (fp32, N = 256): slab networks that failed the exact check and reran the
         # full network, counted by the kernel (net_stats)
         self._net_fb = torch.zeros(1, dtype=torch.int32, device=dev) if (mode == "fast" and dev.type == "cuda") else None
+        # exact rounds on the GPU: [rounds committed by the wide-column unconstrained kernel, rounds handed to the
+        # i128 kernel] (consensus_wsadx.hip; exact_routing)
+        self._xstats = torch.zeros(2, dtype=torch.int32, device=dev) if (mode == "exact" and dev.type == "cuda") else None
         self._pending = _PendingBatches(self)
         self._save_bufs: Dict[tuple, tuple] = {}
         # health counters folded in by every round's epilogue: [rel2 sum (2^-32 units fast / wsad
@@ -292,7 +295,8 @@ class ConsensusEngine:
         else:
             self._ops.exact_round(self.values, self._active, self.cfg.n_failing_oracles, self.cfg.constrained,
                                   self.cfg.max_spread_wsad, self.c1, self.consensus, self.skew, self.kurt,
-                                  self.rel, self.qr, self.reliable, self.status, self.cfg.legacy)
+                                  self.rel, self.qr, self.reliable, self.status, self.cfg.legacy,
+                                  stats=self._xstats)
         self._ops.round_epilogue(self._active, self.status, self.rel, self.consensus_active, self.touched,
                                  self.metrics_fx)
         self.rounds += 1
@@ -532,6 +536,18 @@ class ConsensusEngine:
             return {"slab_networks": 0, "fallbacks": 0}
         processed = int(self.metrics_fx[2].item())
         return {"slab_networks": processed * (self.D // 64) * 4, "fallbacks": int(self._net_fb.item())}
+
+    def exact_routing(self) -> Dict[str, int]:
+        """Exact engine on the GPU: how the rounds so far were computed -- ``processed`` rounds, of which
+        ``wide_column`` committed by the int64 wide-column kernel (unconstrained columns spread past 2^30 wsad,
+        consensus_wsadx.hip) and ``i128`` handed to the i128 kernel (out of every column kernel's domain, or
+        reverting where the wide-column kernel cannot name the status); the rest ran on the column kernel."""
+        self.pipeline_join()
+        processed = int(self.metrics_fx[2].item())
+        if self._xstats is None:
+            return {"processed": processed, "wide_column": 0, "i128": 0}
+        x = self._xstats.tolist()
+        return {"processed": processed, "wide_column": int(x[0]), "i128": int(x[1])}
 
     def metrics(self) -> torch.Tensor:
         """[sum rel2 of committed rounds, committed, processed, reverted] as float64 (device)."""

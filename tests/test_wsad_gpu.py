@@ -163,12 +163,14 @@ def test_fast_bf16_agrees_with_exact_on_shared_grid(N, D, f):
 
 
 @pytest.mark.parametrize("path", ["dispatch", "i128", "wsad_only"])
-@pytest.mark.parametrize("N,D,f", [(16, 24, 3), (64, 300, 8), (256, 70, 32)])
+@pytest.mark.parametrize("N,D,f", [(16, 24, 3), (64, 300, 8), (256, 70, 32), (512, 96, 64), (1500, 40, 150),
+                                   (4096, 16, 512)])
 def test_exact_split_modes_match_whole_round(N, D, f, path):
     """The exact kernels' D-sharded halves (mode 1: c1 + qr partials; mode 2: from the summed qr), run on
     two column slices on one GPU with the all-reduce done by hand, reproduce the whole round bit for bit:
     through the dispatcher (column-parallel kernel + i128 fallback), the i128 kernel alone, and the
-    column-parallel kernel alone (which must then take every round: clean data)."""
+    column-parallel kernel alone (which must then take every round: clean data).  N > 256: the wide lane
+    groups' halves (D-sharded exact rounds no longer fall back to the i128 kernel)."""
     B = 8
     v = _wsad(B, N, D, f, seed=N + 7 * D)
     if path != "wsad_only":
