@@ -700,31 +700,43 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     }
     float cons_v = 0.f;
     if constexpr (CONS) {
-      // removed keys + sentinels: U'[t], t < 2H, ascending keys
-      uint32_t z[64];
-#pragma unroll
-      for (int t = 0; t < 64; ++t) {
-        if (t < 2 * H) {
-          const uint32_t mreal = 0u - (uint32_t)((realm >> t) & 1);
-          const uint32_t kx = (0x80000000u & mreal) | (~mreal & (0u - (uint32_t)(((~lowm) >> t) & 1)));
-          z[t] = (cur.uw[t] & mreal) ^ kx;
-        } else {
-          z[t] = ~0u;
-        }
-      }
-      sort_oem<64>(z);
       // lower window half: position c - H + m pairs with U'[m] (lo) / U'[m - 1] (hi); upper half
       // (stored complemented, position c + H - 1 - m): U'[2H - 1 - m] (lo) / U'[2H - 2 - m] (hi)
-      uint32_t clo = ~0u, chi = ~0u;
+      auto cands = [&](const auto& z) __attribute__((always_inline)) {
+        uint32_t clo = ~0u, chi = ~0u;
 #pragma unroll
-      for (int m = 0; m < H; ++m) {
-        const uint32_t wl = cur.wl[m], wu = cur.wu[m];
-        clo = kmin(clo, winf_cand(wl, z[m]));
-        if (m) chi = kmin(chi, winf_cand(wl, z[m - 1]));
-        clo = kmin(clo, winf_cand(wu, z[2 * H - 1 - m]));
-        chi = kmin(chi, winf_cand(wu, z[2 * H - 2 - m]));
+        for (int m = 0; m < H; ++m) {
+          const uint32_t wl = cur.wl[m], wu = cur.wu[m];
+          clo = kmin(clo, winf_cand(wl, z(m)));
+          if (m) chi = kmin(chi, winf_cand(wl, z(m - 1)));
+          clo = kmin(clo, winf_cand(wu, z(2 * H - 1 - m)));
+          chi = kmin(chi, winf_cand(wu, z(2 * H - 2 - m)));
+        }
+        cons_v = 0.5f * (fkey_val<true>(clo) + fkey_val<true>(chi));
+      };
+      constexpr int NF = H == 17 ? 32 : 8;   // f at the sentinel-free shape (c3: N = 256, f = 32; N = 64, f = 8)
+      if (s0 == 0 && fl == NF) {   // (uniform) U' = the f sorted removed keys, then +inf: an NF-key network
+        uint32_t z[NF];
+#pragma unroll
+        for (int t = 0; t < NF; ++t) z[t] = cur.uw[t] ^ 0x80000000u;
+        sort_oem<NF>(z);
+        cands([&](int t) __attribute__((always_inline)) { return t < NF ? z[t < NF ? t : 0] : ~0u; });
+      } else {
+        // removed keys + sentinels: U'[t], t < 2H, ascending keys
+        uint32_t z[64];
+#pragma unroll
+        for (int t = 0; t < 64; ++t) {
+          if (t < 2 * H) {
+            const uint32_t mreal = 0u - (uint32_t)((realm >> t) & 1);
+            const uint32_t kx = (0x80000000u & mreal) | (~mreal & (0u - (uint32_t)(((~lowm) >> t) & 1)));
+            z[t] = (cur.uw[t] & mreal) ^ kx;
+          } else {
+            z[t] = ~0u;
+          }
+        }
+        sort_oem<64>(z);
+        cands([&](int t) __attribute__((always_inline)) { return z[t]; });
       }
-      cons_v = 0.5f * (fkey_val<true>(clo) + fkey_val<true>(chi));
     }
     // reliable rows' power sums = all-row sums (phase A) - removed rows' sums
     const double a1 = (double)u2f(cur.am[0]), a2 = (double)u2f(cur.am[1]);

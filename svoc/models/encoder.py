@@ -90,7 +90,7 @@ class Layer(nn.Module):
             return _add_ln(x, _emul_linear(o.split3(h, True), self.fc2), self.ln2)   # (split3 applies the GELU)
         a = o.attention_varlen(self.qkv(x), plan.cu, plan.max_len, self.heads)
         x = _add_ln(x, self.out(a), self.ln1)
-        return _add_ln(x, self.fc2(_linear_gelu(x, self.fc1)), self.ln2)
+        return _add_ln(x, _ffn(x, self.fc1, self.fc2), self.ln2)
 
 
 @dataclasses.dataclass
@@ -124,6 +124,27 @@ def _linear_gelu(x: torch.Tensor, fc: nn.Linear) -> torch.Tensor:
             y = torch.ops.aten.gelu_(torch.addmm(fc.bias, x2, fc.weight.t()))
         return y.view(*x.shape[:-1], -1)
     return F.gelu(fc(x))
+
+
+# The FFN in row chunks on the GPU (SVOC_FFN_CHUNK rows; default: 32768 rows at fp32, whole at bf16): with a
+# chunk's [rows, 3072] FC1 activation small enough to stay in the 256 MB Infinity Cache, the erf GELU pass and
+# FC2's read of it are served from there instead of HBM.  Same-box A/B (tools/ab_ffn_chunk.sh, 2 reps): fp32
+# c4 295.5 -> 302.3 windows/s; bf16 1,888-1,895 whole vs 1,846-1,886 chunked (the smaller GEMMs lose more than the
+# GELU pass saves), so bf16 stays whole.
+FFN_CHUNK = os.environ.get("SVOC_FFN_CHUNK")
+
+
+def _ffn(x: torch.Tensor, fc1: nn.Linear, fc2: nn.Linear) -> torch.Tensor:
+    """fc2(gelu(fc1(x))) over [T, H] tokens, in row chunks on the GPU (the same GEMMs per row)."""
+    T = x.shape[0]
+    chunk = int(FFN_CHUNK) if FFN_CHUNK is not None else (32768 if x.dtype == torch.float32 else 0)
+    if not (x.is_cuda and chunk > 0 and T > chunk):
+        return fc2(_linear_gelu(x, fc1))
+    y = torch.empty(T, fc2.weight.shape[0], dtype=x.dtype, device=x.device)
+    for r0 in range(0, T, chunk):
+        r1 = min(T, r0 + chunk)
+        torch.addmm(fc2.bias, _linear_gelu(x[r0:r1], fc1), fc2.weight.t(), out=y[r0:r1])
+    return y
 
 
 # fp32 weights on the GPU: SVOC_FP32_GEMM=bf16x6 runs the four per-layer linears as fp32 GEMMs emulated on
