@@ -31,6 +31,7 @@ run c5_exact 300 --config-file configs/c5_exact_rounds.yaml --steps 20 --warmup 
 run c3_exact 300 --config-file configs/c3_exact_rounds.yaml --steps 10 --warmup 2 &&
 run c2_exact_uncons 300 --config-file configs/c2_exact_unconstrained.yaml --steps 10 --warmup 2 &&
 run c2_exact_uncons_prices 300 --config-file configs/c2_exact_unconstrained_prices.yaml --steps 10 --warmup 2 &&
+run c2_exact_uncons_wide 300 --config-file configs/c2_exact_unconstrained_wide.yaml --steps 10 --warmup 2 &&
 run c5_exact_stream 300 --config-file configs/c5_exact_stream.yaml --steps 20 --warmup 2 &&
 true || exit 1
 fi
@@ -40,14 +41,9 @@ run wide2048 300 --config-file configs/wide2048.yaml --steps 5 --warmup 1 &&
 run wide2048_fp32 300 --config-file configs/wide2048.yaml --storage fp32 --steps 5 --warmup 1 &&
 run wide512_exact 300 --config-file configs/wide512_exact.yaml --steps 3 --warmup 1 &&
 run wide4096_exact 300 --config-file configs/wide4096_exact.yaml --steps 3 --warmup 1 &&
+run wide4096_exact_dshard 300 --config-file configs/wide4096_exact.yaml --dshard --steps 3 --warmup 1 &&
 run c1 300 --config c1 --steps 50 --warmup 3 || exit 1
-for spec in "c3:--storage fp32" "c2:--storage bf16" "c4:"; do   # one storage per trace (no alt run)
-  cfg=${spec%%:*}; extra=${spec#*:}
-  echo "=== rocprof $cfg ($(date +%T))"
-  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-      -d $R/gpurun_out/prof_$cfg -o run -- python3 $R/bench.py --config $cfg --steps 6 --warmup 1 --graph 0 $extra \
-      > $R/gpurun_out/prof_$cfg.log 2>&1) || exit 1
-done
+# (kernel tables of the timed replay only: tools/gpu_replay_profiles.sh)
 # last: 64 exact transactions per instance per step at the YAML batch (1024 instances)
 run c3_exact_stream 150 --config-file configs/c3_exact_stream.yaml --steps 2 --warmup 1 &&
 run c3_exact_stream_indep 150 --config-file configs/c3_exact_stream_indep.yaml --steps 2 --warmup 1 || exit 1

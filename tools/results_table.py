@@ -37,6 +37,8 @@ ROWS = [
      "0.61/s exact Python emulator (constrained)"),
     ("c2_exact_uncons_prices", "c2 shape, exact UNCONSTRAINED rounds over price-like columns (60,000 ± 200 units, "
      "int64 wsad ~6e10)", "0.61/s exact Python emulator (constrained)"),
+    ("c2_exact_uncons_wide", "c2 shape, exact UNCONSTRAINED rounds over WIDE price columns (60,000 ± 20,000 units: "
+     "the int64 wide-column kernel)", "0.61/s exact Python emulator (constrained)"),
     ("c5_exact", "c5 shape (7 × 6), exact wsad, 1M instances", "939/s exact Python emulator"),
     ("c5_exact_stream", "c5 shape, exact transactional update stream (store + round + revert per update)",
      "939/s exact Python emulator"),
@@ -50,6 +52,7 @@ ROWS = [
     ("wide2048_fp32", "2048 × 512, fast mode over fp32 storage", "—"),
     ("wide512_exact", "512 × 2048, exact wsad rounds (column kernel, 8 lanes per column), 1024 instances", "—"),
     ("wide4096_exact", "4096 oracles × 64 dims, exact wsad rounds (N > 1024), 1024 instances", "—"),
+    ("wide4096_exact_dshard", "4096 × 64 exact, D-sharded round (mode 1 + mode 2 halves) at world 1", "—"),
 ]
 
 
