@@ -37,15 +37,21 @@ struct SlabDma {
     vlane = row0 * rowb + colb;
   }
   SVOC_DEV int row_of(int k) const { return row0 + k * (RPI / NSEG); }
+  // the region's LDS byte address (cast once per slab: per piece, the generic -> LDS cast's null test and a
+  // 64-bit add cost four SALU)
+  static SVOC_DEV uint32_t lds_addr(uint32_t* region) {
+    return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)region;
+  }
   // issue this wave's 16 pieces of the slab whose first word (of this wave: an fp32 column, a bf16 column
   // pair) is col0.  Inline asm: the
   // __builtin_amdgcn_raw_ptr_buffer_load_lds form crashes ROCm 7.2's instruction selection in this
   // kernel; M0 is saved and restored around the piece (the compiler reserves it).
   SVOC_DEV void issue(const BufDesc& rs, uint32_t* region, int rowb, int col0) const {
     const int vo = vlane + col0 * 4;
+    const uint32_t lds0 = lds_addr(region);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(region + k * 256);
+      const uint32_t lds = lds0 + k * 1024u;
       int keep;
       asm volatile(
           "s_mov_b32 %0, m0\n\t"
@@ -59,18 +65,21 @@ struct SlabDma {
     }
   }
   // The same slab, with per-piece row sources (fused transactional streaming): piece k is issued twice
-  // under complementary exec masks -- the lanes whose row comes from the update batch (bit k of
-  // `from_batch`) read byte offset off_b(k) of rb, the others off_s(k) of the state rs.  The masks are
-  // switched inside the asm (exec restored before it ends), so the compiler sees no divergent control
-  // flow around the loads (which cost the kernel ~27 spilled VGPRs when written as if / else).
-  template <class OffS, class OffB>
-  SVOC_DEV void issue_mapped(const BufDesc& rs, const BufDesc& rb, uint32_t* region, OffS off_s, OffB off_b,
-                             uint32_t from_batch) const {
+  // under complementary exec masks -- the lanes whose row comes from the update batch (sel(k) != 0) read
+  // byte offset off_b(k) of rb, the others the state rows exactly as issue() does (one voffset for the
+  // slab, the piece's row step in soffset: no per-piece VALU).  The masks are switched inside the asm (exec
+  // restored before it ends), so the compiler sees no divergent control flow around the loads (which cost
+  // the kernel ~27 spilled VGPRs when written as if / else).
+  template <class Sel, class OffB>
+  SVOC_DEV void issue_mapped(const BufDesc& rs, const BufDesc& rb, uint32_t* region, int rowb, int col0, Sel sel,
+                             OffB off_b) const {
+    const int vo = vlane + col0 * 4;
+    const uint32_t lds0 = lds_addr(region);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-      const uint32_t lds = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)(region + k * 256);
-      const int vs = off_s(k), vb = off_b(k);
-      const uint32_t fb = (from_batch >> k) & 1u;
+      const uint32_t lds = lds0 + k * 1024u;
+      const uint32_t fb = sel(k);
+      const int vb = off_b(k, fb);
       int keep;
       uint64_t sx;
       // (the exec masks come from a compare inside the asm: ballots outside it were scheduled early and
@@ -83,14 +92,14 @@ struct SlabDma {
           "s_nop 4\n\t"
           "s_andn2_b64 exec, %1, vcc\n\t"
           "s_nop 0\n\t"
-          "buffer_load_dwordx4 %2, %5, 0 offen lds\n\t"
+          "buffer_load_dwordx4 %2, %5, %8 offen lds\n\t"
           "s_and_b64 exec, %1, vcc\n\t"
           "s_nop 0\n\t"
           "buffer_load_dwordx4 %3, %6, 0 offen lds\n\t"
           "s_mov_b64 exec, %1\n\t"
           "s_mov_b32 m0, %0"
           : "=&s"(keep), "=&s"(sx)
-          : "v"(vs), "v"(vb), "v"(fb), "s"(rs.w), "s"(rb.w), "s"(lds)
+          : "v"(vo), "v"(vb), "v"(fb), "s"(rs.w), "s"(rb.w), "s"(lds), "s"(k * (RPI / NSEG) * rowb)
           : "vcc", "memory");
     }
   }

@@ -301,24 +301,24 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
   };
   auto issue_slab = [&](int s) __attribute__((always_inline)) {
     if constexpr (FUSED) {
-      const int cb = (s * W + wave * P) * 4 + dma.colb;
       // (opaque per slab: the masks and offsets derived from the map are loop-invariant, and hoisted out of
-      // the slab loop they take 32+ SGPRs for the whole phase -- spills)
+      // the slab loop they take 32+ SGPRs / VGPRs for the whole phase -- spills)
       uint32_t pm[4] = {pmap[0], pmap[1], pmap[2], pmap[3]};
       asm volatile("" : "+v"(pm[0]), "+v"(pm[1]), "+v"(pm[2]), "+v"(pm[3]));
       int rowb_o = rowb, d4 = D * 4;
       asm volatile("" : "+s"(rowb_o), "+s"(d4));
       uint32_t* reg_o = region;
       asm volatile("" : "+s"(reg_o));
-      uint32_t pfrom = 0u;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) pfrom |= (((pm[k / 4] >> (8 * (k % 4))) & 0xffu) ? 1u : 0u) << k;
-      // (24-bit multiplies: a 32-bit integer product is a quarter-rate v_mad_u64_u32 here, 32 per slab; the
-      // dispatcher keeps rows and D * 4 below 2^24 bytes on this path.  A state piece's batch offset -- slot
-      // byte 0 -- wraps below zero and is never used: exec-masked)
+      // batch piece: slot byte u + 1 of the map -> byte offset u * D * 4 + the lane's column offset.  (24-bit
+      // multiplies: a 32-bit integer product is a quarter-rate v_mad_u64_u32 here; the dispatcher keeps rows
+      // and D * 4 below 2^24 bytes on this path.  A state piece's batch offset wraps below zero and is never
+      // used: exec-masked.)  Per piece: the byte extract, the multiply-add and the mask compare.
+      int cbm = (s * W + wave * P) * 4 + dma.colb - d4;
+      asm volatile("" : "+v"(cbm));   // (one v_mad_u32_u24 per piece, not a multiply and two adds)
       dma.issue_mapped(
-          rsd, rbd, reg_o, [&](int k) { return (int)__umul24((unsigned)dma.row_of(k), (unsigned)rowb_o) + cb; },
-          [&](int k) { return (int)__umul24((pm[k / 4] >> (8 * (k % 4))) & 0xffu, (unsigned)d4) - d4 + cb; }, pfrom);
+          rsd, rbd, reg_o, rowb_o, s * W + wave * P,
+          [&](int k) { return (pm[k / 4] >> (8 * (k % 4))) & 0xffu; },
+          [&](int, uint32_t fb) { return (int)__umul24(fb, (unsigned)d4) + cbm; });
     } else {
       dma.issue(rsd, region, rowb, s * W + wave * P);
     }
