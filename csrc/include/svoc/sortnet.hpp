@@ -585,10 +585,11 @@ SVOC_DEV void bitonic_top_n(const K (&r)[L], K (&out)[H]) {
 // window_group<4, P, 17> on the middle 32 keys of every lane + the verification (see above).  r: the
 // lane's 64 keys XOR group_polarity<4>(seg) (consumed).  Outputs as window_group; `ok` is the same in the
 // four lanes of a group (K = u16x2: both columns of the pair must pass).
+// (window_group_pruned_sorted: the same from r already sorted in-lane -- a caller that also wants the lane's
+// extremes r[0] / r[63] reads them in between)
 template <int P, int H, class K>
-SVOC_DEV void window_group_pruned(K (&r)[64], int seg, int lane, K (&w)[H], K& lo, K& hi, bool& ok) {
+SVOC_DEV void window_group_pruned_sorted(K (&r)[64], int seg, int lane, K (&w)[H], K& lo, K& hi, bool& ok) {
   static_assert(H == 17, "pruned window: H = 17 (f <= 32 at N = 256)");
-  sort_oem<64>(r);
   const bool pol = seg == 1 || seg == 2;   // complemented lanes: stored ascending = true descending
   // the set-aside keys' extremes in true keys: highest of the low side, lowest of the high side
   K dl = pol ? key_from<K>(~as_u32(r[48])) : r[15];
@@ -612,6 +613,11 @@ SVOC_DEV void window_group_pruned(K (&r)[64], int seg, int lane, K (&w)[H], K& l
   dh = kmin(dh, key_from<K>(xor_lane_u32<16>(as_u32(dh))));
   dh = kmin(dh, key_from<K>(xor_lane_u32<32>(as_u32(dh))));
   ok = as_u32(kmax(dl, wlo)) == as_u32(wlo) && as_u32(kmin(dh, whi)) == as_u32(whi);
+}
+template <int P, int H, class K>
+SVOC_DEV void window_group_pruned(K (&r)[64], int seg, int lane, K (&w)[H], K& lo, K& hi, bool& ok) {
+  sort_oem<64>(r);
+  window_group_pruned_sorted<P, H>(r, seg, lane, w, lo, hi, ok);
 }
 
 }  // namespace svoc

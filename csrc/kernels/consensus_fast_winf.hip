@@ -74,6 +74,7 @@ SVOC_DEV MomKd mom_kd(double n) {
 }
 SVOC_DEV bool moments_from_sums_d(const MomKd& K, double t1, double t2, double t3, double t4, double& dl, float& sk,
                                   float& ku) {
+#pragma clang fp contract(off)   // (as the kernels: every instantiation rounds the same way)
   dl = t1 * K.in;
   const double e2 = t2 * K.in, e3 = t3 * K.in, e4 = t4 * K.in;
   const double mu2 = e2 - dl * dl;
@@ -112,6 +113,7 @@ SVOC_DEV void qr_halve(float (&part)[64], int lane) {
 template <bool MASKW, bool MASKROWS>
 SVOC_DEV void qr_moments_regs(const RawRows& xs, int nvl, float c, uint32_t mw, f32x2 (&acc)[32],
                               f32x2& s1, f32x2& s2, f32x2& s3, f32x2& s4) {
+#pragma clang fp contract(off)   // (explicit fmas only: the fused and plain instantiations must round alike)
   // (rows 2m, 2m + 1 as one packed pair: the slab copy's ds_read2st64 lands them in adjacent registers, so
   // the pair is a v_pk operand without the v_mov that pairing rows m, m + 32 needed)
 #pragma unroll
@@ -149,12 +151,17 @@ SVOC_DEV void qr_keep(const f32x2 (&a)[32], int lane, float (&keep)[64 / P], boo
 }
 
 // window_group_pruned for N = 256 (H = 17, one window part of H keys per lane); `wk` sized by the
-// caller's instantiation (the template parameter keeps the call dependent, so other widths compile)
+// caller's instantiation (the template parameter keeps the call dependent, so other widths compile).
+// e0 / e63: the lane's smallest and largest key (the in-lane sort's ends), for the fused interval check.
 template <int P, int H, int WN>
-SVOC_DEV bool try_pruned(uint32_t (&r)[64], int seg, int lane, uint32_t (&w)[WN], uint32_t& lo, uint32_t& hi) {
+SVOC_DEV bool try_pruned(uint32_t (&r)[64], int seg, int lane, uint32_t (&w)[WN], uint32_t& lo, uint32_t& hi,
+                         uint32_t& e0, uint32_t& e63) {
   if constexpr (WN == H && H == 17) {
     bool ok;
-    window_group_pruned<P, H>(r, seg, lane, w, lo, hi, ok);
+    sort_oem<64>(r);
+    e0 = r[0];
+    e63 = r[63];
+    window_group_pruned_sorted<P, H>(r, seg, lane, w, lo, hi, ok);
     return ok;
   } else {
     return false;
@@ -169,6 +176,9 @@ SVOC_DEV bool try_pruned(uint32_t (&r)[64], int seg, int lane, uint32_t (&w)[WN]
 
 template <int NSEG, int WAVES, int H, bool CONS, int MODE, bool FUSED = false>
 __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2))) void consensus_fast_winf_kernel(FastParams p) {
+  // (no implicit fma contraction: the fused-streaming and plain instantiations compile their arithmetic in
+  // different contexts and must still round alike -- tests/test_fast_transactional.py compares them bit for bit)
+#pragma clang fp contract(off)
   constexpr int P = 64 / NSEG;          // columns per wave (phase A)
   constexpr int NPAD = 64 * NSEG;
   constexpr int W = WAVES * P;          // columns per workgroup step (phase A)
@@ -346,25 +356,28 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);      // lgkmcnt(0): the region is read, the next slab may land
     if (s + 1 < pass1_slabs) issue_slab(s + 1);
-    if (fused) {
-      // interval check of the batch rows (contract.cairo:591-593, math.cairo:298-310): the maximum raw
-      // word of the lane's rows (state rows were checked when stored) against 1.0f; past it (or -0.0
-      // somewhere) the batch rows are checked one by one and a failing slot is marked
+    // interval check of the batch rows (contract.cairo:591-593, math.cairo:298-310): the lane's rows against
+    // [+0, 1.0f] (state rows were checked when stored); past it (or -0.0 somewhere) the batch rows are checked one
+    // by one and a failing slot is marked.  On the pruned-network path the lane's extremes come from its sorted
+    // keys (after the network); elsewhere from the maximum raw word here.
+    constexpr bool IV_LATE = FUSED && FULL && CONS && NSEG == 4 && H == 17;
+    auto mark_bad_rows = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {
+        const int row = seg * 64 + i;
+        const uint32_t raw = xs.at(i);
+        if (vc && row < N && !(raw <= 0x3f800000u || raw == 0x80000000u)) {
+          int u = -1;
+          if constexpr (FUSED) u = smap[row];
+          if (u >= 0) atomicOr(&badu[u >> 5], 1u << (u & 31));
+        }
+      }
+    };
+    if (fused && !IV_LATE) {
       uint32_t mx = 0u;
 #pragma unroll
       for (int i = 0; i < 64; i += 2) mx = __builtin_elementwise_max(mx, __builtin_elementwise_max(xs.at(i), xs.at(i + 1)));
-      if (__ballot(mx > 0x3f800000u) != 0) {
-#pragma unroll
-        for (int i = 0; i < 64; ++i) {
-          const int row = seg * 64 + i;
-          const uint32_t raw = xs.at(i);
-          if (vc && row < N && !(raw <= 0x3f800000u || raw == 0x80000000u)) {
-            int u = -1;
-            if constexpr (FUSED) u = smap[row];
-            if (u >= 0) atomicOr(&badu[u >> 5], 1u << (u & 31));
-          }
-        }
-      }
+      if (__ballot(mx > 0x3f800000u) != 0) mark_bad_rows();
     }
     {
       uint32_t r[64];
@@ -390,7 +403,15 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(2)))
           if constexpr (NSEG == 4 && H == 17 && decltype(full_c2)::value) {
             // N = 256: the pruned network (middle 32 keys of every lane) + its exact check; a wave with any
             // failing column reruns the full network from the raw rows (sortnet.hpp window_group_pruned)
-            const bool ok = try_pruned<P, H>(r, seg, lane, wk, klo, khi);
+            uint32_t e0, e63;
+            const bool ok = try_pruned<P, H>(r, seg, lane, wk, klo, khi, e0, e63);
+            if constexpr (IV_LATE) {
+              // keys = (raw ^ 0x80000000) ^ pol: the lane's raw words all in [+0, 1.0f] <=> its true keys (e0 / e63
+              // XOR pol, in either order) within [0x80000000, 0xbf800000]
+              const uint32_t a = e0 ^ pol, bk = e63 ^ pol;
+              const uint32_t tmin = __builtin_elementwise_min(a, bk), tmax = __builtin_elementwise_max(a, bk);
+              if (__ballot(tmin < 0x80000000u || tmax > 0xbf800000u) != 0) mark_bad_rows();
+            }
             if (__ballot(!ok) != 0) {
               ++net_fallbacks;
               // an opaque copy of the key XOR: otherwise CSE keeps the first 64 keys alive across the

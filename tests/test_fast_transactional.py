@@ -168,6 +168,10 @@ def test_fused_streaming_matches_generic_path(storage, N, D, f, U):
     orc[2 * U + 1] = N + 5
     orc[2 * U + 3] = -1
     vals[2 * U + 3, 0] = 2.0
+    # instance 3: a negative value (rejected) and a -0.0 (inside the interval: accepted) in two update rows
+    # (the N = 256 kernel takes the rows' interval extremes from its sorted keys)
+    vals[3 * U + 1, 5] = -0.25
+    vals[3 * U + 4, 7] = -0.0
     fz.values[4, :, 3] = 0.625
     gen.values[4, :, 3] = 0.625
     vals[4 * U:5 * U, 3] = 0.625
@@ -181,6 +185,7 @@ def test_fused_streaming_matches_generic_path(storage, N, D, f, U):
     assert torch.equal(st_f, st_g), (st_f.view(B, U), st_g.view(B, U))
     assert st_f[1 * U + 2].item() == int(Status.INTERVAL_INPUT)
     assert st_f[2 * U + 1].item() == int(Status.NOT_ORACLE) and st_f[2 * U + 3].item() == int(Status.INTERVAL_INPUT)
+    assert st_f[3 * U + 1].item() == int(Status.INTERVAL_INPUT) and st_f[3 * U + 4].item() == int(Status.OK)
     assert fz.status[4].item() == int(Status.ZERO_VARIANCE)
     for k in ("status", "values", "enabled", "n_active", "consensus", "rel", "c1", "reliable", "skew", "kurt", "qr"):
         a, b_ = getattr(fz, k), getattr(gen, k)
