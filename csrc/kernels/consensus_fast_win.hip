@@ -31,6 +31,7 @@
 
 #include "svoc/bufload.hpp"
 #include "svoc/launch.hpp"
+#include "svoc/rankmask.hpp"
 #include "svoc/sortnet.hpp"
 #include "svoc/status.hpp"
 
@@ -263,7 +264,7 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   // (N = 256: rows i % 4 < 2; N <= 128: even rows; profiles/r1_stage_ab.txt)
   constexpr bool STAGE = CONS && MODE != 2;
   __shared__ uint32_t stage[STAGE ? WAVES * 32 * 64 : 1];
-  __shared__ float qr_part[WAVES * NPAD];
+  __shared__ __attribute__((aligned(16))) float qr_part[WAVES * NPAD];   // (then the rank keys: 2 NPAD words)
   __shared__ float qr_lds[NPAD];
   __shared__ uint64_t relmask[4];
   __shared__ int urow[32];      // removed rows, index order
@@ -463,6 +464,10 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
   // ------------------------------------------------------------ rank mask (contract.cairo:345-363)
   const int f = p.n_failing;
   const int R = N - f;
+  if constexpr (CONS) {
+    static_assert(WAVES >= 2, "rank keys in qr_part");
+    rank_mask_nonneg<NT, NPAD>(qr_lds, reinterpret_cast<uint64_t*>(qr_part), N, R, tid, relmask);
+  } else
   for (int base = 0; base < NPAD; base += NT) {
     const int t = base + tid;
     bool rel = false;
