@@ -116,8 +116,8 @@ def test_non_transactional_keeps_rows():
 def test_pipelined_step_restores_reverted_instances(overlap, storage, D):
     """step_pipelined (per-range update + round + rollback on side streams: the fused fp32 path, the bf16
     window kernel's in-kernel rollback) == step() (update kernel, round, restore kernel) on a batch where
-    some instances revert (eager and overlapped across steps; overlapped fp32 commits take the low-footprint
-    commit kernel, D = 1000: a row of 250 16-B chunks, the last pair of its loop partly past the row end)."""
+    some instances revert (eager and overlapped across steps; D = 1000: fp32 rows of 250 16-B chunks, not a
+    multiple of the commit kernel's 64 lanes)."""
     N, B = 64, 8
     U = N                            # every oracle of every instance publishes
     ref, pipe = _engine("cuda", storage, N=N, D=D, B=B), _engine("cuda", storage, N=N, D=D, B=B)
