@@ -686,15 +686,28 @@ void consensus_wsad_kernel(ExactParams p) {
     else
       for (int w = tid; w < MW; w += NT) relmask[w] = 0ull;   // (no reliable row: the stage checks revert)
   }
+  // constrained: qr <= D (1e6 + 1) < 2^56 and N <= 256, so (qr asc, idx desc) is the one key qr << 8 | (255 - idx):
+  // one 64-bit compare per oracle (rankmask.hpp's form for the exact sums)
+  constexpr bool KEY8 = CONS && !WIDE && NPAD <= 256;
+  __shared__ uint64_t rk_key[KEY8 ? NPAD : 1];
+  if constexpr (KEY8) {
+    for (int t = tid; t < N; t += NT) rk_key[t] = (qr_lds[t] << 8) | (uint64_t)(255 - t);
+    __syncthreads();
+  }
   for (int base = 0; base < (WIDE ? 0 : NPAD); base += NT) {
     const int t = base + tid;
     bool rel = false;
     if (t < N) {
-      const uint64_t myq = qr_lds[t];
       int rank = 0;
-      for (int j = 0; j < N; ++j) {
-        const uint64_t qj = qr_lds[j];
-        rank += (qj < myq || (qj == myq && j > t)) ? 1 : 0;   // (qr asc, idx desc)
+      if constexpr (KEY8) {
+        const uint64_t my = rk_key[t];
+        for (int j = 0; j < N; ++j) rank += rk_key[j] < my ? 1 : 0;
+      } else {
+        const uint64_t myq = qr_lds[t];
+        for (int j = 0; j < N; ++j) {
+          const uint64_t qj = qr_lds[j];
+          rank += (qj < myq || (qj == myq && j > t)) ? 1 : 0;   // (qr asc, idx desc)
+        }
       }
       rel = rank < R;
     }
