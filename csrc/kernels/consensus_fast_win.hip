@@ -647,7 +647,47 @@ __global__ __launch_bounds__(WAVES * 64) __attribute__((amdgpu_waves_per_eu(4)))
 
     uint32_t medw = 0u;   // pass-2 middle pair (true keys) of both columns: lo, hi
     uint32_t mhw = 0u;
-    if constexpr (CONS) {
+    if constexpr (CONS && H == 5) {
+      // c2's shape (N = 64, f = 8, sentinel shift 0): U' = the f sorted removed keys, then +inf -- an 8-key network
+      // instead of the 64-slot one (at H = 17 the 32-key form took the 128-VGPR kernel to scratch:
+      // profiles/r6_rank_key_ab.txt); other shapes the general form below
+      auto cands = [&](const auto& z) __attribute__((always_inline)) {
+        u16x2 clo = as_k(~0u), chi = as_k(~0u);
+#pragma unroll
+        for (int m = 0; m < H; ++m) {
+          const u16x2 wl = as_k(bload(ws, pr * 4, 2 * m * Dp * 4));
+          const u16x2 wu = ~as_k(bload(ws, (Dp + pr) * 4, 2 * m * Dp * 4));
+          clo = kmin(clo, win_cand(wl, z(m)));
+          if (m) chi = kmin(chi, win_cand(wl, z(m - 1)));
+          clo = kmin(clo, win_cand(wu, z(2 * H - 1 - m)));
+          chi = kmin(chi, win_cand(wu, z(2 * H - 2 - m)));
+        }
+        medw = key_to_pos(clo);
+        mhw = key_to_pos(chi);
+      };
+      constexpr int NF = 8;
+      if (s0 == 0 && fl == NF) {   // (uniform)
+        u16x2 z[NF];
+#pragma unroll
+        for (int t = 0; t < NF; ++t) z[t] = as_k(uw[t < NS ? t : 0] ^ 0x80008000u);
+        sort_oem<NF>(z);
+        cands([&](int t) __attribute__((always_inline)) { return t < NF ? z[t < NF ? t : 0] : as_k(~0u); });
+      } else {
+        u16x2 z[64];
+#pragma unroll
+        for (int t = 0; t < 64; ++t) {
+          if (t < 2 * H) {
+            const uint32_t mreal = 0u - (uint32_t)((realm >> t) & 1);
+            const uint32_t kx = (0x80008000u & mreal) | (~mreal & (0u - (uint32_t)(((~lowm) >> t) & 1)));
+            z[t] = as_k((uw[t] & mreal) ^ kx);
+          } else {
+            z[t] = as_k(~0u);
+          }
+        }
+        sort_oem<64>(z);
+        cands([&](int t) __attribute__((always_inline)) { return z[t]; });
+      }
+    } else if constexpr (CONS) {
       // removed keys + sentinels: U'[t], t < 2H, ascending true keys
       u16x2 z[64];
 #pragma unroll
