@@ -131,3 +131,46 @@ def test_service_batched_instances():
     assert st.count(Status.OK) == 4
     for b in range(4):
         assert svc.engine.consensus[b].tolist() == g["consensus"]
+
+
+def test_service_governance_tensor_batch_matches_list():
+    """ConsensusService.governance with a mapping of action tensors (the device path's interface; on the CPU the
+    batch applies in order) == the same actions as a list of tuples: statuses, applied flags and the final
+    oracle / vote state, with several actions per instance, non-admin callers and None propositions."""
+    import torch
+    from svoc.codec import address_to_limbs
+    from svoc.governance import PROPOSE, VOTE
+    cfg = ConsensusConfig(n_oracles=7, dimension=2, n_failing_oracles=2, constrained=True, n_admins=3)
+    rng = random.Random(5)
+    acts = []
+    for _ in range(120):
+        b = rng.randrange(4)
+        caller = rng.choice(ADMINS + [123456789])
+        if rng.random() < 0.4:
+            prop = None if rng.random() < 0.2 else (rng.randrange(-1, 8), NEW_ORACLE + rng.randrange(3))
+            acts.append(("propose", b, caller, prop))
+        else:
+            acts.append(("vote", b, caller, rng.randrange(4), rng.random() < 0.8))
+    svc_l = ConsensusService(cfg, 4, ADMINS, ORACLES, device="cpu", mode="exact")
+    svc_t = ConsensusService(cfg, 4, ADMINS, ORACLES, device="cpu", mode="exact")
+    st_l, ap_l = svc_l.governance(acts)
+    K = len(acts)
+    t = dict(inst=torch.zeros(K, dtype=torch.int64), caller=torch.zeros(K, 4, dtype=torch.int64),
+             kind=torch.zeros(K, dtype=torch.int32), arg0=torch.zeros(K, dtype=torch.int32),
+             arg1=torch.zeros(K, dtype=torch.int64), addr=torch.zeros(K, 4, dtype=torch.int64))
+    for k, a in enumerate(acts):
+        t["inst"][k] = a[1]
+        t["caller"][k] = torch.tensor(address_to_limbs(a[2]))
+        if a[0] == "propose":
+            t["kind"][k] = PROPOSE
+            if a[3] is not None:
+                t["arg0"][k], t["arg1"][k] = 1, a[3][0]
+                t["addr"][k] = torch.tensor(address_to_limbs(a[3][1]))
+        else:
+            t["kind"][k], t["arg0"][k], t["arg1"][k] = VOTE, a[3], int(a[4])
+    st_t, ap_t = svc_t.governance(t)
+    assert [Status(s) for s in st_t.tolist()] == st_l and [bool(a) for a in ap_t.tolist()] == ap_l
+    assert any(ap_l) and st_l.count(Status.OK) < K
+    for b in range(4):
+        assert svc_t.gov.vote_matrix(b) == svc_l.gov.vote_matrix(b)
+    assert torch.equal(svc_t.gov.oracle_addr, svc_l.gov.oracle_addr)
